@@ -1,0 +1,100 @@
+"""The oracle (CPU restatement, oracle/) pinned against the reference's golden vectors.
+
+These run without a GPU.  They establish that oracle/ reproduces zlib 1.2.8 deflate bit-exactly
+(G2, from the reference's vendored zlib) and the reference pipeline's .atz bytes (G1 = the
+reference's own ZT vectors, G3-G5 = cases produced by the real reference binary).
+"""
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+import _libs
+import golden_cases as G
+
+GOLD = G.GOLD
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def test_deflate_kats_full_bytes():
+    full = json.load(open(os.path.join(GOLD, "deflate_kat_text4k_w15.json")))
+    d = open(os.path.join(GOLD, "kat", "text4k.bin"), "rb").read()
+    for key, hexs in full.items():
+        c, m = map(int, key.split("/"))
+        out, hazard = _libs.ora_deflate(d, c, 15, m)
+        assert out.hex() == hexs, key
+        assert hazard == 0
+
+
+@pytest.mark.parametrize("name", ["asd", "text4k", "rand5k", "input8k"])
+def test_deflate_kats_all_params(name):
+    kat = json.load(open(os.path.join(GOLD, "deflate_kat.json")))
+    d = open(os.path.join(GOLD, "kat", name + ".bin"), "rb").read()
+    assert sha(d) == kat["inputs"][name]
+    for c in range(10):
+        for w in range(9, 16):
+            for m in range(1, 10):
+                out, _ = _libs.ora_deflate(d, c, w, m)
+                n, h = kat["results"]["%s/%d/%d/%d" % (name, c, w, m)]
+                assert (len(out), sha(out)) == (n, h), (name, c, w, m)
+
+
+def test_zt_kat_pipeline():
+    data, meta = G.zt_kat()
+    rc, atz, st = _libs.ora_precompress(data)
+    assert rc == 0
+    assert sha(atz) == meta["atz_sha256"]
+    got = [(s["offset"], s["clevel"], s["window"], s["memlevel"]) for s in st["streams"]]
+    want = [(s["offset"], s["clevel"], s["window"], s["memlevel"]) for s in meta["streams"]]
+    assert got == want
+    rc, rec = _libs.ora_reconstruct(atz)
+    assert rc == 0 and rec == data
+
+
+@pytest.mark.parametrize("case", G.cases(), ids=lambda c: c["name"])
+def test_golden_case_pipeline(case):
+    data = G.case_input(case)
+    rc, atz, st = _libs.ora_precompress(data, **G.opts_kwargs(case["opts"]))
+    assert rc == 0
+    assert sha(atz) == case["atz_sha256"], case["name"]
+    assert st["hazard"] == 0
+    rc, rec = _libs.ora_reconstruct(atz)
+    assert rc == 0 and rec == data
+
+
+def test_inflate_roundtrip_and_truncation():
+    r = random.Random(5)
+    for k in range(200):
+        d = _libs.text(r, r.randrange(0, 5000))
+        s, _ = _libs.ora_deflate(d, r.randrange(0, 10), r.randrange(9, 16), r.randrange(1, 10))
+        st, c, p = _libs.ora_inflate(s + b"junk")
+        assert (st, c, p) == (0, len(s), len(d))
+        cut = r.randrange(1, len(s))
+        st, c, p = _libs.ora_inflate(s[:cut])
+        assert st in (1, 2)
+        if st == 2:
+            assert c == cut
+
+
+@pytest.mark.skipif(not _libs.have_zref(), reason="reference build (oracle/_ref) absent")
+def test_live_reference_deflate_inflate_sample():
+    r = random.Random(11)
+    for k in range(150):
+        d = _libs.text(r, r.randrange(1, 20000))
+        c, w, m = r.randrange(0, 10), r.randrange(9, 16), r.randrange(1, 10)
+        a, _ = _libs.ora_deflate(d, c, w, m)
+        assert a == _libs.zref_deflate(d, c, w, m), (c, w, m)
+        s = bytearray(a)
+        s[r.randrange(2, len(s))] ^= 1 << r.randrange(8)
+        s = bytes(s[:r.randrange(2, len(s) + 1)])
+        st, cons, prod = _libs.ora_inflate(s)
+        rf, tf, rl, ti, to, ai = _libs.zref_inflate_scan(s)
+        assert cons == ti and tf == ti
+        assert (st == 0) == (rl == 1)
+        if st == 0:
+            assert prod == to
