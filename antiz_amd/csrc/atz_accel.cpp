@@ -1,0 +1,1275 @@
+// atz_accel.cpp -- libatz_accel.so: host orchestration + C ABI (include/atz_accel.h) for the
+// MI355X zlib-stream precompressor.  Unity build: the HIP kernels are compiled into this TU.
+//
+// Phase 1 (scan)  : k_find_headers over the whole file in HBM, one k_inflate launch over every
+//                   candidate of every chunk, the reference's greedy per-chunk selection
+//                   (ZBuffSearcher::operator(), main.cpp:205-246) replayed on the host from the
+//                   results, boundary continuations (main.cpp:207-217) batched speculatively,
+//                   then one k_inflate launch that writes every recorded stream's inflated bytes
+//                   into a packed HBM buffer (the reference re-inflates each stream in Phase 3
+//                   and again in Phase 4; here they stay resident).
+// Phase 3 (sweep) : rounds; round r evaluates the r-th trial of every stream that has not stopped
+//                   (one wavefront per trial, k_trial_{stored,fast,slow}), so the reference's
+//                   ordered first-improving-within-tolerance rule (main.cpp:685-700, 746-754) is
+//                   applied exactly, per stream, between rounds.  Chain links per (stream,memLevel)
+//                   are built on demand by k_chains and cached in HBM.
+// Phase 4 (write) : ATZ1 (main.cpp:764-834) assembled in HBM by k_gather from the resident
+//                   inflated payloads and the original file.
+#include "k_inflate.hip"
+#include "k_deflate.hip"
+
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/atz_accel.h"
+
+using namespace atz;
+
+namespace {
+
+struct Seg {           // k_gather segment
+  uint32_t src;        // 0 meta, 1 inflated, 2 file
+  uint32_t pad;
+  uint64_t src_off, dst_off, len;
+};
+
+__global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ meta, const uint8_t* __restrict__ infl,
+                                               const uint8_t* __restrict__ file, uint8_t* __restrict__ dst,
+                                               const Seg* __restrict__ segs, uint32_t nseg) {
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint32_t s = blockIdx.x * 4 + wave; s < nseg; s += gridDim.x * 4) {
+    const Seg g = segs[s];
+    const uint8_t* src = (g.src == 0 ? meta : g.src == 1 ? infl : file) + g.src_off;
+    uint8_t* d = dst + g.dst_off;
+    for (uint64_t k = lane; k < g.len; k += 64) d[k] = src[k];
+  }
+}
+
+// Mismatch list of a winning trial (main.cpp:699-714): positions i < min(L, C_s) with out[i] != orig[i],
+// then L..C_s-1 if the recompressed stream is shorter.
+struct DiffJob {
+  uint64_t out_off, out_len, orig_off, comp_len, dst;  // dst: index into pos/val arrays
+  uint64_t cap;                                       // entries reserved
+};
+__global__ __launch_bounds__(64) void k_diffs(const uint8_t* __restrict__ out, const uint8_t* __restrict__ file,
+                                             const DiffJob* __restrict__ jobs, uint32_t* __restrict__ pos,
+                                             uint8_t* __restrict__ val, uint64_t* __restrict__ count, uint32_t n) {
+  const uint32_t j = blockIdx.x;
+  if (j >= n) return;
+  const int lane = threadIdx.x;
+  const DiffJob d = jobs[j];
+  const uint8_t* o = out + d.out_off;
+  const uint8_t* f = file + d.orig_off;
+  uint64_t sm = d.out_len < d.comp_len ? d.out_len : d.comp_len;
+  uint64_t k = 0;
+  uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (uint64_t b = 0; b < d.comp_len; b += 64) {
+    uint64_t i = b + lane;
+    bool m = false;
+    uint8_t v = 0;
+    if (i < d.comp_len) {
+      v = f[i];
+      m = i < sm ? o[i] != v : true;
+    }
+    uint64_t bal = __ballot(m);
+    if (m) {
+      uint64_t at = k + __popcll(bal & lt);
+      if (at < d.cap) { pos[d.dst + at] = (uint32_t)i; val[d.dst + at] = v; }
+    }
+    k += __popcll(bal);
+  }
+  if (lane == 0) count[j] = k;
+}
+
+#define HIPCHK(x)                                                     \
+  do {                                                                \
+    hipError_t e_ = (x);                                              \
+    if (e_ != hipSuccess) {                                           \
+      std::fprintf(stderr, "atz: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      return ATZ_E_HIP;                                               \
+    }                                                                 \
+  } while (0)
+
+struct DBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  int reserve(size_t need) {
+    if (need <= n) return 0;
+    if (p) hipFree(p);
+    p = nullptr;
+    n = 0;
+    size_t cap = need + need / 4 + 65536;
+    if (hipMalloc(&p, cap) != hipSuccess) return ATZ_E_NOMEM;
+    n = cap;
+    return 0;
+  }
+  void release() { if (p) hipFree(p); p = nullptr; n = 0; }
+  template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct Rec {
+  uint64_t offset, comp_len, infl_len;
+  int type;
+  uint32_t flags;
+};
+
+struct StreamState {
+  // sweep
+  std::vector<uint32_t> list;     // packed (c<<16)|(w<<8)|m
+  uint32_t idx = 0;
+  uint32_t phase = 0;             // 0 = list A, 1 = list B, 2 = done
+  uint8_t c = 9, w = 15, m = 9;   // streamOffset ctor defaults (ATZData.h:51-53)
+  uint64_t ident = 0;
+  int64_t first_diff = -1;
+  std::vector<uint32_t> rawdiff;  // raw positions of the current best
+  std::vector<uint8_t> diffval;
+  uint32_t trials = 0;
+  bool recomp = false;
+};
+
+uint32_t pk(int c, int w, int m) { return ((uint32_t)c << 16) | ((uint32_t)w << 8) | (uint32_t)m; }
+
+void prange(std::vector<uint32_t>& l, int cmin, int cmax, int wmin, int wmax, int mmin, int mmax) {
+  for (int w = wmax; w >= wmin; w--)
+    for (int m = mmax; m >= mmin; m--)
+      for (int c = cmax; c >= cmin; c--) l.push_back(pk(c, w, m));
+}
+// tryParamsFastest/Fast/Default/Best (main.cpp:487-560)
+void list_a(std::vector<uint32_t>& l, int type) {
+  int w = 10 + type / 4;
+  switch (type % 4) {
+    case 0: l.push_back(pk(0, w, 8)); l.push_back(pk(1, w, 8)); l.push_back(pk(1, w, 9));
+            prange(l, 1, 1, w, w, 1, 7); prange(l, 2, 9, w, w, 1, 9); break;
+    case 1: prange(l, 2, 5, w, w, 8, 8); prange(l, 2, 5, w, w, 1, 7); prange(l, 2, 5, w, w, 9, 9);
+            prange(l, 1, 1, w, w, 1, 9); prange(l, 6, 9, w, w, 1, 9); break;
+    case 2: l.push_back(pk(6, w, 8)); l.push_back(pk(6, w, 9)); prange(l, 6, 6, w, w, 1, 7);
+            prange(l, 1, 5, w, w, 1, 9); prange(l, 7, 9, w, w, 1, 9); break;
+    default: prange(l, 7, 9, w, w, 8, 8); prange(l, 7, 9, w, w, 1, 7); prange(l, 7, 9, w, w, 9, 9);
+             prange(l, 1, 6, w, w, 1, 9); break;
+  }
+}
+// brute-window continuation (main.cpp:590-601)
+void list_b(std::vector<uint32_t>& l, int type) {
+  int w = 10 + type / 4;
+  if (w == 10) prange(l, 1, 9, 11, 15, 1, 9);
+  else if (w == 15) prange(l, 1, 9, 10, 14, 1, 9);
+  else { prange(l, 1, 9, 10, w - 1, 1, 9); prange(l, 1, 9, w + 1, 15, 1, 9); }
+}
+
+uint64_t bound(uint64_t n, int w, int m) {  // deflateBound (Z/deflate.c:566-621), zlib wrapper
+  uint64_t complen = n + ((n + 7) >> 3) + ((n + 63) >> 6) + 5;
+  if (w != 15 || m + 7 != 15) return complen + 6;
+  return n + (n >> 12) + (n >> 14) + (n >> 25) + 13 - 6 + 6;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+// trees.c tr_static_init (Z/trees.c:232-330)
+void make_tables(DeflTables& T) {
+  static const int xlb[29] = {0,0,0,0,0,0,0,0,1,1,1,1,2,2,2,2,3,3,3,3,4,4,4,4,5,5,5,5,0};
+  static const int xdb[30] = {0,0,0,0,1,1,2,2,3,3,4,4,5,5,6,6,7,7,8,8,9,9,10,10,11,11,12,12,13,13};
+  std::memset(&T, 0, sizeof(T));
+  int len = 0, code;
+  for (code = 0; code < 28; code++) {
+    T.lbase[code] = (uint16_t)len;
+    for (int k = 0; k < (1 << xlb[code]); k++) T.lcode[len++] = (uint8_t)code;
+  }
+  T.lbase[28] = 0;
+  T.lcode[255] = 28;
+  int dist = 0;
+  for (code = 0; code < 16; code++) {
+    T.dbase[code] = (uint16_t)dist;
+    for (int k = 0; k < (1 << xdb[code]); k++) T.dcode[dist++] = (uint8_t)code;
+  }
+  dist >>= 7;
+  for (; code < 30; code++) {
+    T.dbase[code] = (uint16_t)(dist << 7);
+    for (int k = 0; k < (1 << (xdb[code] - 7)); k++) T.dcode[256 + dist++] = (uint8_t)code;
+  }
+  uint16_t blc[16] = {0};
+  for (int n = 0; n < 288; n++) {
+    T.st_llen[n] = n < 144 ? 8 : n < 256 ? 9 : n < 280 ? 7 : 8;
+    blc[T.st_llen[n]]++;
+  }
+  uint16_t next[16];
+  uint32_t c = 0;
+  for (int b = 1; b <= 15; b++) { c = (c + blc[b - 1]) << 1; next[b] = (uint16_t)c; }
+  auto rev = [](uint32_t v, int l) { uint32_t r = 0; for (int i = 0; i < l; i++) { r = (r << 1) | (v & 1); v >>= 1; } return r; };
+  for (int n = 0; n < 288; n++) T.st_lcode[n] = (uint16_t)rev(next[T.st_llen[n]]++, T.st_llen[n]);
+  for (int n = 0; n < 30; n++) { T.st_dlen[n] = 5; T.st_dcode[n] = (uint16_t)rev((uint32_t)n, 5); }
+}
+
+int header_type_host(unsigned b0, unsigned b1) {
+  static const uint16_t H[24] = {0x2815, 0x2853, 0x2891, 0x28cf, 0x3811, 0x384f, 0x388d, 0x38cb,
+                                 0x480d, 0x484b, 0x4889, 0x48c7, 0x5809, 0x5847, 0x5885, 0x58c3,
+                                 0x6805, 0x6843, 0x6881, 0x68de, 0x7801, 0x785e, 0x789c, 0x78da};
+  unsigned h = (b0 << 8) | b1;
+  for (int t = 0; t < 24; t++) if (H[t] == h) return t;
+  return -1;
+}
+
+}  // namespace
+
+struct KTimer {   // HIP events bracketing kernel launches on the library stream
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  std::vector<int> kind;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t get() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e; (void)hipEventCreate(&e); return e;
+  }
+};
+
+struct atz_ctx {
+  KTimer kt;
+  atz_opts_t o{};
+  int dev = 0;
+  hipStream_t st = nullptr;
+  DBuf d_file, d_pos, d_cnt, d_jobs, d_res, d_virt, d_infl, d_chains, d_heads, d_streams, d_trials,
+      d_tres, d_out, d_syms, d_adler, d_meta, d_segs, d_atz, d_diffjobs, d_diffpos, d_diffval, d_diffcnt,
+      d_cjobs, d_tmp;
+  // last scan
+  std::vector<Rec> recs;
+  std::vector<uint64_t> infl_off;   // per record offset in d_infl
+  std::vector<uint32_t> adler;
+  const uint8_t* hfile = nullptr;
+  uint64_t flen = 0;
+  bool file_on_device = false;      // d_file holds the current file
+  const uint8_t* dev_file = nullptr;
+  atz_stats_t stats{};
+  // chains cache: per record and memlevel
+  std::vector<std::array<uint64_t, 10>> chain_off;
+  uint64_t chain_used = 0;
+};
+
+// kind: 0 trial, 1 inflate, 2 chains, 3 other
+static void kbeg(atz_ctx* c, int kind) {
+  hipEvent_t a = c->kt.get(), b = c->kt.get();
+  (void)hipEventRecord(a, c->st);
+  c->kt.pending.push_back({a, b});
+  c->kt.kind.push_back(kind);
+}
+static void kend(atz_ctx* c) { (void)hipEventRecord(c->kt.pending.back().second, c->st); }
+// after a stream synchronisation: fold elapsed times into the stats
+static void kcollect(atz_ctx* c) {
+  for (size_t i = 0; i < c->kt.pending.size(); i++) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->kt.pending[i].first, c->kt.pending[i].second);
+    switch (c->kt.kind[i]) {
+      case 0: c->stats.k_trial_ms += ms; c->stats.k_trial_launches++; break;
+      case 1: c->stats.k_inflate_ms += ms; c->stats.k_inflate_launches++; break;
+      case 2: c->stats.k_chains_ms += ms; c->stats.k_chains_launches++; break;
+      default: c->stats.k_other_ms += ms; break;
+    }
+    c->kt.pool.push_back(c->kt.pending[i].first);
+    c->kt.pool.push_back(c->kt.pending[i].second);
+  }
+  c->kt.pending.clear();
+  c->kt.kind.clear();
+}
+
+// copy n host bytes into b (device capacity n + slack; the slack is never read from the host)
+static int upload(atz_ctx* c, DBuf& b, const void* h, size_t n, size_t slack = 4096) {
+  if (int r = b.reserve(n + slack)) return r;
+  if (n) HIPCHK(hipMemcpyAsync(b.p, h, n, hipMemcpyHostToDevice, c->st));
+  return 0;
+}
+
+static bool sync_debug() {
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_SYNC_DEBUG"); v = e && *e == '1'; }
+  return v == 1;
+}
+// ATZ_SYNC_DEBUG=1: synchronise after every launch and name the kernel that failed
+#define KCHECK(name)                                                                            \
+  do {                                                                                          \
+    hipError_t e_ = hipGetLastError();                                                          \
+    if (e_ == hipSuccess && sync_debug()) e_ = hipStreamSynchronize(c->st);                     \
+    if (e_ != hipSuccess) {                                                                     \
+      std::fprintf(stderr, "atz: kernel %s failed: %s (%s:%d)\n", name, hipGetErrorString(e_), \
+                   __FILE__, __LINE__);                                                         \
+      return ATZ_E_HIP;                                                                         \
+    }                                                                                           \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// Phase 1
+struct Chunk {
+  uint64_t co;    // chunkOffset (file position of buffer[1] minus 1)
+  uint64_t len;   // buffer length
+  uint8_t b0;     // buffer[0]
+  bool b0_file;   // buffer[0] == file[co] (buffer is contiguous file data)
+};
+
+static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, const std::vector<InfJob>& jobs,
+                            std::vector<InfRes>& res) {
+  res.resize(jobs.size());
+  if (jobs.empty()) return 0;
+  if (int r = upload(c, c->d_jobs, jobs.data(), jobs.size() * sizeof(InfJob))) return r;
+  if (int r = c->d_res.reserve(jobs.size() * sizeof(InfRes))) return r;
+  uint32_t n = (uint32_t)jobs.size();
+  kbeg(c, 1);
+  hipLaunchKernelGGL(k_inflate, dim3((n + INF_WAVES - 1) / INF_WAVES), dim3(64 * INF_WAVES), 0, c->st, d_in,
+                     d_out, c->d_jobs.as<InfJob>(), c->d_res.as<InfRes>(), n);
+  kend(c);
+  KCHECK("k_inflate");
+  HIPCHK(hipMemcpyAsync(res.data(), c->d_res.p, n * sizeof(InfRes), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  kcollect(c);
+  for (uint32_t k = 0; k < n; k++)   // bytes read + bytes written (when kept)
+    c->stats.k_inflate_alg_bytes += res[k].consumed + (jobs[k].out_off == NO_OUT ? 0 : res[k].produced);
+  return 0;
+}
+
+// inflate one materialized byte string (boundary continuations)
+static int inflate_bytes(atz_ctx* c, const std::vector<uint8_t>& v, InfRes& out) {
+  if (int r = upload(c, c->d_virt, v.data(), v.size())) return r;
+  std::vector<InfJob> j(1);
+  j[0].in_off = 0; j[0].in_len = v.size(); j[0].out_off = NO_OUT; j[0].out_cap = 0;
+  std::vector<InfRes> rr;
+  if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, j, rr)) return r;
+  out = rr[0];
+  return 0;
+}
+
+static void chunk_bytes(const uint8_t* f, const Chunk& ch, std::vector<uint8_t>& v) {
+  v.push_back(ch.b0);
+  v.insert(v.end(), f + ch.co + 1, f + ch.co + ch.len);
+}
+
+static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64_t F) {
+  auto t0 = std::chrono::steady_clock::now();
+  c->recs.clear();
+  const uint64_t cs = c->o.chunksize;
+  if (cs < 2) return ATZ_E_REF_UB;      // main.cpp:410-415 never reaches eof with chunksize 1
+  if (F == 0) return ATZ_E_REF_UB;      // main.cpp:406 reads rBuffer[-1]
+  // ---- chunk layout exactly as searchInfile reads the file (main.cpp:405-415) ----
+  std::vector<Chunk> chunks;
+  {
+    uint64_t g = F < cs ? F : cs;
+    chunks.push_back({0, g, h[0], true});
+    bool eof = g < cs;
+    uint64_t pos = g;
+    uint8_t last = h[g - 1];
+    while (!eof) {
+      uint64_t gg = F - pos < cs - 1 ? F - pos : cs - 1;
+      Chunk ch{pos - 1, gg + 1, last, h[pos - 1] == last};
+      chunks.push_back(ch);
+      eof = gg < cs - 1;
+      if (gg >= 2) last = h[pos + gg - 2];      // rBuffer[gcount-1] with data at rBuffer[1..gcount]
+      else if (gg == 1) last = ch.b0;
+      pos += gg;
+    }
+  }
+  // ---- all header pairs of the file (GPU) ----
+  uint64_t cap = F / 8 + 1024;
+  if (int r = c->d_pos.reserve(cap * 8)) return r;
+  if (int r = c->d_cnt.reserve(64)) return r;
+  HIPCHK(hipMemsetAsync(c->d_cnt.p, 0, 8, c->st));
+  {
+    uint64_t blocks = (F + 256 * 16 - 1) / (256 * 16);
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    kbeg(c, 3);
+    hipLaunchKernelGGL(k_find_headers, dim3((uint32_t)blocks), dim3(256), 0, c->st, d_file, F,
+                       c->d_pos.as<uint64_t>(), c->d_cnt.as<unsigned long long>(), cap);
+    kend(c);
+    KCHECK("k_find_headers");
+  }
+  uint64_t npairs = 0;
+  HIPCHK(hipMemcpyAsync(&npairs, c->d_cnt.p, 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  kcollect(c);
+  if (npairs > cap) return ATZ_E_INTERNAL;
+  std::vector<uint64_t> pairs(npairs);
+  if (npairs) {
+    HIPCHK(hipMemcpy(pairs.data(), c->d_pos.p, npairs * 8, hipMemcpyDeviceToHost));
+    std::sort(pairs.begin(), pairs.end());
+  }
+  // ---- candidates per chunk: i >= 1 are file pairs, i == 0 uses buffer[0] ----
+  struct Cand { uint32_t chunk; uint64_t i; int type; uint64_t job; };
+  std::vector<Cand> cands;
+  std::vector<InfJob> jobs, vjobs;     // file-backed jobs / jobs on materialized buffers (i==0, b0 != file)
+  std::vector<uint64_t> vjob_of;       // job index -> vjobs index (+1), 0 if file-backed
+  std::vector<uint8_t> virt;
+  {
+    size_t pi = 0;
+    for (uint32_t j = 0; j < chunks.size(); j++) {
+      const Chunk& ch = chunks[j];
+      if (ch.len < 2) continue;
+      int t0 = header_type_host(ch.b0, h[ch.co + 1]);
+      if (t0 >= 0) {
+        InfJob jb;
+        jb.in_len = ch.len; jb.out_off = NO_OUT; jb.out_cap = 0;
+        if (ch.b0_file) {
+          jb.in_off = ch.co;
+          vjob_of.push_back(0);
+        } else {
+          jb.in_off = virt.size();
+          std::vector<uint8_t> v;
+          chunk_bytes(h, ch, v);
+          virt.insert(virt.end(), v.begin(), v.end());
+          virt.resize((virt.size() + 3) & ~(size_t)3);
+          vjobs.push_back(jb);
+          vjob_of.push_back(vjobs.size());
+        }
+        cands.push_back({j, 0, t0, jobs.size()});
+        jobs.push_back(jb);
+      }
+      uint64_t lo = ch.co + 1, hi = ch.co + ch.len - 2;   // file pairs scanned as i = 1 .. len-2
+      while (pi < pairs.size() && pairs[pi] < lo) pi++;
+      size_t pj = pi;
+      while (pj < pairs.size() && pairs[pj] <= hi) {
+        uint64_t p = pairs[pj];
+        InfJob jb;
+        jb.in_off = p; jb.in_len = ch.co + ch.len - p; jb.out_off = NO_OUT; jb.out_cap = 0;
+        cands.push_back({j, p - ch.co, header_type_host(h[p], h[p + 1]), jobs.size()});
+        jobs.push_back(jb);
+        vjob_of.push_back(0);
+        pj++;
+      }
+    }
+  }
+  std::vector<InfRes> res;
+  {
+    std::vector<InfJob> fjobs;
+    std::vector<size_t> fidx;
+    for (size_t k = 0; k < jobs.size(); k++) if (!vjob_of[k]) { fjobs.push_back(jobs[k]); fidx.push_back(k); }
+    std::vector<InfRes> fr, vr;
+    if (int r = run_inflate_jobs(c, d_file, nullptr, fjobs, fr)) return r;
+    if (!vjobs.empty()) {
+      if (int r = upload(c, c->d_virt, virt.data(), virt.size())) return r;
+      if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, vjobs, vr)) return r;
+    }
+    res.resize(jobs.size());
+    for (size_t q = 0; q < fidx.size(); q++) res[fidx[q]] = fr[q];
+    for (size_t k = 0; k < jobs.size(); k++) if (vjob_of[k]) res[k] = vr[vjob_of[k] - 1];
+  }
+  c->stats.n_candidates = jobs.size();
+  // ---- per-chunk candidate index ranges ----
+  std::vector<size_t> cbeg(chunks.size() + 1, cands.size());
+  for (size_t k = cands.size(); k-- > 0;) cbeg[cands[k].chunk] = k;
+  for (size_t j = chunks.size(); j-- > 0;) if (cbeg[j] > cbeg[j + 1]) cbeg[j] = cbeg[j + 1];
+  // greedy selection from position i0 (main.cpp:218-241). Returns pending candidate index or -1.
+  auto select = [&](uint32_t j, uint64_t i0, std::vector<Rec>* out) -> long {
+    const Chunk& ch = chunks[j];
+    uint64_t i = i0;
+    for (size_t k = cbeg[j]; k < cbeg[j + 1]; k++) {
+      const Cand& cd = cands[k];
+      if (cd.i < i) continue;
+      const InfRes& r = res[cd.job];
+      if (r.consumed <= 16) continue;
+      if (r.status == INF_END) {
+        if (out) out->push_back({cd.i + ch.co, r.consumed, r.produced, cd.type, 0});
+        i = cd.i + r.consumed;
+      } else if (r.consumed == ch.len - cd.i) {
+        return (long)k;
+      }
+    }
+    return -1;
+  };
+  // speculative first continuations: pending candidate of chunk j (selection from 0) + buffer j+1
+  std::vector<long> pend0(chunks.size(), -1);
+  std::vector<InfRes> cont0(chunks.size());
+  {
+    std::vector<uint8_t> cv;
+    std::vector<InfJob> cj;
+    std::vector<uint32_t> cj_chunk;
+    for (uint32_t j = 0; j + 1 < chunks.size(); j++) {
+      long k = select(j, 0, nullptr);
+      pend0[j] = k;
+      if (k < 0) continue;
+      const Cand& cd = cands[k];
+      const Chunk& ch = chunks[j];
+      InfJob jb;
+      jb.in_off = cv.size();
+      if (cd.i == 0) { std::vector<uint8_t> v; chunk_bytes(h, ch, v); cv.insert(cv.end(), v.begin(), v.end()); }
+      else cv.insert(cv.end(), h + ch.co + cd.i, h + ch.co + ch.len);
+      std::vector<uint8_t> v; chunk_bytes(h, chunks[j + 1], v);
+      cv.insert(cv.end(), v.begin(), v.end());
+      jb.in_len = cv.size() - jb.in_off; jb.out_off = NO_OUT; jb.out_cap = 0;
+      cj.push_back(jb);
+      cj_chunk.push_back(j);
+      cv.resize((cv.size() + 3) & ~(size_t)3);
+    }
+    if (!cj.empty()) {
+      if (int r = upload(c, c->d_virt, cv.data(), cv.size())) return r;
+      std::vector<InfRes> cr;
+      if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, cj, cr)) return r;
+      for (size_t q = 0; q < cj.size(); q++) cont0[cj_chunk[q]] = cr[q];
+    }
+    c->stats.n_continuations = cj.size();
+  }
+  // ---- sequential replay (main.cpp:205-246 over searchInfile's chunk sequence) ----
+  bool need_more = false;
+  struct Pend { uint64_t off; int type; int state; std::vector<uint8_t> bytes; uint64_t in, out; long spec_chunk; int refills; } pd{};
+  for (uint32_t j = 0; j < chunks.size(); j++) {
+    const Chunk& ch = chunks[j];
+    uint64_t i = 0;
+    if (need_more) {
+      uint64_t avail;
+      int st;
+      if (pd.state == INF_NEED) {
+        InfRes rr;
+        if (pd.refills == 0 && pd.spec_chunk == (long)j - 1) {
+          rr = cont0[j - 1];
+        } else {
+          std::vector<uint8_t> v = pd.bytes;
+          chunk_bytes(h, ch, v);
+          if (int r = inflate_bytes(c, v, rr)) return r;
+        }
+        chunk_bytes(h, ch, pd.bytes);
+        pd.refills++;
+        pd.state = (int)rr.status; pd.in = rr.consumed; pd.out = rr.produced;
+        avail = pd.bytes.size() - rr.consumed;
+        st = (int)rr.status;
+      } else if (pd.state == INF_END) {  // inflate() in DONE mode returns Z_STREAM_END again
+        avail = ch.len; st = INF_END;
+      } else {                           // BAD mode: Z_DATA_ERROR, nothing consumed
+        avail = ch.len; st = INF_ERROR;
+      }
+      if (st == INF_END) {
+        c->recs.push_back({pd.off, pd.in, pd.out, pd.type, 1});
+        i = ch.len - avail;
+      }
+      need_more = avail == 0;
+    }
+    if (!need_more) {
+      long k = select(j, i, &c->recs);
+      if (k >= 0) {
+        const Cand& cd = cands[k];
+        need_more = true;
+        pd.off = cd.i + ch.co; pd.type = cd.type; pd.state = (int)res[cd.job].status;
+        pd.in = res[cd.job].consumed; pd.out = res[cd.job].produced;
+        pd.bytes.clear();
+        if (cd.i == 0) chunk_bytes(h, ch, pd.bytes);
+        else pd.bytes.assign(h + ch.co + cd.i, h + ch.co + ch.len);
+        pd.spec_chunk = (i == 0 && pend0[j] == k) ? (long)j : -2;
+        pd.refills = 0;
+      }
+    }
+  }
+  c->stats.scan_ms = ms_since(t0);
+  return 0;
+}
+
+// final inflate of every record from the FILE bytes (Phase 3's doInflate, main.cpp:431-453)
+static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F) {
+  const size_t n = c->recs.size();
+  c->infl_off.resize(n);
+  c->adler.resize(n);
+  uint64_t tot = 0;
+  std::vector<InfJob> jobs(n);
+  for (size_t s = 0; s < n; s++) {
+    const Rec& r = c->recs[s];
+    if (r.offset + r.comp_len > F) return ATZ_E_REF_UB;   // reads past EOF (uninitialised rBuffer)
+    c->infl_off[s] = tot;
+    jobs[s].in_off = r.offset; jobs[s].in_len = r.comp_len; jobs[s].out_off = tot; jobs[s].out_cap = r.infl_len;
+    tot += (r.infl_len + 255) & ~255ull;
+  }
+  if (int r = c->d_infl.reserve(tot + 65536)) return r;
+  std::vector<InfRes> res;
+  if (int r = run_inflate_jobs(c, d_file, c->d_infl.as<uint8_t>(), jobs, res)) return r;
+  for (size_t s = 0; s < n; s++) {
+    if (res[s].status != INF_END) return ATZ_E_REF_ABORT;          // main.cpp:450-452
+    if (res[s].produced != c->recs[s].infl_len) return ATZ_E_REF_UB;
+    // Adler-32 of the inflated bytes = the verified trailer
+    const uint64_t e = c->recs[s].offset + res[s].consumed;
+    c->adler[s] = ((uint32_t)c->hfile[e - 4] << 24) | ((uint32_t)c->hfile[e - 3] << 16) |
+                  ((uint32_t)c->hfile[e - 2] << 8) | c->hfile[e - 1];
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Phase 3
+static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>& need) {
+  std::vector<ChainJob> jobs;
+  for (auto& q : need) {
+    uint32_t s = q.first;
+    int m = q.second;
+    if (c->chain_off[s][m] != ~0ull) continue;
+    ChainJob jb;
+    jb.infl_off = c->infl_off[s];
+    jb.n = c->recs[s].infl_len;
+    jb.chain_off = c->chain_used;
+    jb.memlevel = (uint32_t)m;
+    jb.slot = 0;
+    c->chain_off[s][m] = c->chain_used;
+    c->chain_used += (jb.n + 63) & ~63ull;
+    jobs.push_back(jb);
+  }
+  if (jobs.empty()) return 0;
+  // grow the chain cache (keeps contents)
+  size_t need_bytes = c->chain_used * 2 + 4096;
+  if (need_bytes > c->d_chains.n) {
+    void* np = nullptr;
+    size_t cap = need_bytes + need_bytes / 2 + (64 << 20);
+    if (hipMalloc(&np, cap) != hipSuccess) return ATZ_E_NOMEM;
+    if (c->d_chains.p) {
+      HIPCHK(hipMemcpyAsync(np, c->d_chains.p, c->d_chains.n, hipMemcpyDeviceToDevice, c->st));
+      HIPCHK(hipStreamSynchronize(c->st));
+      hipFree(c->d_chains.p);
+    }
+    c->d_chains.p = np;
+    c->d_chains.n = cap;
+  }
+  const uint64_t slot_words = 1u << 16;
+  const size_t batch = 4096;
+  if (int r = c->d_heads.reserve(batch * slot_words * 4)) return r;
+  for (size_t b0 = 0; b0 < jobs.size(); b0 += batch) {
+    size_t nb = std::min(batch, jobs.size() - b0);
+    for (size_t k = 0; k < nb; k++) jobs[b0 + k].slot = (uint32_t)k;
+    if (int r = upload(c, c->d_cjobs, jobs.data() + b0, nb * sizeof(ChainJob))) return r;
+    kbeg(c, 2);
+    hipLaunchKernelGGL(k_chains, dim3((uint32_t)nb), dim3(64), 0, c->st, c->d_infl.as<uint8_t>(),
+                       c->d_cjobs.as<ChainJob>(), c->d_chains.as<uint16_t>(), c->d_heads.as<uint32_t>(),
+                       slot_words, (uint32_t)nb);
+    kend(c);
+    KCHECK("k_chains");
+    HIPCHK(hipStreamSynchronize(c->st));
+    kcollect(c);
+    for (size_t k = 0; k < nb; k++) c->stats.k_chains_alg_bytes += 3 * jobs[b0 + k].n;  // read I_s, write 2*I_s
+  }
+  return 0;
+}
+
+static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
+  auto t0 = std::chrono::steady_clock::now();
+  const size_t n = c->recs.size();
+  ss.assign(n, StreamState());
+  c->chain_off.assign(n, {});
+  for (auto& a : c->chain_off) a.fill(~0ull);
+  c->chain_used = 0;
+  std::vector<uint32_t> active;
+  for (size_t s = 0; s < n; s++) {
+    list_a(ss[s].list, c->recs[s].type);
+    active.push_back((uint32_t)s);
+  }
+  // device stream table
+  std::vector<StreamDev> sd(n);
+  for (size_t s = 0; s < n; s++) {
+    sd[s].orig_off = c->recs[s].offset; sd[s].infl_off = c->infl_off[s];
+    sd[s].comp_len = c->recs[s].comp_len; sd[s].infl_len = c->recs[s].infl_len;
+  }
+  if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;
+  if (int r = upload(c, c->d_streams, sd.data(), n * sizeof(StreamDev))) return r;
+  SweepOpts so{c->o.recomp_tresh, c->o.sizediff_tresh, c->o.shortcut_len, c->o.mismatch_tol};
+  uint64_t rounds = 0, ntr = 0, nsc = 0, nhz = 0;
+  std::vector<Trial> tr[3];
+  std::vector<uint32_t> tr_stream[3];
+  std::vector<TrialRes> trres[3];
+  while (!active.empty()) {
+    rounds++;
+    // trials of this round and the chain tables they need
+    std::vector<std::pair<uint32_t, int>> need;
+    for (int k = 0; k < 3; k++) { tr[k].clear(); tr_stream[k].clear(); }
+    uint64_t out_tot = 0, sym_tot = 0;
+    for (uint32_t s : active) {
+      StreamState& st = ss[s];
+      uint32_t p = st.list[st.idx];
+      int cl = (int)(p >> 16), w = (int)((p >> 8) & 0xff), m = (int)(p & 0xff);
+      Trial t{};
+      t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
+      t.best_ident = st.ident;
+      t.out_off = out_tot; t.out_cap = bound(c->recs[s].infl_len, w, m) + 64;
+      out_tot += (t.out_cap + 255) & ~255ull;
+      t.sym_off = sym_tot; sym_tot += 1ull << (m + 6);
+      int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
+      if (kind) need.push_back({s, m});
+      tr[kind].push_back(t);
+      tr_stream[kind].push_back(s);
+    }
+    if (int r = ensure_chains(c, need)) return r;
+    for (int k = 1; k < 3; k++)
+      for (Trial& t : tr[k]) t.chain_off = c->chain_off[t.stream][t.memlevel];
+    if (int r = c->d_out.reserve(out_tot + 4096)) return r;
+    if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
+    size_t tot_trials = tr[0].size() + tr[1].size() + tr[2].size();
+    if (int r = c->d_trials.reserve(tot_trials * sizeof(Trial) + 64)) return r;
+    if (int r = c->d_tres.reserve(tot_trials * sizeof(TrialRes) + 64)) return r;
+    size_t base = 0;
+    for (int k = 0; k < 3; k++) {
+      if (tr[k].empty()) continue;
+      HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + base, tr[k].data(), tr[k].size() * sizeof(Trial),
+                            hipMemcpyHostToDevice, c->st));
+      SweepArgs A;
+      A.file = d_file; A.infl = c->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint16_t>();
+      A.streams = c->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
+      A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
+      A.adler = c->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)tr[k].size();
+      dim3 g((uint32_t)tr[k].size()), b(64);
+      kbeg(c, 0);
+      if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
+      else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, 0, c->st, A);
+      else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
+      kend(c);
+      KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
+      trres[k].resize(tr[k].size());
+      HIPCHK(hipMemcpyAsync(trres[k].data(), c->d_tres.as<TrialRes>() + base, tr[k].size() * sizeof(TrialRes),
+                            hipMemcpyDeviceToHost, c->st));
+      base += tr[k].size();
+    }
+    HIPCHK(hipStreamSynchronize(c->st));
+    kcollect(c);
+    for (int k = 0; k < 3; k++)
+      for (size_t q = 0; q < tr[k].size(); q++) {
+        const TrialRes& r = trres[k][q];
+        const uint64_t C = c->recs[tr[k][q].stream].comp_len;
+        c->stats.trial_parsed_bytes += r.parsed;
+        // trial input read + compare read (bytes emitted and compared against the original)
+        c->stats.k_trial_alg_bytes += c->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
+      }
+    // apply the reference's sequential rule per stream (one trial per stream per round)
+    std::vector<DiffJob> dj;
+    std::vector<uint32_t> dj_stream;
+    uint64_t dpos = 0;
+    for (int k = 0; k < 3; k++) {
+      for (size_t q = 0; q < tr[k].size(); q++) {
+        const Trial& t = tr[k][q];
+        const TrialRes& r = trres[k][q];
+        StreamState& st = ss[t.stream];
+        const uint64_t C = c->recs[t.stream].comp_len;
+        st.trials++;
+        ntr++;
+        if (r.state == TR_SHORTCUT) nsc++;
+        if (r.flags & 1) nhz++;
+        if (r.state == TR_OVERFLOW) return ATZ_E_REF_ABORT;   // deflate() without Z_STREAM_END, main.cpp:663-665
+        bool fullmatch = false;
+        if (r.state == TR_FULL && r.ident > st.ident) {
+          st.ident = r.ident;
+          st.c = t.clevel; st.w = t.window; st.m = t.memlevel;
+          st.first_diff = -1;
+          st.rawdiff.clear(); st.diffval.clear();
+          if (r.ident == C) fullmatch = true;
+          else {
+            if (r.ident + c->o.mismatch_tol >= C) fullmatch = true;
+            if (C - r.ident <= c->o.recomp_tresh) {     // diffs are only ever written for recomp streams
+              DiffJob d;
+              d.out_off = t.out_off; d.out_len = r.out_len; d.orig_off = c->recs[t.stream].offset;
+              d.comp_len = C; d.dst = dpos; d.cap = C - r.ident;
+              dpos += d.cap;
+              dj.push_back(d);
+              dj_stream.push_back(t.stream);
+            }
+          }
+        }
+        st.idx++;
+        if (fullmatch) st.idx = (uint32_t)st.list.size();   // testParamRange/tryParams return
+        if (st.idx >= st.list.size()) {
+          if (st.phase == 0 && (C - st.ident) >= c->o.mismatch_tol && c->o.brute_window) {
+            st.list.clear();
+            list_b(st.list, c->recs[t.stream].type);
+            st.idx = 0;
+            st.phase = 1;
+          } else {
+            st.phase = 2;
+          }
+        }
+      }
+    }
+    if (!dj.empty()) {
+      if (int r = upload(c, c->d_diffjobs, dj.data(), dj.size() * sizeof(DiffJob))) return r;
+      if (int r = c->d_diffpos.reserve(dpos * 4 + 64)) return r;
+      if (int r = c->d_diffval.reserve(dpos + 64)) return r;
+      if (int r = c->d_diffcnt.reserve(dj.size() * 8 + 64)) return r;
+      kbeg(c, 3);
+      hipLaunchKernelGGL(k_diffs, dim3((uint32_t)dj.size()), dim3(64), 0, c->st, c->d_out.as<uint8_t>(), d_file,
+                         c->d_diffjobs.as<DiffJob>(), c->d_diffpos.as<uint32_t>(), c->d_diffval.as<uint8_t>(),
+                         c->d_diffcnt.as<uint64_t>(), (uint32_t)dj.size());
+      kend(c);
+      KCHECK("k_diffs");
+      std::vector<uint32_t> pos(dpos);
+      std::vector<uint8_t> val(dpos);
+      std::vector<uint64_t> cnt(dj.size());
+      HIPCHK(hipMemcpyAsync(pos.data(), c->d_diffpos.p, dpos * 4, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipMemcpyAsync(val.data(), c->d_diffval.p, dpos, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipMemcpyAsync(cnt.data(), c->d_diffcnt.p, dj.size() * 8, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipStreamSynchronize(c->st));
+      kcollect(c);
+      for (size_t q = 0; q < dj.size(); q++) {
+        if (cnt[q] != dj[q].cap) return ATZ_E_INTERNAL;
+        StreamState& st = ss[dj_stream[q]];
+        st.rawdiff.assign(pos.begin() + dj[q].dst, pos.begin() + dj[q].dst + dj[q].cap);
+        st.diffval.assign(val.begin() + dj[q].dst, val.begin() + dj[q].dst + dj[q].cap);
+        st.first_diff = st.rawdiff.empty() ? -1 : (int64_t)st.rawdiff[0];
+      }
+    }
+    std::vector<uint32_t> next;
+    for (uint32_t s : active) if (ss[s].phase != 2) next.push_back(s);
+    active.swap(next);
+  }
+  for (size_t s = 0; s < n; s++) {
+    StreamState& st = ss[s];
+    const uint64_t C = c->recs[s].comp_len;
+    st.recomp = (C - st.ident) <= c->o.recomp_tresh && st.ident > 0;
+  }
+  c->stats.n_trials = ntr; c->stats.n_trials_shortcut = nsc; c->stats.n_rounds = rounds; c->stats.n_hazard = nhz;
+  c->stats.sweep_ms = ms_since(t0);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Phase 4: ATZ1 assembled in HBM
+static void put8(std::vector<uint8_t>& m, uint64_t v) { uint8_t b[8]; std::memcpy(b, &v, 8); m.insert(m.end(), b, b + 8); }
+
+static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::vector<StreamState>& ss,
+                      uint64_t* atz_len) {
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint8_t> meta;
+  std::vector<Seg> segs;
+  uint64_t out = 0;
+  auto emit_meta = [&](const std::vector<uint8_t>& bytes) {
+    Seg g{0, 0, meta.size(), out, bytes.size()};
+    meta.insert(meta.end(), bytes.begin(), bytes.end());
+    segs.push_back(g);
+    out += bytes.size();
+  };
+  const size_t n = c->recs.size();
+  uint64_t nrec = 0;
+  for (size_t s = 0; s < n; s++) nrec += ss[s].recomp;
+  {
+    std::vector<uint8_t> h = {'A', 'T', 'Z', 1};
+    put8(h, 0); put8(h, F); put8(h, nrec);
+    emit_meta(h);
+  }
+  for (size_t s = 0; s < n; s++) {
+    const StreamState& st = ss[s];
+    if (!st.recomp) continue;
+    const Rec& r = c->recs[s];
+    std::vector<uint8_t> d;
+    put8(d, r.offset); put8(d, r.comp_len); put8(d, r.infl_len);
+    d.push_back(st.c); d.push_back(st.w); d.push_back(st.m);
+    uint64_t nd = st.rawdiff.size();
+    put8(d, nd);
+    if (nd) {
+      put8(d, (uint64_t)st.first_diff);
+      for (uint64_t k = 0; k < nd; k++) put8(d, k == 0 ? 0 : (uint64_t)st.rawdiff[k] - st.rawdiff[k - 1]);
+      d.insert(d.end(), st.diffval.begin(), st.diffval.end());
+    }
+    emit_meta(d);
+    segs.push_back({1, 0, c->infl_off[s], out, r.infl_len});
+    out += r.infl_len;
+  }
+  uint64_t lastos = 0, lastlen = 0;
+  for (size_t s = 0; s < n; s++) {
+    const Rec& r = c->recs[s];
+    if (lastos + lastlen != r.offset) {
+      if (r.offset < lastos + lastlen) return ATZ_E_REF_UB;   // copyto() with a wrapped length
+      segs.push_back({2, 0, lastos + lastlen, out, r.offset - (lastos + lastlen)});
+      out += r.offset - (lastos + lastlen);
+    }
+    if (!ss[s].recomp) { segs.push_back({2, 0, r.offset, out, r.comp_len}); out += r.comp_len; }
+    lastos = r.offset; lastlen = r.comp_len;
+  }
+  if (lastos + lastlen < F) { segs.push_back({2, 0, lastos + lastlen, out, F - (lastos + lastlen)}); out += F - (lastos + lastlen); }
+  std::memcpy(meta.data() + 4, &out, 8);   // back-patched length (main.cpp:797-800)
+  if (int r = upload(c, c->d_meta, meta.data(), meta.size())) return r;
+  if (int r = upload(c, c->d_segs, segs.data(), segs.size() * sizeof(Seg))) return r;
+  if (int r = c->d_atz.reserve(out + 4096)) return r;
+  uint32_t nseg = (uint32_t)segs.size();
+  uint32_t blocks = std::min<uint32_t>((nseg + 3) / 4, 65535u);
+  kbeg(c, 3);
+  hipLaunchKernelGGL(k_gather, dim3(blocks ? blocks : 1), dim3(256), 0, c->st, c->d_meta.as<uint8_t>(),
+                     c->d_infl.as<uint8_t>(), d_file, c->d_atz.as<uint8_t>(), c->d_segs.as<Seg>(), nseg);
+  kend(c);
+  KCHECK("k_gather");
+  HIPCHK(hipStreamSynchronize(c->st));
+  kcollect(c);
+  *atz_len = out;
+  c->stats.write_ms = ms_since(t0);
+  return 0;
+}
+
+static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, uint64_t F, uint64_t* atz_len,
+                           std::vector<StreamState>* ss_out) {
+  auto t0 = std::chrono::steady_clock::now();
+  c->stats = atz_stats_t{};
+  c->hfile = h; c->flen = F;
+  c->stats.file_bytes = F;
+  if (int r = scan_impl(c, h, d_file, F)) return r;
+  auto t1 = std::chrono::steady_clock::now();
+  if (int r = inflate_records(c, d_file, F)) return r;
+  c->stats.scan_ms += ms_since(t1);
+  std::vector<StreamState> ss;
+  if (int r = sweep_impl(c, d_file, ss)) return r;
+  if (int r = write_impl(c, d_file, F, ss, atz_len)) return r;
+  c->stats.n_streams = c->recs.size();
+  for (auto& s : ss) c->stats.n_recomp += s.recomp;
+  c->stats.atz_bytes = *atz_len;
+  c->stats.total_ms = ms_since(t0);
+  if (ss_out) ss_out->swap(ss);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// one-shot deflates (reconstruct / atz_deflate): trials with mode "full output" on a temporary stream set
+static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, uint64_t>>& ins,
+                        const std::vector<uint32_t>& params, std::vector<std::vector<uint8_t>>& outs) {
+  const size_t n = ins.size();
+  outs.assign(n, {});
+  if (!n) return 0;
+  uint64_t tot = 0;
+  std::vector<uint64_t> off(n);
+  for (size_t s = 0; s < n; s++) { off[s] = tot; tot += (ins[s].second + 255) & ~255ull; }
+  std::vector<uint8_t> hb(tot + 8);
+  for (size_t s = 0; s < n; s++) if (ins[s].second) std::memcpy(hb.data() + off[s], ins[s].first, ins[s].second);
+  if (int r = upload(c, c->d_infl, hb.data(), hb.size(), 65536)) return r;
+  // fake record table for chain building
+  c->recs.assign(n, Rec{});
+  c->infl_off = off;
+  c->adler.resize(n);
+  for (size_t s = 0; s < n; s++) {
+    c->recs[s].infl_len = ins[s].second;
+    uint32_t a = 1, b = 0;
+    for (uint64_t k = 0; k < ins[s].second; k++) { a = (a + ins[s].first[k]) % 65521; b = (b + a) % 65521; }
+    c->adler[s] = (b << 16) | a;
+  }
+  c->chain_off.assign(n, {});
+  for (auto& a : c->chain_off) a.fill(~0ull);
+  c->chain_used = 0;
+  std::vector<std::pair<uint32_t, int>> need;
+  for (size_t s = 0; s < n; s++) if ((params[s] >> 16) > 0) need.push_back({(uint32_t)s, (int)(params[s] & 0xff)});
+  if (int r = ensure_chains(c, need)) return r;
+  std::vector<StreamDev> sd(n);
+  for (size_t s = 0; s < n; s++) {
+    sd[s].orig_off = 0; sd[s].infl_off = off[s]; sd[s].comp_len = 0; sd[s].infl_len = ins[s].second;
+  }
+  if (int r = upload(c, c->d_streams, sd.data(), n * sizeof(StreamDev))) return r;
+  if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;
+  std::vector<Trial> tr[3];
+  std::vector<uint32_t> idx[3];
+  uint64_t out_tot = 0, sym_tot = 0;
+  for (size_t s = 0; s < n; s++) {
+    int cl = (int)(params[s] >> 16), w = (int)((params[s] >> 8) & 0xff), m = (int)(params[s] & 0xff);
+    Trial t{};
+    t.stream = (uint32_t)s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 1;
+    t.best_ident = 0; t.out_off = out_tot; t.out_cap = bound(ins[s].second, w, m) + 64;
+    out_tot += (t.out_cap + 255) & ~255ull;
+    t.sym_off = sym_tot; sym_tot += 1ull << (m + 6);
+    int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
+    if (kind) t.chain_off = c->chain_off[s][m];
+    tr[kind].push_back(t);
+    idx[kind].push_back((uint32_t)s);
+  }
+  if (int r = c->d_out.reserve(out_tot + 4096)) return r;
+  if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
+  if (int r = c->d_trials.reserve(n * sizeof(Trial) + 64)) return r;
+  if (int r = c->d_tres.reserve(n * sizeof(TrialRes) + 64)) return r;
+  // zero-length "file" for the compare side
+  if (int r = c->d_tmp.reserve(4096)) return r;
+  SweepOpts so{0, 0, 0, 0};
+  size_t base = 0;
+  std::vector<TrialRes> rr[3];
+  for (int k = 0; k < 3; k++) {
+    if (tr[k].empty()) continue;
+    HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + base, tr[k].data(), tr[k].size() * sizeof(Trial),
+                          hipMemcpyHostToDevice, c->st));
+    SweepArgs A;
+    A.file = c->d_tmp.as<uint8_t>(); A.infl = c->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint16_t>();
+    A.streams = c->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
+    A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
+    A.adler = c->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)tr[k].size();
+    dim3 g((uint32_t)tr[k].size()), b(64);
+    kbeg(c, 0);
+    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
+    else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, 0, c->st, A);
+    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
+    kend(c);
+    KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
+    rr[k].resize(tr[k].size());
+    HIPCHK(hipMemcpyAsync(rr[k].data(), c->d_tres.as<TrialRes>() + base, tr[k].size() * sizeof(TrialRes),
+                          hipMemcpyDeviceToHost, c->st));
+    base += tr[k].size();
+  }
+  HIPCHK(hipStreamSynchronize(c->st));
+  kcollect(c);
+  for (int k = 0; k < 3; k++) {
+    for (size_t q = 0; q < tr[k].size(); q++) {
+      if (rr[k][q].state != TR_FULL) return ATZ_E_INTERNAL;
+      std::vector<uint8_t>& o = outs[idx[k][q]];
+      o.resize(rr[k][q].out_len);
+      HIPCHK(hipMemcpy(o.data(), c->d_out.as<uint8_t>() + tr[k][q].out_off, o.size(), hipMemcpyDeviceToHost));
+    }
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+
+void atz_default_opts(atz_opts_t* o) {
+  o->recomp_tresh = 128; o->sizediff_tresh = 128; o->shortcut_len = 512; o->mismatch_tol = 2;
+  o->chunksize = 524288; o->brute_window = 0; o->device = -1;
+}
+
+const char* atz_strerror(int e) {
+  switch (e) {
+    case ATZ_OK: return "ok";
+    case ATZ_E_ARG: return "invalid argument";
+    case ATZ_E_NODEV: return "no usable HIP device (gfx950 kernels not loadable)";
+    case ATZ_E_HIP: return "HIP runtime error";
+    case ATZ_E_NOMEM: return "out of memory";
+    case ATZ_E_REF_ABORT: return "the reference aborts on this input (inflate/deflate failure)";
+    case ATZ_E_REF_UB: return "the reference has undefined behaviour on this input";
+    case ATZ_E_FORMAT: return "invalid ATZ file";
+    default: return "internal error";
+  }
+}
+
+void atz_free(void* p) { std::free(p); }
+
+int atz_open(atz_ctx_t** ctx, const atz_opts_t* opts) {
+  if (!ctx) return ATZ_E_ARG;
+  *ctx = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ATZ_E_NODEV;
+  atz_ctx* c = new atz_ctx();
+  if (opts) c->o = *opts; else atz_default_opts(&c->o);
+  c->dev = c->o.device >= 0 ? c->o.device : 0;
+  if (c->o.device >= 0 && hipSetDevice(c->dev) != hipSuccess) { delete c; return ATZ_E_NODEV; }
+  if (c->o.device < 0) hipGetDevice(&c->dev);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, c->dev) != hipSuccess) { delete c; return ATZ_E_NODEV; }
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+    std::fprintf(stderr, "atz: device %d is %s, kernels are built for gfx950\n", c->dev, prop.gcnArchName);
+    delete c;
+    return ATZ_E_NODEV;
+  }
+  if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { delete c; return ATZ_E_HIP; }
+  DeflTables T;
+  make_tables(T);
+  if (atz_upload_defl_tables(&T) != hipSuccess) { delete c; return ATZ_E_NODEV; }
+  *ctx = c;
+  return ATZ_OK;
+}
+
+void atz_close(atz_ctx_t* c) {
+  if (!c) return;
+  hipStreamSynchronize(c->st);
+  for (DBuf* b : {&c->d_file, &c->d_pos, &c->d_cnt, &c->d_jobs, &c->d_res, &c->d_virt, &c->d_infl, &c->d_chains,
+                  &c->d_heads, &c->d_streams, &c->d_trials, &c->d_tres, &c->d_out, &c->d_syms, &c->d_adler,
+                  &c->d_meta, &c->d_segs, &c->d_atz, &c->d_diffjobs, &c->d_diffpos, &c->d_diffval, &c->d_diffcnt,
+                  &c->d_cjobs, &c->d_tmp})
+    b->release();
+  hipStreamDestroy(c->st);
+  delete c;
+}
+
+int atz_scan(atz_ctx_t* c, const uint8_t* file, uint64_t len, atz_cand_t** out, uint64_t* n) {
+  (void)hipGetLastError();
+  if (!c || (!file && len) || !out || !n) return ATZ_E_ARG;
+  if (int r = upload(c, c->d_file, file, len)) return r;
+  c->hfile = file; c->flen = len;
+  c->stats = atz_stats_t{};
+  if (int r = scan_impl(c, file, c->d_file.as<uint8_t>(), len)) return r;
+  *n = c->recs.size();
+  *out = (atz_cand_t*)std::malloc((c->recs.size() + 1) * sizeof(atz_cand_t));
+  for (size_t s = 0; s < c->recs.size(); s++) {
+    (*out)[s].offset = c->recs[s].offset; (*out)[s].comp_len = c->recs[s].comp_len;
+    (*out)[s].infl_len = c->recs[s].infl_len; (*out)[s].type = c->recs[s].type; (*out)[s].flags = c->recs[s].flags;
+  }
+  return ATZ_OK;
+}
+
+int atz_sweep(atz_ctx_t* c, const atz_cand_t* cands, uint64_t n, atz_result_t* res, uint64_t** diff_off,
+              uint8_t** diff_val, uint64_t* n_diffs) {
+  (void)hipGetLastError();
+  if (!c || !res || n != c->recs.size()) return ATZ_E_ARG;
+  (void)cands;
+  if (int r = inflate_records(c, c->d_file.as<uint8_t>(), c->flen)) return r;
+  std::vector<StreamState> ss;
+  if (int r = sweep_impl(c, c->d_file.as<uint8_t>(), ss)) return r;
+  uint64_t nd = 0;
+  for (auto& s : ss) if (s.recomp) nd += s.rawdiff.size();
+  uint64_t* dof = (uint64_t*)std::malloc((nd + 1) * 8);
+  uint8_t* dva = (uint8_t*)std::malloc(nd + 1);
+  uint64_t k = 0;
+  for (size_t s = 0; s < n; s++) {
+    const StreamState& st = ss[s];
+    atz_result_t& r = res[s];
+    r.clevel = st.c; r.window = st.w; r.memlevel = st.m; r.recomp = st.recomp;
+    r.n_trials = st.trials; r.ident = st.ident; r.first_diff = st.first_diff;
+    r.diff_index = k;
+    r.n_diff = st.recomp ? st.rawdiff.size() : 0;
+    if (st.recomp)
+      for (size_t q = 0; q < st.rawdiff.size(); q++, k++) {
+        dof[k] = q == 0 ? 0 : (uint64_t)st.rawdiff[q] - st.rawdiff[q - 1];
+        dva[k] = st.diffval[q];
+      }
+  }
+  *diff_off = dof; *diff_val = dva; *n_diffs = nd;
+  return ATZ_OK;
+}
+
+int atz_precompress(atz_ctx_t* c, const uint8_t* file, uint64_t len, uint8_t** atz, uint64_t* atz_len,
+                    atz_stats_t* stats) {
+  (void)hipGetLastError();
+  if (!c || (!file && len) || !atz || !atz_len) return ATZ_E_ARG;
+  if (int r = upload(c, c->d_file, file, len)) return r;
+  uint64_t al = 0;
+  if (int r = precompress_dev(c, c->d_file.as<uint8_t>(), file, len, &al, nullptr)) return r;
+  uint8_t* h = (uint8_t*)std::malloc(al + 1);
+  if (!h) return ATZ_E_NOMEM;
+  HIPCHK(hipMemcpy(h, c->d_atz.p, al, hipMemcpyDeviceToHost));
+  *atz = h; *atz_len = al;
+  if (stats) *stats = c->stats;
+  return ATZ_OK;
+}
+
+int atz_precompress_device(atz_ctx_t* c, const uint8_t* d_file, const uint8_t* h_file, uint64_t len,
+                           const uint8_t** d_atz, uint64_t* atz_len, atz_stats_t* stats) {
+  (void)hipGetLastError();
+  if (!c || !d_file || !h_file || !d_atz || !atz_len) return ATZ_E_ARG;
+  uint64_t al = 0;
+  if (int r = precompress_dev(c, d_file, h_file, len, &al, nullptr)) return r;
+  *d_atz = c->d_atz.as<uint8_t>();
+  *atz_len = al;
+  if (stats) *stats = c->stats;
+  return ATZ_OK;
+}
+
+uint64_t atz_deflate_bound(uint64_t n, int window, int memlevel) { return bound(n, window, memlevel); }
+
+int atz_deflate(atz_ctx_t* c, const uint8_t* in, uint64_t in_len, int clevel, int window, int memlevel,
+                uint8_t* out, uint64_t out_cap, uint64_t* out_len) {
+  (void)hipGetLastError();
+  if (!c || (!in && in_len) || !out_len || clevel < 0 || clevel > 9 || window < 8 || window > 15 ||
+      memlevel < 1 || memlevel > 9)
+    return ATZ_E_ARG;
+  if (window == 8) window = 9;
+  std::vector<std::vector<uint8_t>> outs;
+  if (int r = deflate_many(c, {{in, in_len}}, {((uint32_t)clevel << 16) | ((uint32_t)window << 8) | (uint32_t)memlevel}, outs))
+    return r;
+  *out_len = outs[0].size();
+  if (outs[0].size() > out_cap) return ATZ_E_ARG;
+  if (out && !outs[0].empty()) std::memcpy(out, outs[0].data(), outs[0].size());
+  return ATZ_OK;
+}
+
+int atz_deflate_batch(atz_ctx_t* c, const uint8_t* buf, uint64_t len, const uint64_t* offs, const uint64_t* lens,
+                      const uint32_t* params, uint64_t n, uint8_t* out, const uint64_t* out_offs,
+                      const uint64_t* out_caps, uint64_t* out_lens) {
+  (void)hipGetLastError();
+  if (!c || (!buf && len) || !out_lens) return ATZ_E_ARG;
+  std::vector<std::pair<const uint8_t*, uint64_t>> ins(n);
+  std::vector<uint32_t> ps(n);
+  for (uint64_t k = 0; k < n; k++) {
+    if (offs[k] + lens[k] > len) return ATZ_E_ARG;
+    int cl = (int)(params[k] >> 16), w = (int)((params[k] >> 8) & 0xff), m = (int)(params[k] & 0xff);
+    if (cl < 0 || cl > 9 || w < 8 || w > 15 || m < 1 || m > 9) return ATZ_E_ARG;
+    if (w == 8) w = 9;
+    ins[k] = {buf + offs[k], lens[k]};
+    ps[k] = ((uint32_t)cl << 16) | ((uint32_t)w << 8) | (uint32_t)m;
+  }
+  std::vector<std::vector<uint8_t>> outs;
+  if (int r = deflate_many(c, ins, ps, outs)) return r;
+  for (uint64_t k = 0; k < n; k++) {
+    out_lens[k] = outs[k].size();
+    if (outs[k].size() > out_caps[k]) return ATZ_E_ARG;
+    if (!outs[k].empty()) std::memcpy(out + out_offs[k], outs[k].data(), outs[k].size());
+  }
+  return ATZ_OK;
+}
+
+int atz_inflate_batch(atz_ctx_t* c, const uint8_t* buf, uint64_t len, const uint64_t* offs, const uint64_t* lens,
+                      uint64_t n, uint32_t* status, uint64_t* consumed, uint64_t* produced) {
+  (void)hipGetLastError();
+  if (!c || (!buf && len)) return ATZ_E_ARG;
+  if (int r = upload(c, c->d_tmp, buf, len)) return r;
+  std::vector<InfJob> jobs(n);
+  for (uint64_t k = 0; k < n; k++) {
+    if (offs[k] + lens[k] > len) return ATZ_E_ARG;
+    jobs[k].in_off = offs[k]; jobs[k].in_len = lens[k]; jobs[k].out_off = NO_OUT; jobs[k].out_cap = 0;
+  }
+  std::vector<InfRes> res;
+  if (int r = run_inflate_jobs(c, c->d_tmp.as<uint8_t>(), nullptr, jobs, res)) return r;
+  for (uint64_t k = 0; k < n; k++) { status[k] = res[k].status; consumed[k] = res[k].consumed; produced[k] = res[k].produced; }
+  return ATZ_OK;
+}
+
+static uint64_t rd8(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
+
+int atz_reconstruct(atz_ctx_t* c, const uint8_t* atz, uint64_t n, uint8_t** out, uint64_t* out_len) {
+  (void)hipGetLastError();
+  if (!c || !atz || !out || !out_len) return ATZ_E_ARG;
+  if (n < 28 || std::memcmp(atz, "ATZ\1", 4) != 0) return ATZ_E_FORMAT;   // main.cpp:1018-1021
+  if (rd8(atz + 4) != n) return ATZ_E_FORMAT;                              // main.cpp:1022-1025
+  const uint64_t origlen = rd8(atz + 12), nstrms = rd8(atz + 20);
+  std::vector<uint8_t> o;
+  if (nstrms == 0) {
+    if (28 + origlen > n) return ATZ_E_FORMAT;
+    o.assign(atz + 28, atz + 28 + origlen);
+  } else {
+    struct D { uint64_t off, cl, il, nd, fd, dpos, ipos; uint8_t c, w, m; };
+    std::vector<D> d(nstrms);
+    uint64_t lastos = 28;                                                  // main.cpp:1031-1063
+    for (uint64_t j = 0; j < nstrms; j++) {
+      if (lastos + 35 > n) return ATZ_E_FORMAT;
+      d[j].off = rd8(atz + lastos); d[j].cl = rd8(atz + lastos + 8); d[j].il = rd8(atz + lastos + 16);
+      d[j].c = atz[lastos + 24]; d[j].w = atz[lastos + 25]; d[j].m = atz[lastos + 26];
+      d[j].nd = rd8(atz + lastos + 27);
+      if (d[j].nd) {
+        d[j].fd = rd8(atz + lastos + 35); d[j].dpos = lastos + 43; d[j].ipos = 43 + d[j].nd * 9 + lastos;
+        lastos = lastos + 43 + d[j].nd * 9 + d[j].il;
+      } else {
+        d[j].fd = 0; d[j].dpos = 0; d[j].ipos = 35 + lastos;
+        lastos = lastos + 35 + d[j].il;
+      }
+      if (lastos > n) return ATZ_E_FORMAT;
+      if (d[j].c > 9 || d[j].w < 8 || d[j].w > 15 || d[j].m < 1 || d[j].m > 9) return ATZ_E_REF_ABORT;
+    }
+    std::vector<std::pair<const uint8_t*, uint64_t>> ins;
+    std::vector<uint32_t> params;
+    for (auto& x : d) {
+      ins.push_back({atz + x.ipos, x.il});
+      int w = x.w == 8 ? 9 : x.w;
+      params.push_back(((uint32_t)x.c << 16) | ((uint32_t)w << 8) | x.m);
+    }
+    std::vector<std::vector<uint8_t>> defl;
+    if (int r = deflate_many(c, ins, params, defl)) return r;
+    uint64_t residue = lastos, gapsum = 0, lo = 0, ll = 0;
+    for (uint64_t j = 0; j < nstrms; j++) {
+      if (lo + ll != d[j].off) {
+        uint64_t g = d[j].off - (lo + ll);
+        if (residue + gapsum + g > n) return ATZ_E_FORMAT;
+        o.insert(o.end(), atz + residue + gapsum, atz + residue + gapsum + g);
+        gapsum += g;
+      }
+      std::vector<uint8_t>& cb = defl[j];
+      if (cb.size() > d[j].cl + 65535) return ATZ_E_REF_ABORT;            // deflate() != Z_STREAM_END
+      cb.resize(std::max<uint64_t>(cb.size(), d[j].cl), 0);
+      if (d[j].nd) {
+        uint64_t sum = 0;
+        for (uint64_t i = 0; i < d[j].nd; i++) {
+          uint64_t delta = rd8(atz + d[j].dpos + 8 * i);
+          uint64_t at = d[j].fd + delta + sum;
+          if (at < cb.size()) cb[at] = atz[d[j].dpos + 8 * d[j].nd + i];
+          sum += delta;
+        }
+      }
+      o.insert(o.end(), cb.begin(), cb.begin() + d[j].cl);
+      lo = d[j].off; ll = d[j].cl;
+    }
+    if (lo + ll < origlen) {
+      uint64_t t = origlen - (lo + ll);
+      if (residue + gapsum + t > n) return ATZ_E_FORMAT;
+      o.insert(o.end(), atz + residue + gapsum, atz + residue + gapsum + t);
+    }
+  }
+  uint8_t* h = (uint8_t*)std::malloc(o.size() + 1);
+  if (!h) return ATZ_E_NOMEM;
+  if (!o.empty()) std::memcpy(h, o.data(), o.size());
+  *out = h; *out_len = o.size();
+  return ATZ_OK;
+}
+
+}  // extern "C"

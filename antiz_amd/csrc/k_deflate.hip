@@ -1,0 +1,866 @@
+// k_deflate.hip -- zlib 1.2.8-exact deflate trials on CDNA4 (gfx950).
+//
+// The reference's hot loop (testDeflateParams, main.cpp:603-731, ~83 % of its time inside zlib
+// deflate) is re-designed for the GPU in two kernels:
+//
+// k_chains  (one wavefront per (stream, memLevel)): the hash chains of zlib's INSERT_STRING
+//   (Z/deflate.c:181-190) for EVERY position, as a table of u16 distances to the previous
+//   position with the same hash_bits=memLevel+7 rolling hash (0 = none within 32 KiB).  zlib's
+//   rolling hash is a pure function of 3 bytes (3*hash_shift >= hash_bits), and deflate_slow
+//   inserts every position, so these chains are parse-independent and shared by every trial
+//   of the stream at that memLevel; deflate_fast's partial insertion is replayed by skipping
+//   positions a per-trial LDS bitmap marks as not inserted.  Batches of 64 positions are
+//   bitonic-sorted by hash across lanes; only the batch's first/last occurrence per hash touches
+//   the head table.
+//
+// k_trial<KIND>  (one wavefront per (stream, clevel, window, memLevel) trial): replays
+//   deflate_stored/deflate_fast/deflate_slow (Z/deflate.c:1564-1853) on absolute positions --
+//   fill_window and the window slide are reduced to bookkeeping (the slide only matters through
+//   zlib's NIL quirks, which are reproduced) -- walks the chains with longest_match's exact
+//   stop rules (Z/deflate.c:1148-1289), tallies symbols into an HBM symbol buffer and LDS
+//   frequency counters, and at every block flush builds the Huffman trees with zlib's heap,
+//   depth tie-break and overflow fix-up (Z/trees.c:453-699), chooses stored/static/dynamic
+//   (Z/trees.c:907-1004) and bit-packs the block lane-parallel: each lane encodes one symbol,
+//   a wave prefix sum places its bits, LDS atomics assemble the words.  The emitted bytes are
+//   compared positionally against the original stream as they are written, so the reference's
+//   shortcut / size-difference gates (main.cpp:632-681) and "cannot beat the best so far" stop a
+//   trial as early as its outcome is decided.
+#include <hip/hip_runtime.h>
+#include "atz_device.h"
+
+namespace atz {
+
+// ---------------------------------------------------------------------------------------------
+// static tables (trees.c tr_static_init, generated on the host at context creation)
+struct DeflTables {
+  uint16_t st_lcode[288]; uint8_t st_llen[288];
+  uint16_t st_dcode[30];  uint8_t st_dlen[30];
+  uint8_t lcode[256];     // normalized match length -> length code 0..28
+  uint8_t dcode[512];     // d_code()
+  uint16_t lbase[29];
+  uint16_t dbase[30];
+};
+__device__ __constant__ DeflTables c_t;
+__device__ __constant__ uint8_t c_xlb[29] = {0,0,0,0,0,0,0,0,1,1,1,1,2,2,2,2,3,3,3,3,4,4,4,4,5,5,5,5,0};
+__device__ __constant__ uint8_t c_xdb[30] = {0,0,0,0,1,1,2,2,3,3,4,4,5,5,6,6,7,7,8,8,9,9,10,10,11,11,12,12,13,13};
+__device__ __constant__ uint8_t c_xblb[19] = {0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,2,3,7};
+__device__ __constant__ uint8_t c_blorder[19] = {16,17,18,0,8,7,9,6,10,5,11,4,12,3,13,2,14,1,15};
+// configuration_table, Z/deflate.c:131-143: good, lazy, nice, chain
+__device__ __constant__ uint16_t c_cfg[10][4] = {{0,0,0,0},{4,4,8,4},{4,5,16,8},{4,6,32,32},{4,4,16,16},
+    {8,16,32,32},{8,16,128,128},{8,32,128,256},{32,128,258,1024},{32,258,258,4096}};
+
+extern "C" hipError_t atz_upload_defl_tables(const void* host_tables) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_t), host_tables, sizeof(DeflTables));
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_chains
+struct ChainJob {
+  uint64_t infl_off;   // stream bytes in the inflated buffer
+  uint64_t n;          // I_s
+  uint64_t chain_off;  // output offset in u16 units in the chain buffer
+  uint32_t memlevel;
+  uint32_t slot;       // head-table scratch slot
+};
+
+__global__ __launch_bounds__(64) void k_chains(const uint8_t* __restrict__ infl, const ChainJob* __restrict__ jobs,
+                                              uint16_t* __restrict__ chains, uint32_t* __restrict__ heads,
+                                              uint64_t head_slot_words, uint32_t njobs) {
+  const uint32_t j = blockIdx.x;
+  if (j >= njobs) return;
+  const int lane = threadIdx.x;
+  const ChainJob jb = jobs[j];
+  const uint8_t* in = infl + jb.infl_off;
+  uint16_t* out = chains + jb.chain_off;
+  const uint32_t hbits = jb.memlevel + 7, hmask = (1u << hbits) - 1, hshift = (hbits + 2) / 3;
+  uint32_t* head = heads + (uint64_t)jb.slot * head_slot_words;   // stores position+1 (0 = empty)
+  for (uint32_t i = lane; i <= hmask; i += 64) head[i] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  const uint64_t n = jb.n;
+  for (uint64_t base = 0; base < n; base += 64) {
+    const uint64_t p = base + lane;
+    const bool valid = p + 2 < n;
+    uint32_t h = 0x3ffffff;
+    if (valid) h = ((((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask);
+    // bitonic sort of (hash, lane) across the wave
+    uint32_t key = (h << 6) | (uint32_t)lane;
+    for (int k = 2; k <= 64; k <<= 1) {
+      for (int s = k >> 1; s > 0; s >>= 1) {
+        uint32_t o = __shfl_xor(key, s, 64);
+        bool up = (lane & k) == 0;
+        bool lower = (lane & s) == 0;
+        uint32_t mn = key < o ? key : o, mx = key < o ? o : key;
+        key = (lower == up) ? mn : mx;
+      }
+    }
+    const uint32_t kh = key >> 6;
+    const uint64_t mypos = base + (key & 63);
+    uint32_t pk = __shfl_up(key, 1, 64);
+    uint32_t nk = __shfl_down(key, 1, 64);
+    const bool first_of_group = lane == 0 || (pk >> 6) != kh;
+    const bool last_of_group = lane == 63 || (nk >> 6) != kh;
+    const bool real = kh != 0x3ffffff;
+    uint64_t prevpos = 0;  // +1 encoded
+    if (real) {
+      if (first_of_group) prevpos = head[kh];
+      else prevpos = base + (pk & 63) + 1;
+      uint64_t d = prevpos ? mypos - (prevpos - 1) : 0;
+      out[mypos] = (uint16_t)(d && d <= 32768 ? (d == 32768 ? 32768 : d) : 0);
+    } else if (mypos < n) {
+      out[mypos] = 0;
+    }
+    // head updates after all loads of this batch (loads above read the pre-batch heads); the
+    // workgroup-scope acq_rel fences order this wave's HBM store -> later load of another lane
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    if (real && last_of_group) head[kh] = (uint32_t)(mypos + 1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_trial
+static constexpr int NLC = 286, NDC = 30, NBLC = 19, HEAPN = 2 * NLC + 1;
+static constexpr uint32_t LOOKMIN = 262;
+static constexpr uint32_t BITMAP_BITS = 65536;  // fast-mode insertion ring (positions mod 65536)
+
+struct TreeWork {      // one tree under construction (zlib ct_data split into arrays)
+  uint16_t freq[HEAPN];
+  uint16_t dad[HEAPN];
+  uint16_t heap[HEAPN];
+  uint8_t len[HEAPN];
+  uint8_t depth[HEAPN];
+  uint16_t bl_count[16];
+};
+
+struct TrialShared {
+  uint32_t lfreq[NLC];
+  uint32_t dfreq[NDC];
+  uint16_t lcode[NLC]; uint8_t llen[NLC + 2];
+  uint16_t dcode[NDC]; uint8_t dlen[NDC + 2];
+  uint16_t bcode[NBLC]; uint8_t blen[NBLC + 2];
+  uint32_t bfreq[NBLC];
+  TreeWork w;
+  uint32_t stage[112];   // bit-packing staging words (64 symbols x <=48 bits + carry)
+};
+
+struct TrialSharedFast {
+  TrialShared t;
+  uint32_t ins[BITMAP_BITS / 32];
+};
+
+struct SweepArgs {
+  const uint8_t* file;          // original compressed bytes
+  const uint8_t* infl;          // inflated bytes
+  const uint16_t* chains;       // chain links
+  const StreamDev* streams;
+  const Trial* trials;
+  TrialRes* res;
+  uint8_t* out;                 // per-trial output scratch (Trial::out_off)
+  uint32_t* syms;               // symbol buffers (Trial::sym_off)
+  const uint32_t* adler;        // per-stream Adler-32 of the inflated data
+  SweepOpts o;
+  uint32_t ntrials;
+};
+
+struct BitOut {
+  uint8_t* out;
+  uint64_t cap;
+  uint64_t pos;      // bytes written
+  uint64_t bb;       // pending bits (< 8 after every flush)
+  uint32_t bc;
+  // comparison against the original
+  const uint8_t* orig;
+  uint64_t clen;     // C_s
+  uint64_t shortcut; // shortcut length, 0 if the shortcut does not apply
+  uint64_t eq_all;   // equal bytes at positions < min(pos, C_s)
+  uint64_t eq_sc;    // equal bytes at positions < min(pos, shortcut)
+  int overflow;
+};
+
+__device__ inline uint64_t wsum64(uint64_t v) {
+  for (int d = 32; d >= 1; d >>= 1) {
+    uint32_t lo = __shfl_xor((uint32_t)v, d, 64), hi = __shfl_xor((uint32_t)(v >> 32), d, 64);
+    v += ((uint64_t)hi << 32) | lo;
+  }
+  return v;
+}
+
+// write `nb` bytes (lane k supplies byte k via getter semantics: bytes[] in LDS words) -- used by
+// both scalar and lane-parallel emitters.  Compares against the original on the fly.
+__device__ inline void emit_bytes_from_stage(BitOut& b, const uint32_t* stage, uint32_t nb, int lane) {
+  uint64_t eqa = 0, eqs = 0;
+  for (uint32_t k = lane; k < nb; k += 64) {
+    uint8_t x = (uint8_t)(stage[k >> 2] >> (8 * (k & 3)));
+    uint64_t at = b.pos + k;
+    if (at < b.cap) b.out[at] = x;
+    if (at < b.clen) {
+      bool e = b.orig[at] == x;
+      eqa += e;
+      if (at < b.shortcut) eqs += e;
+    }
+  }
+  b.eq_all += wsum64(eqa);
+  b.eq_sc += wsum64(eqs);
+  if (b.pos + nb > b.cap) b.overflow = 1;
+  b.pos += nb;
+}
+
+// scalar emission (block headers, tree descriptions): bits accumulate in bb; whole bytes go out in
+// groups through the staging words.
+__device__ inline void put_bits(BitOut& b, uint32_t* stage, uint32_t v, uint32_t n, int lane) {
+  b.bb |= (uint64_t)v << b.bc;
+  b.bc += n;
+  if (b.bc >= 32) {
+    if (lane == 0) stage[0] = (uint32_t)b.bb;
+    emit_bytes_from_stage(b, stage, 4, lane);
+    b.bb >>= 32;
+    b.bc -= 32;
+  }
+}
+__device__ inline void flush_bits_bytes(BitOut& b, uint32_t* stage, int lane) {  // whole bytes only
+  uint32_t nb = b.bc >> 3;
+  if (!nb) return;
+  if (lane == 0) { stage[0] = (uint32_t)b.bb; stage[1] = (uint32_t)(b.bb >> 32); }
+  emit_bytes_from_stage(b, stage, nb, lane);
+  b.bb = nb >= 8 ? 0 : (b.bb >> (8 * nb));
+  b.bc -= 8 * nb;
+}
+__device__ inline void windup(BitOut& b, uint32_t* stage, int lane) {  // bi_windup
+  flush_bits_bytes(b, stage, lane);
+  if (b.bc) {
+    if (lane == 0) stage[0] = (uint32_t)b.bb;
+    emit_bytes_from_stage(b, stage, 1, lane);
+    b.bb = 0; b.bc = 0;
+  }
+}
+
+// ---- Huffman tree construction, Z/trees.c:453-699 (wave-uniform scalar code) ----
+__device__ inline bool t_smaller(const TreeWork& w, int n, int m) {
+  return w.freq[n] < w.freq[m] || (w.freq[n] == w.freq[m] && w.depth[n] <= w.depth[m]);
+}
+__device__ void pq_down(TreeWork& w, int heap_len, int k) {
+  int v = w.heap[k];
+  int j = k << 1;
+  while (j <= heap_len) {
+    if (j < heap_len && t_smaller(w, w.heap[j + 1], w.heap[j])) j++;
+    if (t_smaller(w, v, w.heap[j])) break;
+    w.heap[k] = w.heap[j];
+    k = j;
+    j <<= 1;
+  }
+  w.heap[k] = (uint16_t)v;
+}
+
+// Builds a tree from w.freq[0..elems).  Leaves' lengths land in w.len; returns max_code.
+// opt/stat accumulate as in gen_bitlen.  stlen: static lengths (or nullptr).
+__device__ int build_tree(TreeWork& w, int elems, int max_length, const uint8_t* xbits, int xbase,
+                          const uint8_t* stlen, uint64_t& opt_len, uint64_t& static_len) {
+  int heap_len = 0, heap_max = HEAPN, max_code = -1, node;
+  for (int n = 0; n < elems; n++) {
+    if (w.freq[n] != 0) { w.heap[++heap_len] = (uint16_t)n; max_code = n; w.depth[n] = 0; }
+    else w.len[n] = 0;
+  }
+  while (heap_len < 2) {
+    node = (max_code < 2 ? ++max_code : 0);
+    w.heap[++heap_len] = (uint16_t)node;
+    w.freq[node] = 1;
+    w.depth[node] = 0;
+    opt_len--;
+    if (stlen) static_len -= stlen[node];
+  }
+  for (int n = heap_len / 2; n >= 1; n--) pq_down(w, heap_len, n);
+  node = elems;
+  do {
+    int n = w.heap[1];
+    w.heap[1] = w.heap[heap_len--];
+    pq_down(w, heap_len, 1);
+    int m = w.heap[1];
+    w.heap[--heap_max] = (uint16_t)n;
+    w.heap[--heap_max] = (uint16_t)m;
+    w.freq[node] = (uint16_t)(w.freq[n] + w.freq[m]);
+    w.depth[node] = (uint8_t)((w.depth[n] >= w.depth[m] ? w.depth[n] : w.depth[m]) + 1);
+    w.dad[n] = w.dad[m] = (uint16_t)node;
+    w.heap[1] = (uint16_t)node++;
+    pq_down(w, heap_len, 1);
+  } while (heap_len >= 2);
+  w.heap[--heap_max] = w.heap[1];
+  // gen_bitlen
+  for (int bits = 0; bits <= 15; bits++) w.bl_count[bits] = 0;
+  w.len[w.heap[heap_max]] = 0;
+  int overflow = 0, h;
+  for (h = heap_max + 1; h < HEAPN; h++) {
+    int n = w.heap[h];
+    int bits = w.len[w.dad[n]] + 1;
+    if (bits > max_length) { bits = max_length; overflow++; }
+    w.len[n] = (uint8_t)bits;
+    if (n > max_code) continue;
+    w.bl_count[bits]++;
+    int xb = (xbits && n >= xbase) ? xbits[n - xbase] : 0;
+    opt_len += (uint64_t)w.freq[n] * (uint64_t)(bits + xb);
+    if (stlen) static_len += (uint64_t)w.freq[n] * (uint64_t)(stlen[n] + xb);
+  }
+  if (overflow) {
+    int bits;
+    do {
+      bits = max_length - 1;
+      while (w.bl_count[bits] == 0) bits--;
+      w.bl_count[bits]--;
+      w.bl_count[bits + 1] += 2;
+      w.bl_count[max_length]--;
+      overflow -= 2;
+    } while (overflow > 0);
+    for (bits = max_length; bits != 0; bits--) {
+      int n = w.bl_count[bits];
+      while (n != 0) {
+        int m = w.heap[--h];
+        if (m > max_code) continue;
+        if (w.len[m] != bits) {
+          opt_len += (uint64_t)((int64_t)bits - (int64_t)w.len[m]) * (uint64_t)w.freq[m];
+          w.len[m] = (uint8_t)bits;
+        }
+        n--;
+      }
+    }
+  }
+  return max_code;
+}
+
+// gen_codes (Z/trees.c:575-607) from w.len/w.bl_count into codes/lens
+__device__ void gen_codes(const TreeWork& w, int max_code, uint16_t* codes, uint8_t* lens) {
+  uint32_t next[16];
+  uint32_t code = 0;
+  next[0] = 0;
+  for (int bits = 1; bits <= 15; bits++) { code = (code + w.bl_count[bits - 1]) << 1; next[bits] = code; }
+  for (int n = 0; n <= max_code; n++) {
+    int l = w.len[n];
+    lens[n] = (uint8_t)l;
+    if (!l) continue;
+    codes[n] = (uint16_t)(__builtin_bitreverse32(next[l]++) >> (32 - l));
+  }
+}
+
+__device__ inline int tl(const uint8_t* ln, int n, int guard) { return n == guard ? 0xffff : ln[n]; }
+
+__device__ void scan_tree(uint32_t* bfreq, const uint8_t* ln, int max_code) {  // Z/trees.c:705-748
+  int prevlen = -1, curlen, nextlen = ln[0], count = 0, max_count = 7, min_count = 4;
+  int guard = max_code + 1;
+  if (nextlen == 0) { max_count = 138; min_count = 3; }
+  for (int n = 0; n <= max_code; n++) {
+    curlen = nextlen; nextlen = tl(ln, n + 1, guard);
+    if (++count < max_count && curlen == nextlen) continue;
+    else if (count < min_count) bfreq[curlen] += (uint32_t)count;
+    else if (curlen != 0) { if (curlen != prevlen) bfreq[curlen]++; bfreq[16]++; }
+    else if (count <= 10) bfreq[17]++;
+    else bfreq[18]++;
+    count = 0; prevlen = curlen;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+    else { max_count = 7; min_count = 4; }
+  }
+}
+
+__device__ void send_tree(BitOut& b, TrialShared& s, const uint8_t* ln, int max_code, int lane) {
+  int prevlen = -1, curlen, nextlen = ln[0], count = 0, max_count = 7, min_count = 4;
+  int guard = max_code + 1;
+  if (nextlen == 0) { max_count = 138; min_count = 3; }
+  for (int n = 0; n <= max_code; n++) {
+    curlen = nextlen; nextlen = tl(ln, n + 1, guard);
+    if (++count < max_count && curlen == nextlen) continue;
+    else if (count < min_count) {
+      do { put_bits(b, s.stage, s.bcode[curlen], s.blen[curlen], lane); } while (--count != 0);
+    } else if (curlen != 0) {
+      if (curlen != prevlen) { put_bits(b, s.stage, s.bcode[curlen], s.blen[curlen], lane); count--; }
+      put_bits(b, s.stage, s.bcode[16], s.blen[16], lane);
+      put_bits(b, s.stage, (uint32_t)(count - 3), 2, lane);
+    } else if (count <= 10) {
+      put_bits(b, s.stage, s.bcode[17], s.blen[17], lane);
+      put_bits(b, s.stage, (uint32_t)(count - 3), 3, lane);
+    } else {
+      put_bits(b, s.stage, s.bcode[18], s.blen[18], lane);
+      put_bits(b, s.stage, (uint32_t)(count - 11), 7, lane);
+    }
+    count = 0; prevlen = curlen;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+    else { max_count = 7; min_count = 4; }
+  }
+}
+
+__device__ inline uint32_t d_code(uint32_t d) { return d < 256 ? c_t.dcode[d] : c_t.dcode[256 + (d >> 7)]; }
+
+// Lane-parallel compress_block (Z/trees.c:1060-1105): 64 symbols per step.
+__device__ void compress_block(BitOut& b, TrialShared& s, const uint32_t* syms, uint32_t nsym,
+                               const uint16_t* lc, const uint8_t* ll, const uint16_t* dc, const uint8_t* dl,
+                               int lane) {
+  // the symbols were stored by lane 0 during the parse: order those HBM stores before the reads
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  for (uint32_t base = 0; base <= nsym; base += 64) {
+    uint32_t k = base + lane;
+    uint64_t v = 0;
+    uint32_t nb = 0;
+    if (k < nsym) {
+      uint32_t sy = syms[k];
+      uint32_t dist = sy >> 8, c = sy & 0xff;
+      if (dist == 0) {
+        v = lc[c]; nb = ll[c];
+      } else {
+        uint32_t code = c_t.lcode[c];
+        v = lc[code + 257]; nb = ll[code + 257];
+        uint32_t xe = c_xlb[code];
+        if (xe) { v |= (uint64_t)(c - c_t.lbase[code]) << nb; nb += xe; }
+        dist--;
+        uint32_t dcd = d_code(dist);
+        v |= (uint64_t)dc[dcd] << nb; nb += dl[dcd];
+        uint32_t xd = c_xdb[dcd];
+        if (xd) { v |= (uint64_t)(dist - c_t.dbase[dcd]) << nb; nb += xd; }
+      }
+    } else if (k == nsym) {
+      v = lc[256]; nb = ll[256];   // END_BLOCK
+    }
+    // exclusive prefix sum of bit lengths
+    uint32_t incl = nb;
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t t = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += t;
+    }
+    uint32_t total = __shfl(incl, 63, 64);
+    if (total == 0) break;
+    // stage words: word 0..1 seeded with the pending bits
+    for (int i = lane; i < 112; i += 64) s.stage[i] = 0;
+    if (lane == 0) { s.stage[0] = (uint32_t)b.bb; s.stage[1] = (uint32_t)(b.bb >> 32); }
+    uint32_t off = b.bc + incl - nb;
+    if (nb) {
+      uint32_t wi = off >> 5, sh = off & 31;
+      uint64_t lo = v << sh;                       // bits 0..63 of the shifted value
+      uint32_t hi = sh ? (uint32_t)(v >> (64 - sh)) : 0;
+      atomicOr(&s.stage[wi], (uint32_t)lo);
+      if ((uint32_t)(lo >> 32)) atomicOr(&s.stage[wi + 1], (uint32_t)(lo >> 32));
+      if (hi) atomicOr(&s.stage[wi + 2], hi);
+    }
+    uint32_t all = b.bc + total;
+    uint32_t full = all >> 3;
+    emit_bytes_from_stage(b, s.stage, full, lane);
+    uint32_t rem = all & 7;
+    uint32_t lastw = s.stage[full >> 2];
+    b.bb = rem ? ((lastw >> (8 * (full & 3))) & 0xff) & ((1u << rem) - 1) : 0;
+    b.bc = rem;
+  }
+}
+
+struct Lz {
+  // parameters
+  uint32_t level, kind, wsize, maxdist, lbs, good, lazy, nice, chain;
+  // absolute-position state
+  uint64_t n;           // I_s
+  uint64_t p;           // strstart
+  uint64_t lookahead;
+  uint64_t S;           // total window slide
+  int64_t block_start;  // absolute
+  uint64_t match_start, prev_match;
+  uint32_t match_length, prev_length;
+  int match_available;
+  uint32_t last_lit;
+  uint64_t ins_cleared;  // fast mode: bitmap cleared up to (exclusive)
+  uint64_t nsym;
+};
+
+// fill_window bookkeeping (Z/deflate.c:1390-1532) on absolute positions
+__device__ inline void fill(Lz& z) {
+  do {
+    uint64_t sw = z.p - z.S;
+    uint64_t more = 2ull * z.wsize - z.lookahead - sw;
+    if (sw >= (uint64_t)z.wsize + z.maxdist) { z.S += z.wsize; more += z.wsize; }
+    uint64_t rd = z.p + z.lookahead;
+    if (rd >= z.n) break;
+    uint64_t k = z.n - rd;
+    if (k > more) k = more;
+    z.lookahead += k;
+  } while (z.lookahead < LOOKMIN && z.p + z.lookahead < z.n);
+}
+
+// common prefix length of in[a..] and in[b..] starting at offset `from`, capped at `cap` (lanes)
+__device__ inline uint32_t common_len(const uint8_t* in, uint64_t a, uint64_t b, uint32_t from, uint32_t cap,
+                                      int lane) {
+  for (uint32_t k0 = from; k0 < cap; k0 += 64) {
+    uint32_t k = k0 + lane;
+    bool ne = k < cap && in[a + k] != in[b + k];
+    if (k >= cap) ne = true;
+    uint64_t m = __ballot(ne);
+    if (m) {
+      uint32_t f = k0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+      return f < cap ? f : cap;
+    }
+  }
+  return cap;
+}
+
+template <int KIND>
+__device__ inline bool is_inserted(const uint32_t* ins, uint64_t q) {
+  if (KIND != 1) return true;
+  uint32_t b = (uint32_t)(q & (BITMAP_BITS - 1));
+  return (ins[b >> 5] >> (b & 31)) & 1;
+}
+
+// longest_match on the shared chains (Z/deflate.c:1148-1289).  Returns match length; sets z.match_start.
+template <int KIND>
+__device__ uint32_t longest_match(Lz& z, const uint8_t* in, const uint16_t* ch, const uint32_t* ins,
+                                  uint64_t cur, int lane) {
+  uint32_t chain = z.chain;
+  const uint64_t p = z.p;
+  uint32_t best = z.prev_length;
+  uint32_t nice = z.nice;
+  if (z.prev_length >= z.good) chain >>= 2;
+  if (nice > z.lookahead) nice = (uint32_t)z.lookahead;
+  // continue while next > limit (window limit translated to absolute positions)
+  const uint64_t sw = p - z.S;
+  const uint64_t limit = sw > z.maxdist ? p - z.maxdist : z.S;
+  const uint64_t avail = z.n - p;                       // bytes left in the input
+  const uint32_t cap = avail < 258 ? (uint32_t)avail : 258u;
+  for (;;) {
+    // quick reject: match[best], match[best-1], match[0], match[1] (bytes past the input read as 0)
+    uint8_t se0 = p + best < z.n ? in[p + best] : 0;
+    uint8_t se1 = p + best - 1 < z.n ? in[p + best - 1] : 0;
+    uint8_t m0 = cur + best < z.n ? in[cur + best] : 0;
+    uint8_t m1 = cur + best - 1 < z.n ? in[cur + best - 1] : 0;
+    if (m0 == se0 && m1 == se1 && in[cur] == in[p] && in[cur + 1] == in[p + 1]) {
+      uint32_t len = common_len(in, cur, p, 2, cap, lane);
+      if (len > best) {
+        z.match_start = cur;
+        best = len;
+        if (len >= nice) break;
+      }
+    }
+    // next link on the chain (skipping positions deflate_fast did not insert)
+    uint64_t nx = cur;
+    bool stop = false;
+    for (;;) {
+      uint32_t d = ch[nx];
+      if (!d || nx < d) { stop = true; break; }
+      nx -= d;
+      if (nx <= limit) { stop = true; break; }
+      if (is_inserted<KIND>(ins, nx)) break;
+    }
+    if (stop || --chain == 0) break;
+    cur = nx;
+  }
+  return best <= z.lookahead ? best : (uint32_t)z.lookahead;
+}
+
+struct BlockCtx {
+  TrialShared* s;
+  uint32_t* syms;
+  const uint8_t* in;
+  BitOut* b;
+};
+
+// _tr_flush_block (Z/trees.c:907-1004) + FLUSH_BLOCK_ONLY bookkeeping
+__device__ void flush_block(Lz& z, BlockCtx& bc, int last, uint32_t& hazard, int lane) {
+  TrialShared& s = *bc.s;
+  BitOut& b = *bc.b;
+  const bool bufok = z.block_start >= (int64_t)z.S;
+  const uint64_t stored_len = (uint64_t)((int64_t)z.p - z.block_start);
+  uint64_t opt_len = 0, static_len = 0, opt_lenb, static_lenb;
+  int lmax = 0, dmax = 0, max_blindex = 0;
+  if (z.level > 0) {
+    // literal/length tree
+    for (int i = lane; i < NLC; i += 64) s.w.freq[i] = (uint16_t)s.lfreq[i];
+    lmax = build_tree(s.w, NLC, 15, c_xlb, 257, c_t.st_llen, opt_len, static_len);
+    gen_codes(s.w, lmax, s.lcode, s.llen);
+    for (int i = lmax + 1 + lane; i < NLC + 2; i += 64) s.llen[i] = 0;
+    // distance tree
+    for (int i = lane; i < NDC; i += 64) s.w.freq[i] = (uint16_t)s.dfreq[i];
+    dmax = build_tree(s.w, NDC, 15, c_xdb, 0, c_t.st_dlen, opt_len, static_len);
+    gen_codes(s.w, dmax, s.dcode, s.dlen);
+    for (int i = dmax + 1 + lane; i < NDC + 2; i += 64) s.dlen[i] = 0;
+    // bit length tree
+    for (int i = lane; i < NBLC; i += 64) s.bfreq[i] = 0;
+    if (lane == 0) { scan_tree(s.bfreq, s.llen, lmax); scan_tree(s.bfreq, s.dlen, dmax); }
+    for (int i = lane; i < NBLC; i += 64) s.w.freq[i] = (uint16_t)s.bfreq[i];
+    int bmax = build_tree(s.w, NBLC, 7, c_xblb, 0, nullptr, opt_len, static_len);
+    gen_codes(s.w, bmax, s.bcode, s.blen);
+    for (int i = bmax + 1 + lane; i < NBLC + 2; i += 64) s.blen[i] = 0;
+    for (max_blindex = NBLC - 1; max_blindex >= 3; max_blindex--)
+      if (s.blen[c_blorder[max_blindex]] != 0) break;
+    opt_len += 3 * ((uint64_t)max_blindex + 1) + 5 + 5 + 4;
+    opt_lenb = (opt_len + 3 + 7) >> 3;
+    static_lenb = (static_len + 3 + 7) >> 3;
+    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+  } else {
+    opt_lenb = static_lenb = stored_len + 5;
+  }
+  const uint64_t blk_start_bytes = b.pos;
+  if (stored_len + 4 <= opt_lenb && bufok) {
+    put_bits(b, s.stage, (uint32_t)last, 3, lane);
+    windup(b, s.stage, lane);
+    uint32_t len = (uint32_t)stored_len;
+    put_bits(b, s.stage, (len & 0xffff) | ((~len & 0xffff) << 16), 32, lane);
+    // copy the block's input bytes (now byte aligned, bc == 0)
+    const uint8_t* src = bc.in + z.block_start;
+    for (uint64_t o = 0; o < stored_len; o += 256) {
+      uint32_t nb = stored_len - o < 256 ? (uint32_t)(stored_len - o) : 256u;
+      for (uint32_t k = lane; k < 64; k += 64) {
+        uint32_t wv = 0;
+        for (int q = 0; q < 4; q++) {
+          uint32_t at = 4 * k + q;
+          if (at < nb) wv |= (uint32_t)src[o + at] << (8 * q);
+        }
+        s.stage[k] = wv;
+      }
+      emit_bytes_from_stage(b, s.stage, nb, lane);
+    }
+  } else if (static_lenb == opt_lenb) {
+    put_bits(b, s.stage, (1u << 1) + (uint32_t)last, 3, lane);
+    compress_block(b, s, bc.syms, z.last_lit, c_t.st_lcode, c_t.st_llen, c_t.st_dcode, c_t.st_dlen, lane);
+  } else {
+    int lcodes = lmax + 1, dcodes = dmax + 1, blcodes = max_blindex + 1;
+    put_bits(b, s.stage, (2u << 1) + (uint32_t)last, 3, lane);
+    put_bits(b, s.stage, (uint32_t)(lcodes - 257), 5, lane);
+    put_bits(b, s.stage, (uint32_t)(dcodes - 1), 5, lane);
+    put_bits(b, s.stage, (uint32_t)(blcodes - 4), 4, lane);
+    for (int r = 0; r < blcodes; r++) put_bits(b, s.stage, s.blen[c_blorder[r]], 3, lane);
+    send_tree(b, s, s.llen, lcodes - 1, lane);
+    send_tree(b, s, s.dlen, dcodes - 1, lane);
+    flush_bits_bytes(b, s.stage, lane);
+    compress_block(b, s, bc.syms, z.last_lit, s.lcode, s.llen, s.dcode, s.dlen, lane);
+  }
+  // 1.2.8 pending_buf/d_buf overlay condition (conservative, cf. oracle/ora_deflate.c)
+  if (b.pos - blk_start_bytes > (uint64_t)z.lbs + 2ull * z.last_lit && z.last_lit) hazard = 1;
+  // init_block
+  for (int i = lane; i < NLC; i += 64) s.lfreq[i] = 0;
+  for (int i = lane; i < NDC; i += 64) s.dfreq[i] = 0;
+  if (lane == 0) s.lfreq[256] = 1;
+  z.last_lit = 0;
+  if (last) windup(b, s.stage, lane);
+  z.block_start = (int64_t)z.p;
+}
+
+__device__ inline bool tally_lit(Lz& z, BlockCtx& bc, uint32_t c, int lane) {
+  if (lane == 0) { bc.syms[z.last_lit] = c; bc.s->lfreq[c]++; }
+  z.last_lit++; z.nsym++;
+  return z.last_lit == z.lbs - 1;
+}
+__device__ inline bool tally_dist(Lz& z, BlockCtx& bc, uint32_t dist, uint32_t len, int lane) {
+  if (lane == 0) {
+    bc.syms[z.last_lit] = (dist << 8) | len;
+    bc.s->lfreq[c_t.lcode[len] + 257]++;
+    bc.s->dfreq[d_code(dist - 1)]++;
+  }
+  z.last_lit++; z.nsym++;
+  return z.last_lit == z.lbs - 1;
+}
+
+// Early-exit test after output progress: returns TR_* state to stop with, or ~0u to continue.
+__device__ inline uint32_t early_exit(const BitOut& b, const SweepOpts& o, uint64_t best_ident, bool full_needed) {
+  if (b.overflow) return TR_OVERFLOW;
+  if (full_needed) return ~0u;
+  if (b.shortcut) {
+    uint64_t seen = b.pos < b.shortcut ? b.pos : b.shortcut;
+    uint64_t mism = seen - b.eq_sc;
+    uint64_t thr = o.shortcut_len - o.recomp_tresh;   // uint64 wrap as in main.cpp:649
+    if (thr > b.shortcut || mism > b.shortcut - thr) return TR_SHORTCUT;
+  }
+  if (b.pos > b.clen + o.sizediff_tresh) return TR_SIZEDIFF;
+  uint64_t seen = b.pos < b.clen ? b.pos : b.clen;
+  if (b.clen - (seen - b.eq_all) <= best_ident) return TR_CANT_BEAT;
+  return ~0u;
+}
+
+template <int KIND, typename SH>
+__device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
+  TrialShared& s = shm.t;
+  const uint32_t t = blockIdx.x;
+  const Trial tr = A.trials[t];
+  const StreamDev sd = A.streams[tr.stream];
+  const uint8_t* in = A.infl + sd.infl_off;
+  const uint16_t* ch = KIND == 0 ? nullptr : A.chains + tr.chain_off;
+  uint32_t* ins = nullptr;
+  if constexpr (KIND == 1) ins = shm.ins;
+  const bool full_needed = tr.mode & 1;
+  Lz z;
+  z.level = tr.clevel; z.kind = KIND;
+  z.wsize = 1u << tr.window; z.maxdist = z.wsize - LOOKMIN; z.lbs = 1u << (tr.memlevel + 6);
+  z.good = c_cfg[z.level][0]; z.lazy = c_cfg[z.level][1]; z.nice = c_cfg[z.level][2]; z.chain = c_cfg[z.level][3];
+  z.n = sd.infl_len; z.p = 0; z.lookahead = 0; z.S = 0; z.block_start = 0;
+  z.match_start = 0; z.prev_match = 0; z.match_length = 2; z.prev_length = 2; z.match_available = 0;
+  z.last_lit = 0; z.ins_cleared = 0; z.nsym = 0;
+  BitOut b;
+  b.out = A.out + tr.out_off; b.cap = tr.out_cap; b.pos = 0; b.bb = 0; b.bc = 0;
+  b.orig = A.file + sd.orig_off; b.clen = sd.comp_len;
+  b.shortcut = sd.comp_len > A.o.shortcut_len ? A.o.shortcut_len : 0;
+  b.eq_all = 0; b.eq_sc = 0; b.overflow = 0;
+  BlockCtx bcx;
+  bcx.s = &s; bcx.syms = A.syms + tr.sym_off; bcx.in = in; bcx.b = &b;
+  for (int i = lane; i < NLC; i += 64) s.lfreq[i] = 0;
+  for (int i = lane; i < NDC; i += 64) s.dfreq[i] = 0;
+  if (lane == 0) s.lfreq[256] = 1;
+  if constexpr (KIND == 1) { for (int i = lane; i < (int)(BITMAP_BITS / 32); i += 64) ins[i] = 0; }
+  uint32_t hazard = 0;
+  uint32_t state = ~0u;
+  // zlib header (Z/deflate.c:738-759)
+  {
+    uint32_t header = (8u + ((uint32_t)(tr.window - 8) << 4)) << 8;
+    uint32_t lf = z.level < 2 ? 0 : z.level < 6 ? 1 : z.level == 6 ? 2 : 3;
+    header |= lf << 6;
+    header += 31 - (header % 31);
+    put_bits(b, s.stage, ((header >> 8) & 0xff) | ((header & 0xff) << 8), 16, lane);
+  }
+  if (KIND == 0) {
+    // deflate_stored (Z/deflate.c:1564-1619)
+    uint64_t max_block = 0xffff;
+    if (max_block > 4ull * z.lbs - 5) max_block = 4ull * z.lbs - 5;
+    for (;;) {
+      if (z.lookahead <= 1) { fill(z); if (z.lookahead == 0) break; }
+      z.p += z.lookahead;
+      z.lookahead = 0;
+      uint64_t max_start = (uint64_t)z.block_start + max_block;
+      if (z.p == 0 || z.p >= max_start) {
+        z.lookahead = z.p - max_start;
+        z.p = max_start;
+        flush_block(z, bcx, 0, hazard, lane);
+        state = early_exit(b, A.o, tr.best_ident, full_needed);
+        if (state != ~0u) break;
+      }
+      if (z.p - (uint64_t)z.block_start >= z.maxdist) {
+        flush_block(z, bcx, 0, hazard, lane);
+        state = early_exit(b, A.o, tr.best_ident, full_needed);
+        if (state != ~0u) break;
+      }
+    }
+  } else if (KIND == 1) {
+    // deflate_fast (Z/deflate.c:1628-1722)
+    for (;;) {
+      if (z.lookahead < LOOKMIN) { fill(z); if (z.lookahead == 0) break; }
+      uint64_t hh = 0; bool hv = false;
+      // clear the insertion ring ahead of the positions about to be inserted
+      while (z.ins_cleared < z.p + 300) {
+        uint32_t wbase = (uint32_t)((z.ins_cleared & (BITMAP_BITS - 1)) >> 5);
+        for (int i = lane; i < 32; i += 64) ins[(wbase + i) & (BITMAP_BITS / 32 - 1)] = 0;
+        z.ins_cleared += 1024;
+      }
+      if (z.lookahead >= 3) {
+        if (lane == 0) { uint32_t bq = (uint32_t)(z.p & (BITMAP_BITS - 1)); atomicOr(&ins[bq >> 5], 1u << (bq & 31)); }
+        // head[] = most recent inserted same-hash position
+        uint64_t q = z.p;
+        for (;;) {
+          uint32_t d = ch[q];
+          if (!d || q < d) break;
+          q -= d;
+          if (z.p - q > z.maxdist) break;
+          if (is_inserted<1>(ins, q)) { hh = q; hv = q > z.S; break; }
+        }
+      }
+      if (hv && z.p - hh <= z.maxdist) z.match_length = longest_match<1>(z, in, ch, ins, hh, lane);
+      bool bflush;
+      if (z.match_length >= 3) {
+        bflush = tally_dist(z, bcx, (uint32_t)(z.p - z.match_start), z.match_length - 3, lane);
+        z.lookahead -= z.match_length;
+        if (z.match_length <= z.lazy && z.lookahead >= 3) {
+          if (lane == 0) {
+            for (uint32_t k = 1; k < z.match_length; k++) {
+              uint32_t bq = (uint32_t)((z.p + k) & (BITMAP_BITS - 1));
+              atomicOr(&ins[bq >> 5], 1u << (bq & 31));
+            }
+          }
+        }
+        z.p += z.match_length;
+        z.match_length = 0;
+      } else {
+        bflush = tally_lit(z, bcx, in[z.p], lane);
+        z.lookahead--;
+        z.p++;
+      }
+      if (bflush) {
+        flush_block(z, bcx, 0, hazard, lane);
+        state = early_exit(b, A.o, tr.best_ident, full_needed);
+        if (state != ~0u) break;
+      }
+    }
+  } else {
+    // deflate_slow (Z/deflate.c:1730-1853)
+    for (;;) {
+      if (z.lookahead < LOOKMIN) { fill(z); if (z.lookahead == 0) break; }
+      uint64_t hh = 0; bool hv = false;
+      if (z.lookahead >= 3) {
+        uint32_t d = ch[z.p];
+        if (d && z.p >= d) { hh = z.p - d; hv = hh > z.S; }
+      }
+      z.prev_length = z.match_length; z.prev_match = z.match_start;
+      z.match_length = 2;
+      if (hv && z.prev_length < z.lazy && z.p - hh <= z.maxdist) {
+        z.match_length = longest_match<2>(z, in, ch, nullptr, hh, lane);
+        if (z.match_length == 3 && z.p - z.match_start > 4096) z.match_length = 2;
+      }
+      if (z.prev_length >= 3 && z.match_length <= z.prev_length) {
+        bool bflush = tally_dist(z, bcx, (uint32_t)(z.p - 1 - z.prev_match), z.prev_length - 3, lane);
+        z.lookahead -= z.prev_length - 1;
+        z.p += z.prev_length - 1;
+        z.match_available = 0;
+        z.match_length = 2;
+        if (bflush) {
+          flush_block(z, bcx, 0, hazard, lane);
+          state = early_exit(b, A.o, tr.best_ident, full_needed);
+          if (state != ~0u) break;
+        }
+      } else if (z.match_available) {
+        bool bflush = tally_lit(z, bcx, in[z.p - 1], lane);
+        if (bflush) {
+          flush_block(z, bcx, 0, hazard, lane);
+          state = early_exit(b, A.o, tr.best_ident, full_needed);
+          if (state != ~0u) break;
+        }
+        z.p++;
+        z.lookahead--;
+      } else {
+        z.match_available = 1;
+        z.p++;
+        z.lookahead--;
+      }
+    }
+    if (state == ~0u && z.match_available) { tally_lit(z, bcx, in[z.p - 1], lane); z.match_available = 0; }
+  }
+  if (state == ~0u) {
+    flush_block(z, bcx, 1, hazard, lane);
+    // adler32 trailer
+    uint32_t ad = A.adler[tr.stream];
+    uint32_t be = ((ad >> 24) & 0xff) | ((ad >> 8) & 0xff00) | ((ad << 8) & 0xff0000) | (ad << 24);
+    put_bits(b, s.stage, be, 32, lane);
+    flush_bits_bytes(b, s.stage, lane);
+    // final gates (main.cpp:632-681)
+    if (b.overflow) state = TR_OVERFLOW;
+    else if (full_needed) state = TR_FULL;
+    else {
+      uint64_t thr = A.o.shortcut_len - A.o.recomp_tresh;
+      uint64_t L = b.pos;
+      int64_t dd = (int64_t)(L - b.clen);
+      uint64_t ad2 = (uint64_t)(dd < 0 ? -dd : dd);
+      if (b.shortcut && b.eq_sc < thr) state = TR_SHORTCUT;
+      else if (ad2 > A.o.sizediff_tresh) state = TR_SIZEDIFF;
+      else state = TR_FULL;
+    }
+  }
+  if (lane == 0) {
+    TrialRes r;
+    r.state = state;
+    r.flags = hazard | (b.shortcut ? 2u : 0u);
+    r.out_len = b.pos;
+    r.ident = b.eq_all;
+    r.symbols = z.nsym;
+    r.parsed = z.p;
+    A.res[t] = r;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_trial_stored(SweepArgs A) {
+  __shared__ struct { TrialShared t; } shm;
+  trial_body<0>(A, shm, threadIdx.x);
+}
+__global__ __launch_bounds__(64) void k_trial_fast(SweepArgs A) {
+  __shared__ TrialSharedFast shm;
+  trial_body<1>(A, shm, threadIdx.x);
+}
+__global__ __launch_bounds__(64) void k_trial_slow(SweepArgs A) {
+  __shared__ struct { TrialShared t; } shm;
+  trial_body<2>(A, shm, threadIdx.x);
+}
+
+}  // namespace atz

@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""bench.py -- input MB/s precompressed on MI355X (BASELINE.json metric), one JSON line on rank 0.
+
+Workload (BASELINE.json configs[3]): 1 GB synthetic file, 100 000 zlib streams,
+clevel U{1..9} x memLevel U{1..9}, w15, ~10 KB compressed each, 0-64 B random gaps, seed 4.
+A step = one full precompress (Phase 1 scan+inflate, Phase 3 parameter sweep, Phase 4 ATZ1 assembly)
+of that file, input already resident in HBM, ATZ1 output assembled in HBM.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the path shards by
+stream/file with no data-path exchange, so every rank precompresses its own 1 GB shard (seed 4 + rank;
+rank 0's shard is the single-GPU workload) -- weak scaling; the only collectives are the barrier and
+the max-over-ranks of the step time (plus an all_gather of per-rank ATZ sizes: the shard index).
+
+roofline: the dominant kernel (k_trial_*: deflate trials) -- achieved = algorithmic bytes
+(trial input read + compare read, summed over the launches) / the kernels' summed
+device time (HIP events recorded inside libatz_accel on its own stream), peak = MI355X HBM 8 TB/s.
+cpu_baseline: the REAL reference (oracle/_ref/uncomp, built from /root/reference) on a bounded
+sample of the same workload (first seed, fewer streams), 1 core, --notest.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(n_streams, seed):
+    """Time the real reference binary on a bounded sample of the workload (1 thread)."""
+    from antiz_amd import datagen
+    ref = os.path.join(ROOT, "oracle", "_ref", "uncomp")
+    if not os.path.exists(ref):
+        return None
+    data = datagen.gen_c4(seed=seed, n_streams=n_streams)
+    d = tempfile.mkdtemp(prefix="atzcpu")
+    p = os.path.join(d, "sample.bin")
+    with open(p, "wb") as f:
+        f.write(data)
+    cmd = [ref, "-i", p, "-o", p + ".atz", "--notest"]
+    try:
+        cmd = ["taskset", "-c", "0"] + cmd if subprocess.run(["which", "taskset"], capture_output=True).returncode == 0 else cmd
+        t0 = time.perf_counter()
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        dt = time.perf_counter() - t0
+        ok = r.returncode == 0
+    finally:
+        for fn in (p, p + ".atz"):
+            if os.path.exists(fn):
+                os.remove(fn)
+        os.rmdir(d)
+    if not ok:
+        return None
+    return {"value": round(len(data) / 1e6 / dt, 4), "unit": "MB/s", "cores": 1, "kind": "reference",
+            "sample": "%d-stream prefix config of the same generator (%.1f MB, seed %d), oracle/_ref/uncomp --notest, "
+                      "%.1f s wall" % (n_streams, len(data) / 1e6, seed, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--streams", type=int, default=100000, help="streams per rank (C4: 100000 = 1 GB)")
+    ap.add_argument("--cpu-sample-streams", type=int, default=3000)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cache", default=os.environ.get("ATZ_BENCH_CACHE", "/tmp/atz_bench_cache"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import antiz_amd
+    from antiz_amd import datagen
+
+    seed = 4 + rank
+    t0 = time.time()
+    path = datagen.cached("c4", args.cache, seed=seed, n_streams=args.streams)
+    with open(path, "rb") as f:
+        data = f.read()
+    log("rank %d: workload %s (%.1f MB) ready in %.1fs" % (rank, os.path.basename(path), len(data) / 1e6, time.time() - t0))
+    # input resident in HBM before the timed region (+4 KiB slack the kernels may over-read)
+    host = torch.frombuffer(bytearray(data) + bytearray(4096), dtype=torch.uint8)
+    dev = host.to("cuda", non_blocking=False)
+    torch.cuda.synchronize()
+
+    ctx = antiz_amd.Context(device=local)
+
+    def step():
+        dptr, n, st = ctx.precompress_device(dev.data_ptr(), data)
+        return n, st
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        n, st = step()
+        stats.append(st)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tmax = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    sizes = torch.tensor([float(n)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        gathered = [torch.zeros_like(sizes) for _ in range(world)]
+        dist.all_gather(gathered, sizes)
+    dt = float(tmax.item())
+    ms_per_step = dt * 1000.0 / args.steps
+    total_bytes = len(data) * world          # every rank: one shard of the same size per step
+    value = total_bytes / 1e6 / (dt / args.steps)
+
+    last = stats[-1]
+    ktime = last["k_trial_ms"] / 1000.0
+    alg = last["k_trial_alg_bytes"]
+    achieved = alg / ktime / 1e9 if ktime > 0 else 0.0
+    launches = max(1, last["k_trial_launches"])
+    roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+            "kernel": "k_trial_{stored,fast,slow}", "launches": last["k_trial_launches"],
+            "avg_launch_ms": round(last["k_trial_ms"] / launches, 4),
+            "alg_bytes_per_launch": int(alg / launches)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.cpu_sample_streams, seed)
+
+    if rank == 0:
+        out = {
+            "metric": "input MB/s precompressed (1 GB synthetic, 100k streams) at 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "MB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (antiz_amd.datagen C4, seed 4+rank; text from a seeded 20k-word vocabulary)",
+            "config": {"workload": "C4: %d zlib streams (clevel U1-9, memLevel U1-9, w15), %.3f GB per GPU, "
+                                   "default thresholds" % (args.streams, len(data) / 1e9),
+                       "streams_per_gpu": args.streams, "bytes_per_gpu": len(data), "parallelism": "stream-sharded dp%d" % world},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "detail": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in last.items()},
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

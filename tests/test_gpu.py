@@ -1,0 +1,182 @@
+"""Parity of the MI355X product (libatz_accel.so, HIP) with the oracle and the reference's golden vectors.
+
+Run on the GPU box: python -m pytest tests -m gpu.  Every test calls through the C ABI
+(include/atz_accel.h); integer/byte work must be bit-exact.
+"""
+import hashlib
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import _libs
+import golden_cases as G
+
+pytestmark = pytest.mark.gpu
+
+GOLD = G.GOLD
+HDRS = [0x2815, 0x2853, 0x2891, 0x28cf, 0x3811, 0x384f, 0x388d, 0x38cb, 0x480d, 0x484b, 0x4889, 0x48c7,
+        0x5809, 0x5847, 0x5885, 0x58c3, 0x6805, 0x6843, 0x6881, 0x68de, 0x7801, 0x785e, 0x789c, 0x78da]
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def atz():
+    import antiz_amd
+    from antiz_amd import build
+    build.build()
+    return antiz_amd
+
+
+@pytest.fixture(scope="module")
+def ctx(atz):
+    c = atz.Context()
+    yield c
+    c.close()
+
+
+def inflate_cases(seed=7, n=600):
+    r = random.Random(seed)
+    out = []
+    for k in range(n):
+        kind = r.randrange(6)
+        if kind == 0:
+            d = _libs.text(r, r.randrange(1, 6000))
+            s, _ = _libs.ora_deflate(d, r.randrange(0, 10), r.randrange(10, 16), r.randrange(1, 10))
+            s = s[:r.randrange(1, len(s) + 1)] if r.random() < 0.5 else s + bytes(r.getrandbits(8) for _ in range(r.randrange(0, 20)))
+        elif kind == 1:
+            d = _libs.text(r, r.randrange(1, 6000))
+            s = bytearray(_libs.ora_deflate(d, r.randrange(1, 10), 15, 8)[0])
+            for _ in range(r.randrange(1, 4)):
+                p = r.randrange(2, len(s))
+                s[p] ^= 1 << r.randrange(8)
+            s = bytes(s)
+        elif kind == 2:
+            h = r.choice(HDRS)
+            s = bytes([h >> 8, h & 255]) + bytes(r.getrandbits(8) for _ in range(r.randrange(0, 300)))
+        elif kind == 3:
+            d = bytes(r.getrandbits(8) for _ in range(r.randrange(1, 400)))
+            s = _libs.ora_deflate(d, r.choice([0, 1, 9]), 15, r.randrange(1, 10))[0]
+            s = s[:r.randrange(2, len(s))] + bytes(r.getrandbits(8) for _ in range(r.randrange(0, 50)))
+        elif kind == 4:
+            d = bytes(r.choice(b"\x00\x01\x02\xff") for _ in range(r.randrange(1, 70000 if k % 50 == 0 else 3000)))
+            s = _libs.ora_deflate(d, r.randrange(0, 10), r.randrange(10, 16), r.randrange(1, 10))[0]
+            if r.random() < 0.3:
+                s = s[:r.randrange(1, len(s) + 1)]
+        else:
+            h = r.choice(HDRS)
+            s = bytes([h >> 8, h & 255, r.choice([0x04, 0x05, 0x0c, 0x0d, 0x14, 0x15, 0xed, 0xec, 0x1d])]) + \
+                bytes(r.getrandbits(8) for _ in range(r.randrange(0, 200)))
+        out.append(s)
+    return out
+
+
+def test_inflate_matches_zlib_semantics(ctx):
+    cases = inflate_cases()
+    buf = bytearray()
+    ranges = []
+    for s in cases:
+        pad = r_pad = (len(buf) * 7 + 3) % 5      # unaligned starts
+        buf += bytes(pad)
+        ranges.append((len(buf), len(s)))
+        buf += s
+    got = ctx.inflate_batch(bytes(buf), ranges)
+    bad = []
+    for i, s in enumerate(cases):
+        want = _libs.ora_inflate(s)
+        if tuple(got[i]) != tuple(want):
+            bad.append((i, got[i], want, s[:8].hex()))
+    assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("name", ["asd", "text4k", "rand5k", "input8k"])
+def test_deflate_kats_all_params(ctx, name):
+    kat = json.load(open(os.path.join(GOLD, "deflate_kat.json")))
+    d = open(os.path.join(GOLD, "kat", name + ".bin"), "rb").read()
+    items, keys = [], []
+    for c in range(10):
+        for w in range(9, 16):
+            for m in range(1, 10):
+                items.append((0, len(d), c, w, m))
+                keys.append("%s/%d/%d/%d" % (name, c, w, m))
+    outs = ctx.deflate_batch(d, items)
+    bad = [k for k, o in zip(keys, outs) if [len(o), sha(o)] != kat["results"][k]]
+    assert not bad, bad[:20]
+
+
+def test_deflate_random_vs_oracle(ctx):
+    r = random.Random(99)
+    rng = np.random.default_rng(99)
+    from antiz_amd import datagen
+    buf = bytearray()
+    items = []
+    for k in range(400):
+        kind = k % 4
+        if kind == 0:
+            d = datagen.text(rng, r.randrange(1, 60000))
+        elif kind == 1:
+            d = bytes(r.choice(b"ab") for _ in range(r.randrange(1, 20000)))
+        elif kind == 2:
+            d = rng.integers(0, 256, size=r.randrange(1, 9000), dtype=np.uint8).tobytes()
+        else:
+            d = (b"\0" * r.randrange(0, 5000)) + datagen.text(rng, r.randrange(1, 9000)) + b"\xff" * r.randrange(0, 3000)
+        items.append((len(buf), len(d), r.randrange(0, 10), r.randrange(9, 16), r.randrange(1, 10)))
+        buf += d
+    outs = ctx.deflate_batch(bytes(buf), items)
+    bad = []
+    for it, o in zip(items, outs):
+        want, _ = _libs.ora_deflate(bytes(buf[it[0]:it[0] + it[1]]), it[2], it[3], it[4])
+        if o != want:
+            first = next((i for i in range(min(len(o), len(want))) if o[i] != want[i]), min(len(o), len(want)))
+            bad.append((it[1:], len(o), len(want), first))
+    assert not bad, bad[:10]
+
+
+def test_zt_kat_precompress(atz):
+    data, meta = G.zt_kat()
+    with atz.Context() as c:
+        out, st = c.precompress(data)
+        assert sha(out) == meta["atz_sha256"]
+        assert c.reconstruct(out) == data
+
+
+@pytest.mark.parametrize("case", G.cases(), ids=lambda c: c["name"])
+def test_golden_case(atz, case):
+    data = G.case_input(case)
+    o = case["opts"]
+    with atz.Context(recomp_tresh=o.get("recomp_tresh", 128), sizediff_tresh=o.get("sizediff_tresh", 128),
+                     shortcut_len=o.get("shortcut_len", 512), mismatch_tol=o.get("mismatch_tol", 2),
+                     chunksize=o.get("chunksize", 524288), brute_window=bool(o.get("brute_window", 0))) as c:
+        out, st = c.precompress(data)
+        assert sha(out) == case["atz_sha256"], (case["name"], st)
+        assert c.reconstruct(out) == data
+
+
+def test_scan_and_sweep_tables_match_oracle(atz):
+    from antiz_amd import datagen
+    data = datagen.gen_c4(seed=123, n_streams=60, workers=1)
+    rc, atz_bytes, st = _libs.ora_precompress(data, chunksize=65536)
+    assert rc == 0
+    with atz.Context(chunksize=65536) as c:
+        recs = c.scan(data)
+        want = [(s["offset"], s["type"], s["comp_len"], s["infl_len"]) for s in st["streams"]]
+        assert [r[:4] for r in recs] == want
+        res, diffs = c.sweep()
+        got = [(r["clevel"], r["window"], r["memlevel"], r["ident"], r["recomp"]) for r in res]
+        exp = [(s["clevel"], s["window"], s["memlevel"], s["ident"], s["recomp"]) for s in st["streams"]]
+        assert got == exp
+
+
+def test_roundtrip_large_mixed(atz):
+    """Size-independent property at a bigger size: -r restores the input bit-exactly."""
+    from antiz_amd import datagen
+    data = datagen.gen_c4(seed=77, n_streams=1500, workers=4) + datagen.gen_c3(seed=78, total=4_000_000, workers=4)
+    with atz.Context() as c:
+        out, st = c.precompress(data)
+        assert st["n_streams"] > 1000
+        assert c.reconstruct(out) == data
