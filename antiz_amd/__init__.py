@@ -38,7 +38,12 @@ class Stats(C.Structure):
                                           "k_inflate_ms", "k_chains_ms", "k_other_ms")] + \
                [(k, u64) for k in ("k_trial_launches", "k_inflate_launches", "k_chains_launches",
                                    "k_trial_alg_bytes", "k_inflate_alg_bytes", "k_chains_alg_bytes",
-                                   "trial_parsed_bytes")]
+                                   "trial_parsed_bytes")] + \
+               [("k_match_ms", C.c_double)] + \
+               [(k, u64) for k in ("k_match_launches", "k_match_positions", "n_trials_rerun", "n_fast_fallbacks",
+                                   "trial_cyc_total", "trial_cyc_tree", "trial_cyc_emit", "trial_blocks",
+                                   "trial_cyc_lookup", "trial_cyc_fallback", "trial_symbols",
+                                   "n_trials_speculative")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -235,7 +235,7 @@ struct atz_ctx {
   hipStream_t st = nullptr;
   DBuf d_file, d_pos, d_cnt, d_jobs, d_res, d_virt, d_infl, d_chains, d_heads, d_streams, d_trials,
       d_tres, d_out, d_syms, d_adler, d_meta, d_segs, d_atz, d_diffjobs, d_diffpos, d_diffval, d_diffcnt,
-      d_cjobs, d_tmp;
+      d_cjobs, d_tmp, d_R, d_mjobs;
   // last scan
   std::vector<Rec> recs;
   std::vector<uint64_t> infl_off;   // per record offset in d_infl
@@ -250,7 +250,7 @@ struct atz_ctx {
   uint64_t chain_used = 0;
 };
 
-// kind: 0 trial, 1 inflate, 2 chains, 3 other
+// kind: 0 trial, 1 inflate, 2 chains, 3 other, 4 match tables
 static void kbeg(atz_ctx* c, int kind) {
   hipEvent_t a = c->kt.get(), b = c->kt.get();
   (void)hipEventRecord(a, c->st);
@@ -267,6 +267,7 @@ static void kcollect(atz_ctx* c) {
       case 0: c->stats.k_trial_ms += ms; c->stats.k_trial_launches++; break;
       case 1: c->stats.k_inflate_ms += ms; c->stats.k_inflate_launches++; break;
       case 2: c->stats.k_chains_ms += ms; c->stats.k_chains_launches++; break;
+      case 4: c->stats.k_match_ms += ms; c->stats.k_match_launches++; break;
       default: c->stats.k_other_ms += ms; break;
     }
     c->kt.pool.push_back(c->kt.pending[i].first);
@@ -642,6 +643,119 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
   return 0;
 }
 
+// Match-table prefix for a trial that may stop early: enough positions for the blocks that decide
+// the shortcut (~3 positions per symbol, lit_bufsize symbols per block); the rest on demand.
+static uint64_t match_prefix(uint64_t n, int memlevel) {
+  uint64_t x = std::max<uint64_t>(8192, 6ull << (memlevel + 6));
+  return std::min(n, x);
+}
+
+static int launch_match(atz_ctx* c, const std::vector<MatchJob>& mj) {
+  if (mj.empty()) return 0;
+  if (int r = upload(c, c->d_mjobs, mj.data(), mj.size() * sizeof(MatchJob))) return r;
+  kbeg(c, 4);
+  hipLaunchKernelGGL(k_match, dim3((uint32_t)mj.size()), dim3(256), 0, c->st, c->d_infl.as<uint8_t>(),
+                     c->d_chains.as<uint16_t>(), c->d_R.as<uint2>(), c->d_mjobs.as<MatchJob>());
+  kend(c);
+  KCHECK("k_match");
+  for (const MatchJob& m : mj) c->stats.k_match_positions += m.p1 - m.p0;
+  return 0;
+}
+
+// Runs the trials tr[k] (k = 0 stored, 1 fast, 2 slow levels); res[k] receives their results.
+// Chain tables must exist.  Match tables are built for a prefix of each trial's positions; a
+// trial that parses past it (TR_NEED_R) gets the rest of its table and is run again.
+static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
+                      std::vector<TrialRes>* res) {
+  uint64_t r_tot = 0;
+  std::vector<MatchJob> mj;
+  for (int k = 1; k < 3; k++)
+    for (Trial& t : tr[k]) {
+      const uint64_t n = c->recs[t.stream].infl_len;
+      t.r_off = r_tot;
+      r_tot += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
+      t.x_lim = (t.mode & 1) ? n : match_prefix(n, t.memlevel);
+      MatchJob m{};
+      m.infl_off = c->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
+      m.p0 = 0; m.p1 = t.x_lim; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
+      if (m.p1 > m.p0) mj.push_back(m);
+    }
+  if (int r = c->d_R.reserve(r_tot * sizeof(uint2) + 4096)) return r;
+  if (int r = launch_match(c, mj)) return r;
+  const size_t tot_trials = tr[0].size() + tr[1].size() + tr[2].size();
+  if (int r = c->d_trials.reserve(2 * tot_trials * sizeof(Trial) + 64)) return r;
+  if (int r = c->d_tres.reserve(2 * tot_trials * sizeof(TrialRes) + 64)) return r;
+  auto launch = [&](int k, const Trial* h, size_t cnt, size_t base) -> int {
+    HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + base, h, cnt * sizeof(Trial), hipMemcpyHostToDevice, c->st));
+    SweepArgs A;
+    A.file = d_cmp; A.infl = c->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint16_t>();
+    A.R = c->d_R.as<uint2>();
+    A.streams = c->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
+    A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
+    A.adler = c->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)cnt;
+    dim3 g((uint32_t)cnt), b(64);
+    kbeg(c, 0);
+    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
+    else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, 0, c->st, A);
+    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
+    kend(c);
+    KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
+    return 0;
+  };
+  size_t base = 0;
+  size_t bases[3];
+  for (int k = 0; k < 3; k++) {
+    bases[k] = base;
+    res[k].resize(tr[k].size());
+    if (tr[k].empty()) continue;
+    if (int r = launch(k, tr[k].data(), tr[k].size(), base)) return r;
+    base += tr[k].size();
+  }
+  for (int k = 0; k < 3; k++)
+    if (!tr[k].empty())
+      HIPCHK(hipMemcpyAsync(res[k].data(), c->d_tres.as<TrialRes>() + bases[k], tr[k].size() * sizeof(TrialRes),
+                            hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  kcollect(c);
+  // second pass: complete the match tables of the trials that need them and run those again
+  std::vector<Trial> again[3];
+  std::vector<size_t> where[3];
+  mj.clear();
+  for (int k = 1; k < 3; k++)
+    for (size_t q = 0; q < tr[k].size(); q++) {
+      if (res[k][q].state != TR_NEED_R) continue;
+      Trial t = tr[k][q];
+      const uint64_t n = c->recs[t.stream].infl_len;
+      MatchJob m{};
+      m.infl_off = c->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
+      m.p0 = t.x_lim; m.p1 = n; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
+      if (m.p1 > m.p0) mj.push_back(m);
+      t.x_lim = n;
+      again[k].push_back(t);
+      where[k].push_back(q);
+      c->stats.n_trials_rerun++;
+    }
+  if (mj.empty()) return 0;
+  if (int r = launch_match(c, mj)) return r;
+  std::vector<TrialRes> rr[3];
+  for (int k = 1; k < 3; k++) {
+    if (again[k].empty()) continue;
+    if (int r = launch(k, again[k].data(), again[k].size(), base)) return r;
+    rr[k].resize(again[k].size());
+    HIPCHK(hipMemcpyAsync(rr[k].data(), c->d_tres.as<TrialRes>() + base, again[k].size() * sizeof(TrialRes),
+                          hipMemcpyDeviceToHost, c->st));
+    base += again[k].size();
+  }
+  HIPCHK(hipStreamSynchronize(c->st));
+  kcollect(c);
+  for (int k = 1; k < 3; k++)
+    for (size_t q = 0; q < again[k].size(); q++) {
+      if (rr[k][q].state == TR_NEED_R) return ATZ_E_INTERNAL;
+      res[k][where[k][q]] = rr[k][q];
+    }
+  return 0;
+}
+
 static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
   auto t0 = std::chrono::steady_clock::now();
   const size_t n = c->recs.size();
@@ -663,81 +777,73 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
   if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;
   if (int r = upload(c, c->d_streams, sd.data(), n * sizeof(StreamDev))) return r;
   SweepOpts so{c->o.recomp_tresh, c->o.sizediff_tresh, c->o.shortcut_len, c->o.mismatch_tol};
-  uint64_t rounds = 0, ntr = 0, nsc = 0, nhz = 0;
+  uint64_t rounds = 0, ntr = 0, nsc = 0, nhz = 0, nspec = 0;
   std::vector<Trial> tr[3];
-  std::vector<uint32_t> tr_stream[3];
   std::vector<TrialRes> trres[3];
+  // A round evaluates the next K trials of every active stream (speculatively: a stream that
+  // stops at its j-th trial discards the results of the later ones), K sized so a round fills the
+  // GPU.  Results are applied per stream strictly in list order, so the outcome is the
+  // reference's sequential one; the speculation only changes how much work runs per launch.
+  const size_t target = 16384;
   while (!active.empty()) {
     rounds++;
-    // trials of this round and the chain tables they need
+    const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, target / active.size()));
     std::vector<std::pair<uint32_t, int>> need;
-    for (int k = 0; k < 3; k++) { tr[k].clear(); tr_stream[k].clear(); }
+    for (int k = 0; k < 3; k++) tr[k].clear();
+    // per stream, its trials of this round in list order: (kind, index in tr[kind])
+    std::vector<std::vector<std::pair<int, uint32_t>>> mine(active.size());
     uint64_t out_tot = 0, sym_tot = 0;
-    for (uint32_t s : active) {
+    for (size_t a = 0; a < active.size(); a++) {
+      const uint32_t s = active[a];
       StreamState& st = ss[s];
-      uint32_t p = st.list[st.idx];
-      int cl = (int)(p >> 16), w = (int)((p >> 8) & 0xff), m = (int)(p & 0xff);
-      Trial t{};
-      t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
-      t.best_ident = st.ident;
-      t.out_off = out_tot; t.out_cap = bound(c->recs[s].infl_len, w, m) + 64;
-      out_tot += (t.out_cap + 255) & ~255ull;
-      t.sym_off = sym_tot; sym_tot += 1ull << (m + 6);
-      int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
-      if (kind) need.push_back({s, m});
-      tr[kind].push_back(t);
-      tr_stream[kind].push_back(s);
+      for (uint32_t j = 0; j < K && st.idx + j < st.list.size(); j++) {
+        uint32_t p = st.list[st.idx + j];
+        int cl = (int)(p >> 16), w = (int)((p >> 8) & 0xff), m = (int)(p & 0xff);
+        Trial t{};
+        t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
+        t.best_ident = st.ident;
+        t.out_off = out_tot; t.out_cap = bound(c->recs[s].infl_len, w, m) + 64;
+        out_tot += (t.out_cap + 255) & ~255ull;
+        t.sym_off = sym_tot; sym_tot += (1ull << (m + 6)) + 64;
+        int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
+        if (kind) need.push_back({s, m});
+        mine[a].push_back({kind, (uint32_t)tr[kind].size()});
+        tr[kind].push_back(t);
+      }
     }
     if (int r = ensure_chains(c, need)) return r;
     for (int k = 1; k < 3; k++)
       for (Trial& t : tr[k]) t.chain_off = c->chain_off[t.stream][t.memlevel];
     if (int r = c->d_out.reserve(out_tot + 4096)) return r;
     if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
-    size_t tot_trials = tr[0].size() + tr[1].size() + tr[2].size();
-    if (int r = c->d_trials.reserve(tot_trials * sizeof(Trial) + 64)) return r;
-    if (int r = c->d_tres.reserve(tot_trials * sizeof(TrialRes) + 64)) return r;
-    size_t base = 0;
-    for (int k = 0; k < 3; k++) {
-      if (tr[k].empty()) continue;
-      HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + base, tr[k].data(), tr[k].size() * sizeof(Trial),
-                            hipMemcpyHostToDevice, c->st));
-      SweepArgs A;
-      A.file = d_file; A.infl = c->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint16_t>();
-      A.streams = c->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
-      A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
-      A.adler = c->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)tr[k].size();
-      dim3 g((uint32_t)tr[k].size()), b(64);
-      kbeg(c, 0);
-      if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
-      else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, 0, c->st, A);
-      else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
-      kend(c);
-      KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
-      trres[k].resize(tr[k].size());
-      HIPCHK(hipMemcpyAsync(trres[k].data(), c->d_tres.as<TrialRes>() + base, tr[k].size() * sizeof(TrialRes),
-                            hipMemcpyDeviceToHost, c->st));
-      base += tr[k].size();
-    }
-    HIPCHK(hipStreamSynchronize(c->st));
-    kcollect(c);
+    if (int r = run_trials(c, d_file, tr, so, trres)) return r;
     for (int k = 0; k < 3; k++)
       for (size_t q = 0; q < tr[k].size(); q++) {
         const TrialRes& r = trres[k][q];
         const uint64_t C = c->recs[tr[k][q].stream].comp_len;
         c->stats.trial_parsed_bytes += r.parsed;
+        c->stats.n_fast_fallbacks += r.fallbacks;
+        c->stats.trial_cyc_total += r.cyc_total; c->stats.trial_cyc_tree += r.cyc_tree;
+        c->stats.trial_cyc_emit += r.cyc_emit; c->stats.trial_blocks += r.blocks;
+        c->stats.trial_cyc_lookup += r.cyc_lookup; c->stats.trial_cyc_fallback += r.cyc_fallback;
+        c->stats.trial_symbols += r.symbols;
         // trial input read + compare read (bytes emitted and compared against the original)
         c->stats.k_trial_alg_bytes += c->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
       }
-    // apply the reference's sequential rule per stream (one trial per stream per round)
+    // apply the reference's sequential rule per stream, in list order
     std::vector<DiffJob> dj;
-    std::vector<uint32_t> dj_stream;
+    std::vector<uint32_t> dj_stream;   // ~0u: superseded by a later improvement of the same stream
     uint64_t dpos = 0;
-    for (int k = 0; k < 3; k++) {
-      for (size_t q = 0; q < tr[k].size(); q++) {
-        const Trial& t = tr[k][q];
-        const TrialRes& r = trres[k][q];
-        StreamState& st = ss[t.stream];
-        const uint64_t C = c->recs[t.stream].comp_len;
+    for (size_t a = 0; a < active.size(); a++) {
+      const uint32_t s = active[a];
+      StreamState& st = ss[s];
+      const uint64_t C = c->recs[s].comp_len;
+      const uint32_t phase0 = st.phase;
+      int64_t last_dj = -1;
+      for (size_t j = 0; j < mine[a].size(); j++) {
+        if (st.phase != phase0) { nspec += mine[a].size() - j; break; }   // stopped earlier this round
+        const Trial& t = tr[mine[a][j].first][mine[a][j].second];
+        const TrialRes& r = trres[mine[a][j].first][mine[a][j].second];
         st.trials++;
         ntr++;
         if (r.state == TR_SHORTCUT) nsc++;
@@ -749,16 +855,18 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
           st.c = t.clevel; st.w = t.window; st.m = t.memlevel;
           st.first_diff = -1;
           st.rawdiff.clear(); st.diffval.clear();
+          if (last_dj >= 0) { dj_stream[last_dj] = ~0u; last_dj = -1; }
           if (r.ident == C) fullmatch = true;
           else {
             if (r.ident + c->o.mismatch_tol >= C) fullmatch = true;
             if (C - r.ident <= c->o.recomp_tresh) {     // diffs are only ever written for recomp streams
               DiffJob d;
-              d.out_off = t.out_off; d.out_len = r.out_len; d.orig_off = c->recs[t.stream].offset;
+              d.out_off = t.out_off; d.out_len = r.out_len; d.orig_off = c->recs[s].offset;
               d.comp_len = C; d.dst = dpos; d.cap = C - r.ident;
               dpos += d.cap;
+              last_dj = (int64_t)dj.size();
               dj.push_back(d);
-              dj_stream.push_back(t.stream);
+              dj_stream.push_back(s);
             }
           }
         }
@@ -767,7 +875,7 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
         if (st.idx >= st.list.size()) {
           if (st.phase == 0 && (C - st.ident) >= c->o.mismatch_tol && c->o.brute_window) {
             st.list.clear();
-            list_b(st.list, c->recs[t.stream].type);
+            list_b(st.list, c->recs[s].type);
             st.idx = 0;
             st.phase = 1;
           } else {
@@ -797,6 +905,7 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
       kcollect(c);
       for (size_t q = 0; q < dj.size(); q++) {
         if (cnt[q] != dj[q].cap) return ATZ_E_INTERNAL;
+        if (dj_stream[q] == ~0u) continue;
         StreamState& st = ss[dj_stream[q]];
         st.rawdiff.assign(pos.begin() + dj[q].dst, pos.begin() + dj[q].dst + dj[q].cap);
         st.diffval.assign(val.begin() + dj[q].dst, val.begin() + dj[q].dst + dj[q].cap);
@@ -813,6 +922,7 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
     st.recomp = (C - st.ident) <= c->o.recomp_tresh && st.ident > 0;
   }
   c->stats.n_trials = ntr; c->stats.n_trials_shortcut = nsc; c->stats.n_rounds = rounds; c->stats.n_hazard = nhz;
+  c->stats.n_trials_speculative = nspec;
   c->stats.sweep_ms = ms_since(t0);
   return 0;
 }
@@ -962,36 +1072,11 @@ static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, 
   }
   if (int r = c->d_out.reserve(out_tot + 4096)) return r;
   if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
-  if (int r = c->d_trials.reserve(n * sizeof(Trial) + 64)) return r;
-  if (int r = c->d_tres.reserve(n * sizeof(TrialRes) + 64)) return r;
   // zero-length "file" for the compare side
   if (int r = c->d_tmp.reserve(4096)) return r;
   SweepOpts so{0, 0, 0, 0};
-  size_t base = 0;
   std::vector<TrialRes> rr[3];
-  for (int k = 0; k < 3; k++) {
-    if (tr[k].empty()) continue;
-    HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + base, tr[k].data(), tr[k].size() * sizeof(Trial),
-                          hipMemcpyHostToDevice, c->st));
-    SweepArgs A;
-    A.file = c->d_tmp.as<uint8_t>(); A.infl = c->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint16_t>();
-    A.streams = c->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
-    A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
-    A.adler = c->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)tr[k].size();
-    dim3 g((uint32_t)tr[k].size()), b(64);
-    kbeg(c, 0);
-    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
-    else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, 0, c->st, A);
-    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
-    kend(c);
-    KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
-    rr[k].resize(tr[k].size());
-    HIPCHK(hipMemcpyAsync(rr[k].data(), c->d_tres.as<TrialRes>() + base, tr[k].size() * sizeof(TrialRes),
-                          hipMemcpyDeviceToHost, c->st));
-    base += tr[k].size();
-  }
-  HIPCHK(hipStreamSynchronize(c->st));
-  kcollect(c);
+  if (int r = run_trials(c, c->d_tmp.as<uint8_t>(), tr, so, rr)) return r;
   for (int k = 0; k < 3; k++) {
     for (size_t q = 0; q < tr[k].size(); q++) {
       if (rr[k][q].state != TR_FULL) return ATZ_E_INTERNAL;

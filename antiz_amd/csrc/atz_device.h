@@ -34,6 +34,23 @@ struct Trial {
   uint64_t out_cap;     // scratch output capacity (bytes)
   uint64_t sym_off;     // symbol-buffer offset (uint32 units), capacity 1 << (memlevel + 6)
   uint64_t chain_off;   // chain-link table of (stream, memlevel) (uint16 units); unused for level 0
+  uint64_t r_off;       // match table of this trial (uint2 units, indexed by absolute position)
+  uint64_t x_lim;       // match-table entries exist for positions < x_lim (else the trial stops: TR_NEED_R)
+};
+
+// ---- match tables (k_match) ----------------------------------------------------------------
+// longest_match (Z/deflate.c:1148-1289) evaluated for every position p of a stream, one lane per
+// position, for one (level, window) on the (stream, memLevel) chains:
+//   slow levels: .x = result with the full chain budget, .y = with budget >> 2 (prev_length >= good)
+//   fast levels: .x = full-budget result, .y = p - (lowest chain node the walk visited), hash slot
+// result = len:9 | dist:15 (0 = no match longer than MIN_MATCH-1); see k_match for the packing.
+struct MatchJob {
+  uint64_t infl_off, n;   // stream bytes
+  uint64_t chain_off;     // u16 units
+  uint64_t r_off;         // uint2 units
+  uint64_t p0, p1;        // positions [p0, p1)
+  uint32_t level, window;
+  uint32_t fast, memlevel;
 };
 
 struct StreamDev {
@@ -50,6 +67,10 @@ struct TrialRes {
   uint64_t ident;       // positional equal bytes over min(out_len, C_s) (TR_FULL) / shortcut ident
   uint64_t symbols;     // diagnostic: symbols tallied
   uint64_t parsed;      // input positions consumed when the trial stopped
+  uint64_t fallbacks;   // fast levels: steps that walked the chain because a skipped position was on it
+  uint64_t cyc_total, cyc_tree, cyc_emit, blocks;   // diagnostics: shader clocks in the trial / tree
+                                                    // construction / block emission, blocks flushed
+  uint64_t cyc_lookup, cyc_fallback;                // match lookup in the parse / fast-level chain walks
 };
 enum : uint32_t {
   TR_FULL = 0,        // full output produced and compared: ident valid
@@ -57,6 +78,7 @@ enum : uint32_t {
   TR_SIZEDIFF = 2,    // |out - C_s| > sizediff_tresh: no compare
   TR_CANT_BEAT = 3,   // stopped: cannot exceed best_ident (result irrelevant to the sweep)
   TR_OVERFLOW = 4,    // output capacity exceeded (host treats as reference abort)
+  TR_NEED_R = 5,      // parse reached x_lim: extend the match table and run the trial again
 };
 
 struct SweepOpts {

@@ -49,6 +49,13 @@ __device__ __constant__ uint8_t c_blorder[19] = {16,17,18,0,8,7,9,6,10,5,11,4,12
 __device__ __constant__ uint16_t c_cfg[10][4] = {{0,0,0,0},{4,4,8,4},{4,5,16,8},{4,6,32,32},{4,4,16,16},
     {8,16,32,32},{8,16,128,128},{8,32,128,256},{32,128,258,1024},{32,258,258,4096}};
 
+// Values that are wave-uniform but come from memory, a call or a lane-masked region: re-declare
+// them uniform so the parse state stays in SGPRs with scalar branches.
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uni(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+
 extern "C" hipError_t atz_upload_defl_tables(const void* host_tables) {
   return hipMemcpyToSymbol(HIP_SYMBOL(c_t), host_tables, sizeof(DeflTables));
 }
@@ -118,10 +125,83 @@ __global__ __launch_bounds__(64) void k_chains(const uint8_t* __restrict__ infl,
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_match: longest_match (Z/deflate.c:1148-1289) for every position of a trial, lanes = positions.
+//
+// zlib's result at position p depends on the parse only through prev_length (deflate_slow):
+// the chain budget is quartered when prev_length >= good_match, and a candidate must beat
+// prev_length.  The winner is the FIRST candidate reaching the maximum length, so computing the
+// first-maximum from MIN_MATCH-1 and comparing it with prev_length at parse time is exact; both
+// budgets are evaluated in one walk (the quarter budget sees a prefix of the same candidates).
+// The window slide does not change the walk: with S the slide offset, zlib stops at nodes
+// <= max(p - MAX_DIST, S), and S > 0 implies S <= p - MAX_DIST; its only trace is hash_head == S
+// (NIL after the slide), which the parse checks.  nice_match is clamped to the lookahead, i.e.
+// to n - p near the end; bytes beyond the input can only extend candidates that already reach
+// n - p, which break at nice_match first.
+static constexpr uint32_t HOLE_SLOTS_M = 4096;   // == HOLE_SLOTS (fast-level hash slots)
+
+__global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl, const uint16_t* __restrict__ chains,
+                                              uint2* __restrict__ R, const MatchJob* __restrict__ jobs) {
+  const MatchJob jb = jobs[blockIdx.x];
+  const uint8_t* in = infl + jb.infl_off;
+  const uint16_t* ch = chains + jb.chain_off;
+  uint2* r = R + jb.r_off;
+  const uint32_t B = c_cfg[jb.level][3], nice = c_cfg[jb.level][2], Bq = B >> 2;
+  const uint64_t n = jb.n, maxdist = (1u << jb.window) - 262;
+  const uint32_t hbits = jb.memlevel + 7u, hmask = (1u << hbits) - 1u, hshift = (hbits + 2u) / 3u;
+  for (uint64_t p = jb.p0 + threadIdx.x; p < jb.p1; p += 256) {
+    uint32_t bf = 2, df = 0, bq = 2, dq = 0, valid = 0, slot = 0;
+    uint64_t reach = p;
+    const uint32_t s0 = in[p];
+    if (p + 3 <= n) {
+      const uint32_t s1 = in[p + 1];
+      slot = (((s0 << (2 * hshift)) ^ (s1 << hshift) ^ (uint32_t)in[p + 2]) & hmask) & (HOLE_SLOTS_M - 1);
+      const uint32_t d = ch[p];
+      const uint64_t lim = p > maxdist ? p - maxdist : 0;   // walk continues to q only if q > lim
+      const uint64_t cur0 = p - d;
+      uint64_t cur = cur0;
+      if (d && d <= p && cur0 >= 1 && cur0 + maxdist >= p) {  // hash_head valid
+        valid = 1;
+        const uint64_t left = n - p;
+        const uint32_t cap = left < 258 ? (uint32_t)left : 258u;
+        const uint32_t nn = nice < cap ? nice : cap;
+        for (uint32_t i = 0;;) {
+          reach = cur;
+          // quick reject (bf < nn <= cap, so every read is inside the input)
+          if (in[cur + bf] == in[p + bf] && in[cur + bf - 1] == in[p + bf - 1] && in[cur] == s0 &&
+              in[cur + 1] == s1) {
+            uint32_t len = 2;
+            while (len < cap && in[cur + len] == in[p + len]) len++;
+            if (len > bf) {
+              bf = len; df = (uint32_t)(p - cur);
+              if (i < Bq) { bq = len; dq = df; }
+              if (len >= nn) break;
+            }
+          }
+          if (++i == B) break;
+          const uint32_t dd = ch[cur];
+          if (!dd || cur < dd) break;
+          cur -= dd;
+          if (cur <= lim) break;
+        }
+      }
+    }
+    // .x = len_full:9 | dist_full:15 | input byte:8
+    // .y = slow: len_quarter:9 | dist_quarter:15 | 0:7 | head valid:1
+    //      fast: (p - lowest visited node):16 | 0:3 | hash slot:12 | head valid:1
+    uint2 e;
+    e.x = (bf > 2 ? (bf << 23) | (df << 8) : 0u) | s0;
+    if (jb.fast) e.y = ((uint32_t)(p - reach) << 16) | (slot << 1) | valid;
+    else e.y = (bq > 2 ? (bq << 23) | (dq << 8) : 0u) | valid;
+    r[p] = e;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_trial
 static constexpr int NLC = 286, NDC = 30, NBLC = 19, HEAPN = 2 * NLC + 1;
 static constexpr uint32_t LOOKMIN = 262;
 static constexpr uint32_t BITMAP_BITS = 65536;  // fast-mode insertion ring (positions mod 65536)
+static constexpr uint32_t HOLE_SLOTS = HOLE_SLOTS_M;   // fast mode: latest skipped position per hash slot
 
 struct TreeWork {      // one tree under construction (zlib ct_data split into arrays)
   uint16_t freq[HEAPN];
@@ -146,12 +226,14 @@ struct TrialShared {
 struct TrialSharedFast {
   TrialShared t;
   uint32_t ins[BITMAP_BITS / 32];
+  uint32_t holes[HOLE_SLOTS];   // position + 1 of the latest non-inserted position with hash & (SLOTS-1)
 };
 
 struct SweepArgs {
   const uint8_t* file;          // original compressed bytes
   const uint8_t* infl;          // inflated bytes
   const uint16_t* chains;       // chain links
+  const uint2* R;               // match tables (k_match)
   const StreamDev* streams;
   const Trial* trials;
   TrialRes* res;
@@ -175,6 +257,7 @@ struct BitOut {
   uint64_t eq_all;   // equal bytes at positions < min(pos, C_s)
   uint64_t eq_sc;    // equal bytes at positions < min(pos, shortcut)
   int overflow;
+  uint64_t cyc_tree, cyc_emit, blocks;   // diagnostics (shader clock)
 };
 
 __device__ inline uint64_t wsum64(uint64_t v) {
@@ -464,8 +547,42 @@ struct Lz {
   uint64_t nsym;
 };
 
+// Double-buffered lane-resident window over the trial's match table: lane l holds the entry of
+// position rb + l and the entry of rb + 64 + l is in flight, so the wave-uniform parse reads its
+// per-position data with v_readlane and the next HBM round trip overlaps ~64 positions of work.
+struct PosWin {
+  const uint2* R;
+  uint64_t rb;
+  uint32_t cx, cy, nx, ny;
+  __device__ __forceinline__ void init(const uint2* r) { R = r; rb = 1ull << 62; cx = cy = nx = ny = 0; }
+  __device__ __forceinline__ uint2 get(uint64_t p, int lane) {
+    if (p - rb >= 64) {
+      if (p - rb < 128) { cx = nx; cy = ny; rb += 64; }
+      else { rb = p; const uint2 e = R[rb + lane]; cx = e.x; cy = e.y; }
+      const uint2 f = R[rb + 64 + lane];
+      nx = f.x; ny = f.y;
+    }
+    uint2 e;
+    e.x = (uint32_t)__builtin_amdgcn_readlane((int)cx, (int)(p - rb));
+    e.y = (uint32_t)__builtin_amdgcn_readlane((int)cy, (int)(p - rb));
+    return e;
+  }
+};
+
+__device__ __forceinline__ uint32_t len_code(uint32_t len) {   // _length_code[len], len = length - 3
+  if (len < 8) return len;
+  if (len == 255) return 28;
+  const uint32_t lg = 31u - (uint32_t)__clz(len);
+  return 4u * (lg - 1u) + ((len >> (lg - 2u)) & 3u);
+}
+__device__ __forceinline__ uint32_t dist_code(uint32_t d) {    // d_code(d), d = distance - 1
+  if (d < 4) return d;
+  const uint32_t lg = 31u - (uint32_t)__clz(d);
+  return 2u * lg + ((d >> (lg - 1u)) & 1u);
+}
+
 // fill_window bookkeeping (Z/deflate.c:1390-1532) on absolute positions
-__device__ inline void fill(Lz& z) {
+__device__ __forceinline__ void fill(Lz& z) {
   do {
     uint64_t sw = z.p - z.S;
     uint64_t more = 2ull * z.wsize - z.lookahead - sw;
@@ -503,7 +620,7 @@ __device__ inline bool is_inserted(const uint32_t* ins, uint64_t q) {
 
 // longest_match on the shared chains (Z/deflate.c:1148-1289).  Returns match length; sets z.match_start.
 template <int KIND>
-__device__ uint32_t longest_match(Lz& z, const uint8_t* in, const uint16_t* ch, const uint32_t* ins,
+__device__ __forceinline__ uint32_t longest_match(Lz& z, const uint8_t* in, const uint16_t* ch, const uint32_t* ins,
                                   uint64_t cur, int lane) {
   uint32_t chain = z.chain;
   const uint64_t p = z.p;
@@ -522,8 +639,8 @@ __device__ uint32_t longest_match(Lz& z, const uint8_t* in, const uint16_t* ch, 
     uint8_t se1 = p + best - 1 < z.n ? in[p + best - 1] : 0;
     uint8_t m0 = cur + best < z.n ? in[cur + best] : 0;
     uint8_t m1 = cur + best - 1 < z.n ? in[cur + best - 1] : 0;
-    if (m0 == se0 && m1 == se1 && in[cur] == in[p] && in[cur + 1] == in[p + 1]) {
-      uint32_t len = common_len(in, cur, p, 2, cap, lane);
+    if (uni((uint32_t)(m0 == se0 && m1 == se1 && in[cur] == in[p] && in[cur + 1] == in[p + 1]))) {
+      uint32_t len = uni(common_len(in, cur, p, 2, cap, lane));
       if (len > best) {
         z.match_start = cur;
         best = len;
@@ -534,11 +651,11 @@ __device__ uint32_t longest_match(Lz& z, const uint8_t* in, const uint16_t* ch, 
     uint64_t nx = cur;
     bool stop = false;
     for (;;) {
-      uint32_t d = ch[nx];
+      uint32_t d = uni((uint32_t)ch[nx]);
       if (!d || nx < d) { stop = true; break; }
       nx -= d;
       if (nx <= limit) { stop = true; break; }
-      if (is_inserted<KIND>(ins, nx)) break;
+      if (uni((uint32_t)is_inserted<KIND>(ins, nx))) break;
     }
     if (stop || --chain == 0) break;
     cur = nx;
@@ -546,22 +663,19 @@ __device__ uint32_t longest_match(Lz& z, const uint8_t* in, const uint16_t* ch, 
   return best <= z.lookahead ? best : (uint32_t)z.lookahead;
 }
 
-struct BlockCtx {
-  TrialShared* s;
-  uint32_t* syms;
-  const uint8_t* in;
-  BitOut* b;
-};
-
 // _tr_flush_block (Z/trees.c:907-1004) + FLUSH_BLOCK_ONLY bookkeeping
-__device__ void flush_block(Lz& z, BlockCtx& bc, int last, uint32_t& hazard, int lane) {
-  TrialShared& s = *bc.s;
-  BitOut& b = *bc.b;
-  const bool bufok = z.block_start >= (int64_t)z.S;
-  const uint64_t stored_len = (uint64_t)((int64_t)z.p - z.block_start);
+// The parse state is passed by value so that it never leaves registers (a reference to it here
+// would put the whole parse state in scratch memory).  Returns the overlay-hazard bit.
+__device__ __noinline__ uint32_t flush_block(TrialShared& s, BitOut& b, const uint32_t* syms, const uint8_t* in,
+                                             int64_t block_start, uint64_t p, uint64_t S, uint32_t last_lit,
+                                             uint32_t level, uint32_t lbs, int last, int lane) {
+  uint32_t hazard = 0;
+  const uint64_t c0 = clock64();
+  const bool bufok = block_start >= (int64_t)S;
+  const uint64_t stored_len = (uint64_t)((int64_t)p - block_start);
   uint64_t opt_len = 0, static_len = 0, opt_lenb, static_lenb;
   int lmax = 0, dmax = 0, max_blindex = 0;
-  if (z.level > 0) {
+  if (level > 0) {
     // literal/length tree
     for (int i = lane; i < NLC; i += 64) s.w.freq[i] = (uint16_t)s.lfreq[i];
     lmax = build_tree(s.w, NLC, 15, c_xlb, 257, c_t.st_llen, opt_len, static_len);
@@ -589,13 +703,16 @@ __device__ void flush_block(Lz& z, BlockCtx& bc, int last, uint32_t& hazard, int
     opt_lenb = static_lenb = stored_len + 5;
   }
   const uint64_t blk_start_bytes = b.pos;
+  const uint64_t c1 = clock64();
+  b.cyc_tree += c1 - c0;
+  b.blocks++;
   if (stored_len + 4 <= opt_lenb && bufok) {
     put_bits(b, s.stage, (uint32_t)last, 3, lane);
     windup(b, s.stage, lane);
     uint32_t len = (uint32_t)stored_len;
     put_bits(b, s.stage, (len & 0xffff) | ((~len & 0xffff) << 16), 32, lane);
     // copy the block's input bytes (now byte aligned, bc == 0)
-    const uint8_t* src = bc.in + z.block_start;
+    const uint8_t* src = in + block_start;
     for (uint64_t o = 0; o < stored_len; o += 256) {
       uint32_t nb = stored_len - o < 256 ? (uint32_t)(stored_len - o) : 256u;
       for (uint32_t k = lane; k < 64; k += 64) {
@@ -610,7 +727,7 @@ __device__ void flush_block(Lz& z, BlockCtx& bc, int last, uint32_t& hazard, int
     }
   } else if (static_lenb == opt_lenb) {
     put_bits(b, s.stage, (1u << 1) + (uint32_t)last, 3, lane);
-    compress_block(b, s, bc.syms, z.last_lit, c_t.st_lcode, c_t.st_llen, c_t.st_dcode, c_t.st_dlen, lane);
+    compress_block(b, s, syms, last_lit, c_t.st_lcode, c_t.st_llen, c_t.st_dcode, c_t.st_dlen, lane);
   } else {
     int lcodes = lmax + 1, dcodes = dmax + 1, blcodes = max_blindex + 1;
     put_bits(b, s.stage, (2u << 1) + (uint32_t)last, 3, lane);
@@ -621,32 +738,17 @@ __device__ void flush_block(Lz& z, BlockCtx& bc, int last, uint32_t& hazard, int
     send_tree(b, s, s.llen, lcodes - 1, lane);
     send_tree(b, s, s.dlen, dcodes - 1, lane);
     flush_bits_bytes(b, s.stage, lane);
-    compress_block(b, s, bc.syms, z.last_lit, s.lcode, s.llen, s.dcode, s.dlen, lane);
+    compress_block(b, s, syms, last_lit, s.lcode, s.llen, s.dcode, s.dlen, lane);
   }
   // 1.2.8 pending_buf/d_buf overlay condition (conservative, cf. oracle/ora_deflate.c)
-  if (b.pos - blk_start_bytes > (uint64_t)z.lbs + 2ull * z.last_lit && z.last_lit) hazard = 1;
+  if (b.pos - blk_start_bytes > (uint64_t)lbs + 2ull * last_lit && last_lit) hazard = 1;
   // init_block
   for (int i = lane; i < NLC; i += 64) s.lfreq[i] = 0;
   for (int i = lane; i < NDC; i += 64) s.dfreq[i] = 0;
   if (lane == 0) s.lfreq[256] = 1;
-  z.last_lit = 0;
   if (last) windup(b, s.stage, lane);
-  z.block_start = (int64_t)z.p;
-}
-
-__device__ inline bool tally_lit(Lz& z, BlockCtx& bc, uint32_t c, int lane) {
-  if (lane == 0) { bc.syms[z.last_lit] = c; bc.s->lfreq[c]++; }
-  z.last_lit++; z.nsym++;
-  return z.last_lit == z.lbs - 1;
-}
-__device__ inline bool tally_dist(Lz& z, BlockCtx& bc, uint32_t dist, uint32_t len, int lane) {
-  if (lane == 0) {
-    bc.syms[z.last_lit] = (dist << 8) | len;
-    bc.s->lfreq[c_t.lcode[len] + 257]++;
-    bc.s->dfreq[d_code(dist - 1)]++;
-  }
-  z.last_lit++; z.nsym++;
-  return z.last_lit == z.lbs - 1;
+  b.cyc_emit += clock64() - c1;
+  return hazard;
 }
 
 // Early-exit test after output progress: returns TR_* state to stop with, or ~0u to continue.
@@ -688,14 +790,61 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   b.orig = A.file + sd.orig_off; b.clen = sd.comp_len;
   b.shortcut = sd.comp_len > A.o.shortcut_len ? A.o.shortcut_len : 0;
   b.eq_all = 0; b.eq_sc = 0; b.overflow = 0;
-  BlockCtx bcx;
-  bcx.s = &s; bcx.syms = A.syms + tr.sym_off; bcx.in = in; bcx.b = &b;
+  uint32_t* const syms = A.syms + tr.sym_off;
+  b.cyc_tree = b.cyc_emit = b.blocks = 0;
+  const uint64_t cstart = clock64();
   for (int i = lane; i < NLC; i += 64) s.lfreq[i] = 0;
   for (int i = lane; i < NDC; i += 64) s.dfreq[i] = 0;
   if (lane == 0) s.lfreq[256] = 1;
   if constexpr (KIND == 1) { for (int i = lane; i < (int)(BITMAP_BITS / 32); i += 64) ins[i] = 0; }
   uint32_t hazard = 0;
+  // Block statistics live in VGPRs across lanes (lfreq[c] in lane c & 63, register c >> 6) and
+  // symbols are staged one per lane, 64 per coalesced store: the scalar parse issues no LDS
+  // read-modify-write and no per-symbol HBM store.
+  uint32_t lf0 = 0, lf1 = 0, lf2 = 0, lf3 = 0, lf4 = lane == 0 ? 1u : 0u;   // lfreq[256] = 1 (END_BLOCK)
+  uint32_t dfr = 0, symreg = 0;
+  auto count_l = [&](uint32_t code) {
+    const uint32_t me = (uint32_t)lane == (code & 63u) ? 1u : 0u;
+    switch (code >> 6) {
+      case 0: lf0 += me; break;
+      case 1: lf1 += me; break;
+      case 2: lf2 += me; break;
+      case 3: lf3 += me; break;
+      default: lf4 += me; break;
+    }
+  };
+  auto stage = [&](uint32_t v) {
+    const uint32_t slot = z.last_lit & 63u;
+    if ((uint32_t)lane == slot) symreg = v;
+    if (slot == 63u) syms[z.last_lit - 63u + lane] = symreg;
+    z.last_lit++; z.nsym++;
+  };
+  auto tally_lit = [&](uint32_t c) -> bool {
+    stage(c);
+    count_l(c);
+    return z.last_lit == z.lbs - 1;
+  };
+  auto tally_dist = [&](uint32_t dist, uint32_t len) -> bool {
+    stage((dist << 8) | len);
+    count_l(len_code(len) + 257u);
+    dfr += (uint32_t)lane == dist_code(dist - 1) ? 1u : 0u;
+    return z.last_lit == z.lbs - 1;
+  };
+  auto FLUSH = [&](int last) {
+    const uint32_t part = z.last_lit & 63u;
+    if (part && (uint32_t)lane < part) syms[(z.last_lit & ~63u) + lane] = symreg;
+    s.lfreq[lane] = lf0; s.lfreq[64 + lane] = lf1; s.lfreq[128 + lane] = lf2; s.lfreq[192 + lane] = lf3;
+    if (lane < NLC - 256) s.lfreq[256 + lane] = lf4;
+    if (lane < NDC) s.dfreq[lane] = dfr;
+    hazard |= uni(flush_block(s, b, syms, in, z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, lane));
+    lf0 = lf1 = lf2 = lf3 = 0; lf4 = lane == 0 ? 1u : 0u; dfr = 0;
+    z.last_lit = 0;
+    z.block_start = (int64_t)z.p;
+  };
   uint32_t state = ~0u;
+  uint64_t fallbacks = 0, cyc_lookup = 0, cyc_fb = 0;
+  PosWin pw;
+  pw.init(A.R + tr.r_off);
   // zlib header (Z/deflate.c:738-759)
   {
     uint32_t header = (8u + ((uint32_t)(tr.window - 8) << 4)) << 8;
@@ -704,7 +853,14 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     header += 31 - (header % 31);
     put_bits(b, s.stage, ((header >> 8) & 0xff) | ((header & 0xff) << 8), 16, lane);
   }
-  if (KIND == 0) {
+  // hash_head of zlib after a window slide: NIL when it is exactly the slide offset S.  Only
+  // possible while p - S <= MAX_DIST (right at a slide); then the chain link is read directly.
+  auto head_is_S = [&]() -> bool {
+    if (z.S == 0 || z.p - z.S > z.maxdist) return false;
+    const uint32_t d = uni((uint32_t)ch[z.p]);
+    return d && z.p - d == z.S;
+  };
+  if constexpr (KIND == 0) {
     // deflate_stored (Z/deflate.c:1564-1619)
     uint64_t max_block = 0xffff;
     if (max_block > 4ull * z.lbs - 5) max_block = 4ull * z.lbs - 5;
@@ -716,110 +872,150 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       if (z.p == 0 || z.p >= max_start) {
         z.lookahead = z.p - max_start;
         z.p = max_start;
-        flush_block(z, bcx, 0, hazard, lane);
-        state = early_exit(b, A.o, tr.best_ident, full_needed);
+        FLUSH(0);
+        state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
         if (state != ~0u) break;
       }
       if (z.p - (uint64_t)z.block_start >= z.maxdist) {
-        flush_block(z, bcx, 0, hazard, lane);
-        state = early_exit(b, A.o, tr.best_ident, full_needed);
+        FLUSH(0);
+        state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
         if (state != ~0u) break;
       }
     }
-  } else if (KIND == 1) {
-    // deflate_fast (Z/deflate.c:1628-1722)
+  } else if constexpr (KIND == 1) {
+    // deflate_fast (Z/deflate.c:1628-1722).  The match table holds each position's walk over ALL
+    // same-hash positions; it equals deflate_fast's walk over the INSERTED ones unless a position
+    // this parse skipped (interior of a match longer than max_insert_length) lies in the walked
+    // range [p - reach, p) with the same hash -- detected through holes[] (per hash slot, the
+    // latest skipped position; slot collisions only cause extra exact walks).
+    uint32_t* holes = shm.holes;
+    for (int i = lane; i < (int)HOLE_SLOTS; i += 64) holes[i] = 0;
+    const uint32_t hbits = tr.memlevel + 7u, hmask = (1u << hbits) - 1u, hshift = (hbits + 2u) / 3u;
     for (;;) {
       if (z.lookahead < LOOKMIN) { fill(z); if (z.lookahead == 0) break; }
-      uint64_t hh = 0; bool hv = false;
+      if (z.p >= tr.x_lim) { state = TR_NEED_R; break; }
       // clear the insertion ring ahead of the positions about to be inserted
       while (z.ins_cleared < z.p + 300) {
         uint32_t wbase = (uint32_t)((z.ins_cleared & (BITMAP_BITS - 1)) >> 5);
         for (int i = lane; i < 32; i += 64) ins[(wbase + i) & (BITMAP_BITS / 32 - 1)] = 0;
         z.ins_cleared += 1024;
       }
+      const uint64_t cl0 = clock64();
+      const uint2 e = pw.get(z.p, lane);
       if (z.lookahead >= 3) {
         if (lane == 0) { uint32_t bq = (uint32_t)(z.p & (BITMAP_BITS - 1)); atomicOr(&ins[bq >> 5], 1u << (bq & 31)); }
-        // head[] = most recent inserted same-hash position
-        uint64_t q = z.p;
-        for (;;) {
-          uint32_t d = ch[q];
-          if (!d || q < d) break;
-          q -= d;
-          if (z.p - q > z.maxdist) break;
-          if (is_inserted<1>(ins, q)) { hh = q; hv = q > z.S; break; }
+        const uint32_t hl = uni(holes[(e.y >> 1) & (HOLE_SLOTS - 1)]);
+        if (hl == 0 || (uint64_t)(hl - 1) < z.p - (e.y >> 16)) {
+          if ((e.y & 1u) && !head_is_S()) {
+            const uint32_t len = e.x >> 23;
+            if (len > 2) { z.match_length = len; z.match_start = z.p - ((e.x >> 8) & 0x7fffu); }
+            else z.match_length = 2;
+          }
+        } else {
+          fallbacks++;
+          const uint64_t cf0 = clock64();
+          // head[] = most recent inserted same-hash position
+          uint64_t q = z.p, hh = 0;
+          bool hv = false;
+          for (;;) {
+            uint32_t d = uni((uint32_t)ch[q]);
+            if (!d || q < d) break;
+            q -= d;
+            if (z.p - q > z.maxdist) break;
+            if (uni((uint32_t)is_inserted<1>(ins, q))) { hh = q; hv = q > z.S; break; }
+          }
+          if (hv && z.p - hh <= z.maxdist) {
+            z.match_length = uni(longest_match<1>(z, in, ch, ins, hh, lane));
+            z.match_start = uni(z.match_start);
+          }
+          cyc_fb += clock64() - cf0;
         }
       }
-      if (hv && z.p - hh <= z.maxdist) z.match_length = longest_match<1>(z, in, ch, ins, hh, lane);
+      cyc_lookup += clock64() - cl0;
       bool bflush;
       if (z.match_length >= 3) {
-        bflush = tally_dist(z, bcx, (uint32_t)(z.p - z.match_start), z.match_length - 3, lane);
-        z.lookahead -= z.match_length;
-        if (z.match_length <= z.lazy && z.lookahead >= 3) {
-          if (lane == 0) {
-            for (uint32_t k = 1; k < z.match_length; k++) {
-              uint32_t bq = (uint32_t)((z.p + k) & (BITMAP_BITS - 1));
-              atomicOr(&ins[bq >> 5], 1u << (bq & 31));
+        const uint32_t ml = z.match_length;
+        bflush = tally_dist((uint32_t)(z.p - z.match_start), ml - 3);
+        z.lookahead -= ml;
+        if (ml <= z.lazy && z.lookahead >= 3) {
+          if (lane >= 1 && (uint32_t)lane < ml) {
+            uint32_t bq = (uint32_t)((z.p + lane) & (BITMAP_BITS - 1));
+            atomicOr(&ins[bq >> 5], 1u << (bq & 31));
+          }
+        } else {
+          // p+1 .. p+ml-1 are not inserted: record them per hash slot
+          for (uint32_t k0 = 1; k0 < ml; k0 += 64) {
+            const uint64_t q = z.p + k0 + lane;
+            if (k0 + lane < ml && q + 3 <= z.n) {
+              const uint32_t hq = (((uint32_t)in[q] << (2 * hshift)) ^ ((uint32_t)in[q + 1] << hshift) ^ in[q + 2]) & hmask;
+              atomicMax(&holes[hq & (HOLE_SLOTS - 1)], (uint32_t)(q + 1));
             }
           }
         }
-        z.p += z.match_length;
+        z.p += ml;
         z.match_length = 0;
       } else {
-        bflush = tally_lit(z, bcx, in[z.p], lane);
+        bflush = tally_lit(e.x & 0xffu);
         z.lookahead--;
         z.p++;
       }
       if (bflush) {
-        flush_block(z, bcx, 0, hazard, lane);
-        state = early_exit(b, A.o, tr.best_ident, full_needed);
+        FLUSH(0);
+        state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
         if (state != ~0u) break;
       }
     }
   } else {
-    // deflate_slow (Z/deflate.c:1730-1853)
+    // deflate_slow (Z/deflate.c:1730-1853) reading longest_match's results from the match table
+    uint32_t prev_byte = 0;   // input byte at strstart - 1 (the lazily held literal)
     for (;;) {
       if (z.lookahead < LOOKMIN) { fill(z); if (z.lookahead == 0) break; }
-      uint64_t hh = 0; bool hv = false;
-      if (z.lookahead >= 3) {
-        uint32_t d = ch[z.p];
-        if (d && z.p >= d) { hh = z.p - d; hv = hh > z.S; }
-      }
+      if (z.p >= tr.x_lim) { state = TR_NEED_R; break; }
+      const uint64_t cl0 = clock64();
+      const uint2 e = pw.get(z.p, lane);
+      const bool hv = z.lookahead >= 3 && (e.y & 1u) && !head_is_S();
       z.prev_length = z.match_length; z.prev_match = z.match_start;
       z.match_length = 2;
-      if (hv && z.prev_length < z.lazy && z.p - hh <= z.maxdist) {
-        z.match_length = longest_match<2>(z, in, ch, nullptr, hh, lane);
+      if (hv && z.prev_length < z.lazy) {
+        const uint32_t ev = z.prev_length >= z.good ? e.y : e.x;
+        const uint32_t len = ev >> 23;
+        if (len > z.prev_length) { z.match_length = len; z.match_start = z.p - ((ev >> 8) & 0x7fffu); }
+        else z.match_length = z.prev_length <= z.lookahead ? z.prev_length : (uint32_t)z.lookahead;
         if (z.match_length == 3 && z.p - z.match_start > 4096) z.match_length = 2;
       }
+      cyc_lookup += clock64() - cl0;
       if (z.prev_length >= 3 && z.match_length <= z.prev_length) {
-        bool bflush = tally_dist(z, bcx, (uint32_t)(z.p - 1 - z.prev_match), z.prev_length - 3, lane);
+        bool bflush = tally_dist((uint32_t)(z.p - 1 - z.prev_match), z.prev_length - 3);
         z.lookahead -= z.prev_length - 1;
         z.p += z.prev_length - 1;
         z.match_available = 0;
         z.match_length = 2;
         if (bflush) {
-          flush_block(z, bcx, 0, hazard, lane);
-          state = early_exit(b, A.o, tr.best_ident, full_needed);
+          FLUSH(0);
+          state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
           if (state != ~0u) break;
         }
       } else if (z.match_available) {
-        bool bflush = tally_lit(z, bcx, in[z.p - 1], lane);
+        bool bflush = tally_lit(prev_byte);
+        prev_byte = e.x & 0xffu;
         if (bflush) {
-          flush_block(z, bcx, 0, hazard, lane);
-          state = early_exit(b, A.o, tr.best_ident, full_needed);
+          FLUSH(0);
+          state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
           if (state != ~0u) break;
         }
         z.p++;
         z.lookahead--;
       } else {
+        prev_byte = e.x & 0xffu;
         z.match_available = 1;
         z.p++;
         z.lookahead--;
       }
     }
-    if (state == ~0u && z.match_available) { tally_lit(z, bcx, in[z.p - 1], lane); z.match_available = 0; }
+    if (state == ~0u && z.match_available) { tally_lit(prev_byte); z.match_available = 0; }
   }
   if (state == ~0u) {
-    flush_block(z, bcx, 1, hazard, lane);
+    FLUSH(1);
     // adler32 trailer
     uint32_t ad = A.adler[tr.stream];
     uint32_t be = ((ad >> 24) & 0xff) | ((ad >> 8) & 0xff00) | ((ad << 8) & 0xff0000) | (ad << 24);
@@ -846,6 +1042,13 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     r.ident = b.eq_all;
     r.symbols = z.nsym;
     r.parsed = z.p;
+    r.fallbacks = fallbacks;
+    r.cyc_total = clock64() - cstart;
+    r.cyc_tree = b.cyc_tree;
+    r.cyc_emit = b.cyc_emit;
+    r.blocks = b.blocks;
+    r.cyc_lookup = cyc_lookup;
+    r.cyc_fallback = cyc_fb;
     A.res[t] = r;
   }
 }

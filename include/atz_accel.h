@@ -65,6 +65,13 @@ typedef struct {
     uint64_t k_trial_launches, k_inflate_launches, k_chains_launches;
     uint64_t k_trial_alg_bytes, k_inflate_alg_bytes, k_chains_alg_bytes;
     uint64_t trial_parsed_bytes;                         /* inflated bytes the trials actually parsed */
+    double k_match_ms;                                   /* match-table kernel (longest_match per position) */
+    uint64_t k_match_launches, k_match_positions;
+    uint64_t n_trials_rerun;                             /* trials run again after extending their match table */
+    uint64_t n_fast_fallbacks;                           /* fast-level steps that walked a chain in the parse */
+    uint64_t trial_cyc_total, trial_cyc_tree, trial_cyc_emit, trial_blocks;  /* shader clocks summed over trials */
+    uint64_t trial_cyc_lookup, trial_cyc_fallback, trial_symbols;
+    uint64_t n_trials_speculative;                       /* trials run ahead of a stream's stop and discarded */
 } atz_stats_t;
 
 enum {
