@@ -65,6 +65,24 @@ def cpu_baseline(n_streams, seed):
                       "%.1f s wall" % (n_streams, len(data) / 1e6, seed, dt)}
 
 
+def aggregate(dt, atz_len, shard_bytes, steps, world, device):
+    """Cross-rank reduction of one timed run: max step time over ranks, per-rank ATZ sizes.
+    value = bytes all ranks processed / the slowest rank's time (weak scaling: one shard per rank)."""
+    import torch
+    import torch.distributed as dist
+    tmax = torch.tensor([dt], dtype=torch.float64, device=device)
+    sizes = torch.tensor([float(atz_len)], dtype=torch.float64, device=device)
+    gathered = [sizes]
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        gathered = [torch.zeros_like(sizes) for _ in range(world)]
+        dist.all_gather(gathered, sizes)
+    dt = float(tmax.item())
+    total_bytes = shard_bytes * world
+    value = total_bytes / 1e6 / (dt / steps)
+    return dt, value, [int(g.item()) for g in gathered]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,16 +137,8 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    tmax = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    sizes = torch.tensor([float(n)], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        gathered = [torch.zeros_like(sizes) for _ in range(world)]
-        dist.all_gather(gathered, sizes)
-    dt = float(tmax.item())
+    dt, value, atz_sizes = aggregate(dt, n, len(data), args.steps, world, "cuda")
     ms_per_step = dt * 1000.0 / args.steps
-    total_bytes = len(data) * world          # every rank: one shard of the same size per step
-    value = total_bytes / 1e6 / (dt / args.steps)
 
     last = stats[-1]
     ktime = last["k_trial_ms"] / 1000.0
@@ -164,6 +174,7 @@ def main():
                        "streams_per_gpu": args.streams, "bytes_per_gpu": len(data), "parallelism": "stream-sharded dp%d" % world},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "atz_bytes_per_rank": atz_sizes,
             "detail": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in last.items()},
         }
         print(json.dumps(out), flush=True)
