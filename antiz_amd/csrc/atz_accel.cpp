@@ -318,7 +318,7 @@ static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, con
   if (int r = c->d_res.reserve(jobs.size() * sizeof(InfRes))) return r;
   uint32_t n = (uint32_t)jobs.size();
   kbeg(c, 1);
-  hipLaunchKernelGGL(k_inflate, dim3((n + INF_WAVES - 1) / INF_WAVES), dim3(64 * INF_WAVES), 0, c->st, d_in,
+  hipLaunchKernelGGL(k_inflate, dim3(n), dim3(64), 0, c->st, d_in,
                      d_out, c->d_jobs.as<InfJob>(), c->d_res.as<InfRes>(), n);
   kend(c);
   KCHECK("k_inflate");

@@ -15,7 +15,6 @@
 
 namespace atz {
 
-static constexpr int INF_WAVES = 4;           // waves (= jobs) per workgroup
 static constexpr uint32_t RING = 32768;        // history ring per wave (LDS)
 static constexpr uint32_t RMASK = RING - 1;
 static constexpr uint32_t FLUSH_AT = 16384;    // flush ring to HBM / Adler every 16 KiB
@@ -84,147 +83,10 @@ __global__ __launch_bounds__(256) void k_find_headers(const uint8_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------
-struct BitReader {
-  const uint32_t* abase;  // 4-byte aligned base of the input
-  uint64_t limit;         // bit limit in aligned coordinates
-  uint64_t skip_bits;     // 8 * (misalignment of the job's first byte)
-  uint64_t pos;           // aligned bit position of bb's bit 0
-  uint64_t bb;
-  uint32_t bc;
-  uint64_t next_dw;
-  uint64_t chunk;
-  uint32_t cw;            // this lane's dword of the staged 256-byte chunk
-};
+// k_inflate: one wavefront per job, everything inlined into the kernel so the decoder state stays
+// in (wave-uniform) SGPRs -- a by-reference state struct crossing a call would live in scratch.
 
-__device__ inline void br_load_chunk(BitReader& r, uint64_t ch, int lane) {
-  uint64_t dw = ch * 64 + lane;
-  uint64_t byte0 = dw * 4;
-  uint64_t lim_b = r.limit >> 3;
-  uint32_t v = 0;
-  if (byte0 < lim_b) {
-    v = r.abase[dw];
-    uint64_t valid = lim_b - byte0;
-    if (valid < 4) v &= (1u << (8 * valid)) - 1;
-  }
-  r.cw = v;
-  r.chunk = ch;
-}
-
-__device__ inline void br_refill(BitReader& r, int lane) {
-  while (r.bc <= 32) {
-    uint64_t k = r.next_dw;
-    uint64_t ch = k >> 6;
-    if (ch != r.chunk) br_load_chunk(r, ch, lane);
-    uint32_t w = __builtin_amdgcn_readlane(r.cw, (int)(k & 63));
-    r.bb |= (uint64_t)w << r.bc;
-    r.bc += 32;
-    r.next_dw = k + 1;
-  }
-}
-
-__device__ inline void br_seek(BitReader& r, uint64_t apos, int lane) {
-  r.bb = 0; r.bc = 0;
-  r.next_dw = apos >> 5;
-  r.pos = apos & ~31ull;
-  br_refill(r, lane);
-  uint32_t d = (uint32_t)(apos & 31);
-  r.bb >>= d; r.bc -= d; r.pos += d;
-  br_refill(r, lane);
-}
-
-__device__ inline uint32_t br_peek(const BitReader& r, uint32_t k) {
-  return (uint32_t)(r.bb & ((k >= 32) ? 0xffffffffull : ((1ull << k) - 1)));
-}
-__device__ inline void br_drop(BitReader& r, uint32_t k, int lane) {
-  r.bb >>= k; r.bc -= k; r.pos += k;
-  if (r.bc <= 32) br_refill(r, lane);
-}
-__device__ inline bool br_has(const BitReader& r, uint64_t k) { return r.pos + k <= r.limit; }
-
-// Per-wave canonical Huffman code: lane l (1..15) holds the values for code length l.
-struct Huff {
-  uint32_t first, count, offs;  // per-lane registers
-  int max;                      // longest length (0: empty)
-  int incomplete;               // incomplete (only legal with max==1) or empty
-};
-
-// inflate_table acceptance (Z/inftrees.c:32-141); type 0 CODES, 1 LENS, 2 DISTS. Returns 0 / -1.
-__device__ int huff_build(Huff& h, const uint16_t* lens, int n, int type, uint16_t* syms, int lane) {
-  uint32_t cnt = 0;
-  for (int g = 0; g < n; g += 64) {
-    int i = g + lane;
-    uint32_t len = i < n ? lens[i] : 0;
-    for (int l = 1; l <= 15; l++) {
-      uint32_t c = __popcll(__ballot(len == (uint32_t)l));
-      if (lane == l) cnt += c;
-    }
-  }
-  int max = 0;
-  int left = 1;
-  int bad = 0;
-  uint32_t code = 0, offs = 0;
-  uint32_t my_first = 0, my_offs = 0;
-  for (int l = 1; l <= 15; l++) {
-    uint32_t c = __builtin_amdgcn_readlane(cnt, l);
-    if (c) max = l;
-    left <<= 1;
-    left -= (int)c;
-    if (left < 0) bad = 1;
-    if (lane == l) { my_first = code; my_offs = offs; }
-    code = (code + c) << 1;
-    offs += c;
-  }
-  h.max = max;
-  h.incomplete = 0;
-  if (max == 0) { h.incomplete = 1; h.count = 0; h.first = 0; h.offs = 0; return 0; }
-  if (bad) return -1;
-  if (left > 0 && (type == 0 || max != 1)) return -1;
-  if (left > 0) h.incomplete = 1;
-  h.first = my_first; h.count = (lane >= 1 && lane <= 15) ? cnt : 0; h.offs = my_offs;
-  // ballot-ranked symbol sort: syms[offs_l + rank] = i
-  uint32_t run = my_offs;
-  for (int g = 0; g < n; g += 64) {
-    int i = g + lane;
-    uint32_t len = i < n ? lens[i] : 0;
-    uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int l = 1; l <= 15; l++) {
-      uint64_t m = __ballot(len == (uint32_t)l);
-      if (!m) continue;
-      uint32_t base = __builtin_amdgcn_readlane(run, l);
-      if (len == (uint32_t)l) syms[base + __popcll(m & lt)] = (uint16_t)i;
-      if (lane == l) run += __popcll(m);
-    }
-  }
-  return 0;
-}
-
-// Decode one symbol. Returns symbol >= 0, -1 invalid code (bits already dropped/accounted in *need),
-// -2 need more input.  *need receives the relative bit position zlib would have required.
-__device__ inline int huff_decode(BitReader& r, const Huff& h, const uint16_t* syms, int lane,
-                                  bool cl_quirk, uint64_t& need) {
-  if (h.max == 0) {
-    need = r.pos + 1;
-    if (!br_has(r, 1)) return -2;
-    br_drop(r, 1, lane);
-    return cl_quirk ? 0 : -1;
-  }
-  uint32_t v = __builtin_bitreverse32((uint32_t)r.bb) >> 17;   // first stream bit at bit 14
-  uint32_t c = v >> (15 - (lane & 15));
-  bool hit = lane >= 1 && lane <= 15 && (c - h.first) < h.count;
-  uint64_t m = __ballot(hit);
-  if (!m) {  // only incomplete codes have unused patterns: zlib's invalid entry has 1 bit
-    need = r.pos + 1;
-    if (!br_has(r, 1)) return -2;
-    br_drop(r, 1, lane);
-    return -1;
-  }
-  int L = __ffsll((unsigned long long)m) - 1;
-  need = r.pos + (uint64_t)L;
-  if (!br_has(r, (uint64_t)L)) return -2;
-  uint32_t idx = __builtin_amdgcn_readlane(h.offs + (c - h.first), L);
-  br_drop(r, (uint32_t)L, lane);
-  return syms[idx];
-}
+__device__ __forceinline__ uint32_t iuni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 __device__ __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
                                                 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -237,7 +99,7 @@ __device__ __constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4
                                               6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __device__ __constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-__device__ inline uint64_t wave_sum_u64(uint64_t v) {
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   for (int d = 32; d >= 1; d >>= 1) {
     uint32_t lo = __shfl_xor((uint32_t)v, d, 64);
     uint32_t hi = __shfl_xor((uint32_t)(v >> 32), d, 64);
@@ -246,262 +108,378 @@ __device__ inline uint64_t wave_sum_u64(uint64_t v) {
   return v;
 }
 
-struct OutState {
-  uint8_t* out;       // HBM output (nullptr: discard)
-  uint64_t out_cap;
-  uint64_t prod;      // bytes produced
-  uint64_t flushed;   // bytes folded into Adler / written to HBM
-  uint32_t a, b;      // Adler-32 halves
-  int overflow;
+// Canonical Huffman code of one table: lane l (1..15) holds first-code/count/offset of length l;
+// the sorted symbols live in VGPRs (entry e in lane e & 63, register e >> 6) and are read with
+// v_readlane at a wave-uniform index -- no memory access per decoded symbol.
+struct Huff {
+  uint32_t first, count, offs;
+  uint32_t s0, s1, s2, s3, s4;
+  int max;
+  __device__ __forceinline__ uint32_t sym(uint32_t e) const {
+    uint32_t v;
+    switch (e >> 6) {
+      case 0: v = s0; break;
+      case 1: v = s1; break;
+      case 2: v = s2; break;
+      case 3: v = s3; break;
+      default: v = s4; break;
+    }
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(e & 63));
+  }
 };
-
-__device__ void ring_flush(OutState& o, const uint8_t* ring, int lane) {
-  uint64_t n = o.prod - o.flushed;
-  if (!n) return;
-  uint64_t S = 0, W = 0;
-  for (uint64_t k = lane; k < n; k += 64) {
-    uint32_t x = ring[(o.flushed + k) & RMASK];
-    S += x;
-    W += (n - k) * x;
-    if (o.out && o.flushed + k < o.out_cap) o.out[o.flushed + k] = (uint8_t)x;
-  }
-  S = wave_sum_u64(S);
-  W = wave_sum_u64(W);
-  uint64_t a = o.a, b = o.b;
-  b = (b + (n % 65521) * a + W) % 65521;
-  a = (a + S) % 65521;
-  o.a = (uint32_t)a; o.b = (uint32_t)b;
-  if (o.out && o.prod > o.out_cap) o.overflow = 1;
-  o.flushed = o.prod;
-}
-
-__device__ inline void put_lit(OutState& o, uint8_t* ring, uint32_t sym, int lane) {
-  if (lane == 0) ring[o.prod & RMASK] = (uint8_t)sym;
-  o.prod++;
-  if (o.prod - o.flushed >= FLUSH_AT) ring_flush(o, ring, lane);
-}
-
-__device__ inline void put_copy(OutState& o, uint8_t* ring, uint32_t len, uint32_t dist, int lane) {
-  uint8_t v[5];
-#pragma unroll
-  for (int r = 0; r < 5; r++) {
-    uint32_t i = lane + 64 * r;
-    uint32_t src = dist >= len ? i : i % dist;
-    v[r] = i < len ? ring[(o.prod - dist + src) & RMASK] : 0;
-  }
-#pragma unroll
-  for (int r = 0; r < 5; r++) {
-    uint32_t i = lane + 64 * r;
-    if (i < len) ring[(o.prod + i) & RMASK] = v[r];
-  }
-  o.prod += len;
-  if (o.prod - o.flushed >= FLUSH_AT) ring_flush(o, ring, lane);
-}
 
 enum { R_OK = 0, R_ERR = -1, R_NEED = -2 };
 
-struct Ctx {
-  BitReader r;
-  OutState o;
-  uint64_t errneed;  // aligned bit position required by the failing item
-  uint32_t errcode;
-};
-
-#define NEEDB(k) do { if (!br_has(c.r, (k))) return R_NEED; } while (0)
-#define FAIL(code, needpos) do { c.errneed = (needpos); c.errcode = (code); return R_ERR; } while (0)
-
-__device__ int decode_codes(Ctx& c, const Huff& lh, const uint16_t* lsym, const Huff& dh,
-                            const uint16_t* dsym, uint8_t* ring, int lane) {
-  uint64_t need;
-  for (;;) {
-    int sym = huff_decode(c.r, lh, lsym, lane, false, need);
-    if (sym == -2) return R_NEED;
-    if (sym == -1) FAIL(10, need);
-    if (sym < 256) { put_lit(c.o, ring, (uint32_t)sym, lane); continue; }
-    if (sym == 256) return R_OK;
-    sym -= 257;
-    if (sym >= 29) FAIL(11, need);                       // fixed codes 286/287
-    uint32_t le = c_lext[sym];
-    NEEDB(le);
-    uint32_t len = c_lbase[sym] + br_peek(c.r, le);
-    br_drop(c.r, le, lane);
-    int ds = huff_decode(c.r, dh, dsym, lane, false, need);
-    if (ds == -2) return R_NEED;
-    if (ds == -1) FAIL(12, need);
-    if (ds >= 30) FAIL(13, need);                        // fixed distance 30/31
-    uint32_t de = c_dext[ds];
-    NEEDB(de);
-    uint32_t dist = c_dbase[ds] + br_peek(c.r, de);
-    br_drop(c.r, de, lane);
-    if ((uint64_t)dist > c.o.prod) FAIL(14, c.r.pos);     // invalid distance too far back
-    put_copy(c.o, ring, len, dist, lane);
-  }
-}
-
-__device__ int inflate_body(Ctx& c, uint8_t* ring, uint16_t* lsym, uint16_t* dsym, uint16_t* csym,
-                            uint16_t* lens, int lane) {
-  // HEAD (Z/inflate.c:640-685): wrap=1, wbits=15
-  NEEDB(16);
-  uint32_t cmf = br_peek(c.r, 8);
-  uint32_t flg = (br_peek(c.r, 16) >> 8) & 0xff;
-  if (((cmf << 8) + flg) % 31) FAIL(1, c.r.pos + 16);
-  if ((cmf & 15) != 8) FAIL(2, c.r.pos + 16);
-  if ((cmf >> 4) + 8 > 15) FAIL(3, c.r.pos + 16);
-  br_drop(c.r, 16, lane);
-  if (flg & 0x20) { NEEDB(32); FAIL(4, c.r.pos + 32); }   // preset dictionary: not a stream end
-  int last;
-  do {
-    NEEDB(3);
-    last = (int)br_peek(c.r, 1);
-    uint32_t type = (br_peek(c.r, 3) >> 1) & 3;
-    br_drop(c.r, 3, lane);
-    if (type == 0) {                                      // STORED
-      uint32_t al = (uint32_t)((8 - (c.r.pos & 7)) & 7);
-      br_drop(c.r, al, lane);
-      NEEDB(32);
-      uint32_t len = br_peek(c.r, 16);
-      uint32_t nlen = (br_peek(c.r, 32) >> 16) & 0xffff;
-      if (len != (~nlen & 0xffff)) FAIL(5, c.r.pos + 32);
-      br_drop(c.r, 32, lane);
-      // copy `len` bytes straight from the input (byte aligned now)
-      uint64_t avail = (c.r.limit - c.r.pos) >> 3;
-      uint64_t take = len < avail ? len : avail;
-      const uint8_t* src = reinterpret_cast<const uint8_t*>(c.r.abase) + (c.r.pos >> 3);
-      uint64_t done = 0;
-      while (done < take) {
-        uint64_t step = take - done;
-        if (step > 4096) step = 4096;
-        uint64_t room = RING - (c.o.prod - c.o.flushed);
-        if (step > room) { ring_flush(c.o, ring, lane); continue; }
-        for (uint64_t k = lane; k < step; k += 64) ring[(c.o.prod + k) & RMASK] = src[done + k];
-        c.o.prod += step;
-        done += step;
-        if (c.o.prod - c.o.flushed >= FLUSH_AT) ring_flush(c.o, ring, lane);
-      }
-      br_seek(c.r, c.r.pos + 8 * take, lane);
-      if (take < len) return R_NEED;
-    } else if (type == 1) {                               // FIXED
-      for (int i = lane; i < 288; i += 64) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
-      Huff lh, dh;
-      huff_build(lh, lens, 288, 1, lsym, lane);
-      for (int i = lane; i < 32; i += 64) lens[i] = 5;
-      huff_build(dh, lens, 32, 2, dsym, lane);
-      int rr = decode_codes(c, lh, lsym, dh, dsym, ring, lane);
-      if (rr != R_OK) return rr;
-    } else if (type == 2) {                               // DYNAMIC (Z/inflate.c:908-1013)
-      NEEDB(14);
-      uint32_t nlen = br_peek(c.r, 5) + 257;
-      uint32_t ndist = ((br_peek(c.r, 10) >> 5) & 31) + 1;
-      uint32_t ncode = ((br_peek(c.r, 14) >> 10) & 15) + 4;
-      if (nlen > 286 || ndist > 30) FAIL(6, c.r.pos + 14);
-      br_drop(c.r, 14, lane);
-      for (int i = lane; i < 320; i += 64) lens[i] = 0;
-      for (uint32_t i = 0; i < ncode; i++) {
-        NEEDB(3);
-        uint32_t v = br_peek(c.r, 3);
-        br_drop(c.r, 3, lane);
-        if (lane == 0) lens[c_clorder[i]] = (uint16_t)v;
-      }
-      Huff ch;
-      if (huff_build(ch, lens, 19, 0, csym, lane)) FAIL(7, c.r.pos);
-      uint32_t have = 0;
-      uint32_t total = nlen + ndist;
-      uint64_t need;
-      for (int i = lane; i < 320; i += 64) lens[i] = 0;
-      while (have < total) {
-        int sym = huff_decode(c.r, ch, csym, lane, true, need);
-        if (sym == -2) return R_NEED;
-        if (sym < 16) { if (lane == 0) lens[have] = (uint16_t)sym; have++; continue; }
-        uint32_t copy, len = 0, eb;
-        if (sym == 16) eb = 2; else if (sym == 17) eb = 3; else eb = 7;
-        NEEDB(eb);
-        if (sym == 16) {
-          if (have == 0) FAIL(8, c.r.pos + eb);
-          len = lens[have - 1];
-          copy = 3 + br_peek(c.r, 2);
-        } else if (sym == 17) {
-          copy = 3 + br_peek(c.r, 3);
-        } else {
-          copy = 11 + br_peek(c.r, 7);
-        }
-        br_drop(c.r, eb, lane);
-        if (have + copy > total) FAIL(8, c.r.pos);
-        for (uint32_t k = lane; k < copy; k += 64) lens[have + k] = (uint16_t)len;
-        have += copy;
-      }
-      if (lens[256] == 0) FAIL(9, c.r.pos);
-      Huff lh, dh;
-      if (huff_build(lh, lens, (int)nlen, 1, lsym, lane)) FAIL(9, c.r.pos);
-      if (huff_build(dh, lens + nlen, (int)ndist, 2, dsym, lane)) FAIL(9, c.r.pos);
-      int rr = decode_codes(c, lh, lsym, dh, dsym, ring, lane);
-      if (rr != R_OK) return rr;
-    } else {
-      FAIL(15, c.r.pos);                                  // invalid block type
-    }
-  } while (!last);
-  // CHECK (Z/inflate.c:1174-1195)
-  uint32_t al = (uint32_t)((8 - (c.r.pos & 7)) & 7);
-  br_drop(c.r, al, lane);
-  NEEDB(32);
-  uint32_t t = br_peek(c.r, 32);
-  uint32_t want = ((t & 0xff) << 24) | ((t & 0xff00) << 8) | ((t >> 8) & 0xff00) | (t >> 24);
-  br_drop(c.r, 32, lane);
-  ring_flush(c.o, ring, lane);
-  uint32_t adler = (c.o.b << 16) | c.o.a;
-  if (want != adler) FAIL(16, c.r.pos);
-  return R_OK;
-}
-
 struct InfShared {
-  uint8_t ring[INF_WAVES][RING];
-  uint16_t lsym[INF_WAVES][320];
-  uint16_t dsym[INF_WAVES][32];
-  uint16_t csym[INF_WAVES][32];
-  uint16_t lens[INF_WAVES][320];
+  uint8_t ring[RING];
+  uint16_t lens[320];
+  uint16_t sort[320];
 };
 
-__global__ __launch_bounds__(64 * INF_WAVES) void k_inflate(const uint8_t* __restrict__ in_base,
-                                                           uint8_t* __restrict__ out_base,
-                                                           const InfJob* __restrict__ jobs,
-                                                           InfRes* __restrict__ res, uint32_t njobs) {
+__global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_base, uint8_t* __restrict__ out_base,
+                                               const InfJob* __restrict__ jobs, InfRes* __restrict__ res,
+                                               uint32_t njobs) {
   __shared__ InfShared sh;
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const uint32_t j = blockIdx.x * INF_WAVES + wave;
+  const int lane = threadIdx.x;
+  const uint32_t j = blockIdx.x;
   if (j >= njobs) return;
   const InfJob job = jobs[j];
-  Ctx c;
-  const uint8_t* p = in_base + job.in_off;
-  uintptr_t ap = reinterpret_cast<uintptr_t>(p);
-  uint64_t skip = ap & 3;
-  c.r.abase = reinterpret_cast<const uint32_t*>(ap - skip);
-  c.r.skip_bits = 8 * skip;
-  c.r.limit = 8 * (skip + job.in_len);
-  c.r.chunk = ~0ull;
-  c.r.cw = 0;
-  br_seek(c.r, 8 * skip, lane);
-  c.o.out = job.out_off == NO_OUT ? nullptr : out_base + job.out_off;
-  c.o.out_cap = job.out_cap;
-  c.o.prod = 0; c.o.flushed = 0; c.o.a = 1; c.o.b = 0; c.o.overflow = 0;
-  c.errneed = 0; c.errcode = 0;
-  int rr = inflate_body(c, sh.ring[wave], sh.lsym[wave], sh.dsym[wave], sh.csym[wave], sh.lens[wave], lane);
-  InfRes out;
-  out.produced = c.o.prod;
-  out.err = c.errcode;
-  if (rr == R_OK && !c.o.overflow) {
-    out.status = INF_END;
-    out.consumed = (c.r.pos - c.r.skip_bits) >> 3;
+  uint8_t* const ring = sh.ring;
+  uint16_t* const lens = sh.lens;
+
+  // ---- bit reader over the job's bytes: 256-byte windows staged in lane VGPRs, next one in flight
+  const uint8_t* p0 = in_base + job.in_off;
+  const uintptr_t ap = reinterpret_cast<uintptr_t>(p0);
+  const uint64_t skip = ap & 3;
+  const uint32_t* const abase = reinterpret_cast<const uint32_t*>(ap - skip);
+  const uint64_t skip_bits = 8 * skip;
+  const uint64_t limit = 8 * (skip + job.in_len);   // bit limit (aligned coordinates)
+  const uint64_t lim_b = limit >> 3;
+  uint64_t pos = 0, bb = 0, next_dw = 0, wbase = 1ull << 62;
+  uint32_t bc = 0, cw = 0, nw = 0;
+  auto load_dw = [&](uint64_t dw) __attribute__((always_inline)) -> uint32_t {
+    const uint64_t byte0 = dw * 4;
+    uint32_t v = 0;
+    if (byte0 < lim_b) {
+      v = abase[dw];
+      const uint64_t valid = lim_b - byte0;
+      if (valid < 4) v &= (1u << (8 * valid)) - 1;
+    }
+    return v;
+  };
+  auto refill = [&]() __attribute__((always_inline)) {
+    while (bc <= 32) {
+      const uint64_t k = next_dw;
+      if (k - wbase >= 64) {
+        if (k - wbase < 128) { cw = nw; wbase += 64; }
+        else { wbase = k & ~63ull; cw = load_dw(wbase + lane); }
+        nw = load_dw(wbase + 64 + lane);
+      }
+      const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cw, (int)(k - wbase));
+      bb |= (uint64_t)w << bc;
+      bc += 32;
+      next_dw = k + 1;
+    }
+  };
+  auto seek = [&](uint64_t apos) __attribute__((always_inline)) {
+    bb = 0; bc = 0;
+    next_dw = apos >> 5;
+    pos = apos & ~31ull;
+    refill();
+    const uint32_t d = (uint32_t)(apos & 31);
+    bb >>= d; bc -= d; pos += d;
+    refill();
+  };
+  auto peek = [&](uint32_t k) __attribute__((always_inline)) -> uint32_t { return (uint32_t)(bb & ((k >= 32) ? 0xffffffffull : ((1ull << k) - 1))); };
+  auto drop = [&](uint32_t k) __attribute__((always_inline)) { bb >>= k; bc -= k; pos += k; if (bc <= 32) refill(); };
+  auto has = [&](uint64_t k) __attribute__((always_inline)) -> bool { return pos + k <= limit; };
+
+  // ---- output: LDS history ring, flushed to HBM (if kept) and folded into Adler-32 every 16 KiB
+  uint8_t* const out = job.out_off == NO_OUT ? nullptr : out_base + job.out_off;
+  const uint64_t out_cap = job.out_cap;
+  uint64_t prod = 0, flushed = 0;
+  uint32_t ad_a = 1, ad_b = 0;
+  int overflow = 0;
+  auto flush = [&]() __attribute__((always_inline)) {
+    const uint64_t n = prod - flushed;
+    if (!n) return;
+    uint64_t S = 0, W = 0;
+    for (uint64_t k = lane; k < n; k += 64) {
+      const uint32_t x = ring[(flushed + k) & RMASK];
+      S += x;
+      W += (n - k) * x;
+      if (out && flushed + k < out_cap) out[flushed + k] = (uint8_t)x;
+    }
+    S = wave_sum_u64(S);
+    W = wave_sum_u64(W);
+    uint64_t a = ad_a, b = ad_b;
+    b = (b + (n % 65521) * a + W) % 65521;
+    a = (a + S) % 65521;
+    ad_a = iuni((uint32_t)a); ad_b = iuni((uint32_t)b);
+    if (out && prod > out_cap) overflow = 1;
+    flushed = prod;
+  };
+
+  // inflate_table acceptance (Z/inftrees.c:32-141); type 0 CODES, 1 LENS, 2 DISTS. Returns 0 / -1.
+  auto build = [&](Huff& h, const uint16_t* ln, int n, int type) __attribute__((always_inline)) -> int {
+    uint32_t cnt = 0;
+    for (int g = 0; g < n; g += 64) {
+      const int i = g + lane;
+      const uint32_t len = i < n ? ln[i] : 0;
+      for (int l = 1; l <= 15; l++) {
+        const uint32_t c = __popcll(__ballot(len == (uint32_t)l));
+        if (lane == l) cnt += c;
+      }
+    }
+    int max = 0, left = 1, bad = 0;
+    uint32_t code = 0, offs = 0, my_first = 0, my_offs = 0;
+    for (int l = 1; l <= 15; l++) {
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cnt, l);
+      if (c) max = l;
+      left <<= 1;
+      left -= (int)c;
+      if (left < 0) bad = 1;
+      if (lane == l) { my_first = code; my_offs = offs; }
+      code = (code + c) << 1;
+      offs += c;
+    }
+    h.max = max;
+    if (max == 0) { h.count = 0; h.first = 0; h.offs = 0; return 0; }
+    if (bad) return -1;
+    if (left > 0 && (type == 0 || max != 1)) return -1;
+    h.first = my_first; h.count = (lane >= 1 && lane <= 15) ? cnt : 0; h.offs = my_offs;
+    // ballot-ranked counting sort into LDS, then into the VGPR table
+    uint32_t run = my_offs;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int g = 0; g < n; g += 64) {
+      const int i = g + lane;
+      const uint32_t len = i < n ? ln[i] : 0;
+      for (int l = 1; l <= 15; l++) {
+        const uint64_t m = __ballot(len == (uint32_t)l);
+        if (!m) continue;
+        const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)run, l);
+        if (len == (uint32_t)l) sh.sort[base + __popcll(m & lt)] = (uint16_t)i;
+        if (lane == l) run += __popcll(m);
+      }
+    }
+    h.s0 = sh.sort[lane];
+    h.s1 = n > 64 ? sh.sort[64 + lane] : 0;
+    h.s2 = n > 128 ? sh.sort[128 + lane] : 0;
+    h.s3 = n > 192 ? sh.sort[192 + lane] : 0;
+    h.s4 = n > 256 && lane < 64 ? sh.sort[256 + lane] : 0;
+    return 0;
+  };
+
+  // Decode one symbol: >= 0 symbol, -1 invalid code, -2 need more input.  need = the bit position
+  // zlib would have required when it stops here.
+  auto decode = [&](const Huff& h, bool cl_quirk, uint64_t& need) __attribute__((always_inline)) -> int {
+    if (h.max == 0) {
+      need = pos + 1;
+      if (!has(1)) return -2;
+      drop(1);
+      return cl_quirk ? 0 : -1;
+    }
+    const uint32_t v = __builtin_bitreverse32((uint32_t)bb) >> 17;   // first stream bit at bit 14
+    const uint32_t c = v >> (15 - (lane & 15));
+    const bool hit = lane >= 1 && lane <= 15 && (c - h.first) < h.count;
+    const uint64_t m = __ballot(hit);
+    if (!m) {  // only incomplete codes have unused patterns: zlib's invalid entry has 1 bit
+      need = pos + 1;
+      if (!has(1)) return -2;
+      drop(1);
+      return -1;
+    }
+    const uint32_t L = (uint32_t)__ffsll((unsigned long long)m) - 1;
+    need = pos + L;
+    if (!has(L)) return -2;
+    const uint32_t idx = (uint32_t)__builtin_amdgcn_readlane((int)(h.offs + (c - h.first)), (int)L);
+    drop(L);
+    return (int)h.sym(idx);
+  };
+
+  uint64_t errneed = 0;
+  uint32_t errcode = 0;
+#define NEEDB(k) do { if (!has(k)) return R_NEED; } while (0)
+#define FAIL(code, needpos) do { errneed = (needpos); errcode = (code); return R_ERR; } while (0)
+
+  auto codes = [&](const Huff& lh, const Huff& dh) __attribute__((always_inline)) -> int {
+    uint64_t need;
+    for (;;) {
+      int sym = decode(lh, false, need);
+      if (sym == -2) return R_NEED;
+      if (sym == -1) FAIL(10, need);
+      if (sym < 256) {
+        if (lane == 0) ring[prod & RMASK] = (uint8_t)sym;
+        prod++;
+        if (prod - flushed >= FLUSH_AT) flush();
+        continue;
+      }
+      if (sym == 256) return R_OK;
+      sym -= 257;
+      if (sym >= 29) FAIL(11, need);                       // fixed codes 286/287
+      const uint32_t le = c_lext[sym];
+      NEEDB(le);
+      const uint32_t len = c_lbase[sym] + peek(le);
+      drop(le);
+      const int ds = decode(dh, false, need);
+      if (ds == -2) return R_NEED;
+      if (ds == -1) FAIL(12, need);
+      if (ds >= 30) FAIL(13, need);                        // fixed distance 30/31
+      const uint32_t de = c_dext[ds];
+      NEEDB(de);
+      const uint32_t dist = c_dbase[ds] + peek(de);
+      drop(de);
+      if ((uint64_t)dist > prod) FAIL(14, pos);            // invalid distance too far back
+      // copy: read the whole source first (a period of `dist` repeats for overlapping copies)
+      for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint32_t src = dist >= len ? i : i % dist;
+        uint8_t v = 0;
+        if (i < len) v = ring[(prod - dist + src) & RMASK];
+        __builtin_amdgcn_wave_barrier();
+        if (i < len) ring[(prod + i) & RMASK] = v;
+      }
+      prod += len;
+      if (prod - flushed >= FLUSH_AT) flush();
+    }
+  };
+
+  auto body = [&]() __attribute__((always_inline)) -> int {
+    // HEAD (Z/inflate.c:640-685): wrap=1, wbits=15
+    NEEDB(16);
+    const uint32_t cmf = peek(8);
+    const uint32_t flg = (peek(16) >> 8) & 0xff;
+    if (((cmf << 8) + flg) % 31) FAIL(1, pos + 16);
+    if ((cmf & 15) != 8) FAIL(2, pos + 16);
+    if ((cmf >> 4) + 8 > 15) FAIL(3, pos + 16);
+    drop(16);
+    if (flg & 0x20) { NEEDB(32); FAIL(4, pos + 32); }      // preset dictionary: not a stream end
+    int last;
+    do {
+      NEEDB(3);
+      last = (int)peek(1);
+      const uint32_t type = (peek(3) >> 1) & 3;
+      drop(3);
+      if (type == 0) {                                      // STORED
+        const uint32_t al = (uint32_t)((8 - (pos & 7)) & 7);
+        drop(al);
+        NEEDB(32);
+        const uint32_t len = peek(16);
+        const uint32_t nlen = (peek(32) >> 16) & 0xffff;
+        if (len != (~nlen & 0xffff)) FAIL(5, pos + 32);
+        drop(32);
+        // copy `len` bytes straight from the input (byte aligned now)
+        const uint64_t avail = (limit - pos) >> 3;
+        const uint64_t take = len < avail ? len : avail;
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(abase) + (pos >> 3);
+        uint64_t done = 0;
+        while (done < take) {
+          uint64_t step = take - done;
+          if (step > 4096) step = 4096;
+          const uint64_t room = RING - (prod - flushed);
+          if (step > room) { flush(); continue; }
+          for (uint64_t k = lane; k < step; k += 64) ring[(prod + k) & RMASK] = src[done + k];
+          prod += step;
+          done += step;
+          if (prod - flushed >= FLUSH_AT) flush();
+        }
+        seek(pos + 8 * take);
+        if (take < len) return R_NEED;
+      } else if (type == 1) {                               // FIXED
+        for (int i = lane; i < 288; i += 64) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
+        Huff lh, dh;
+        build(lh, lens, 288, 1);
+        for (int i = lane; i < 32; i += 64) lens[i] = 5;
+        build(dh, lens, 32, 2);
+        const int rr = codes(lh, dh);
+        if (rr != R_OK) return rr;
+      } else if (type == 2) {                               // DYNAMIC (Z/inflate.c:908-1013)
+        NEEDB(14);
+        const uint32_t nlen = peek(5) + 257;
+        const uint32_t ndist = ((peek(10) >> 5) & 31) + 1;
+        const uint32_t ncode = ((peek(14) >> 10) & 15) + 4;
+        if (nlen > 286 || ndist > 30) FAIL(6, pos + 14);
+        drop(14);
+        for (int i = lane; i < 320; i += 64) lens[i] = 0;
+        for (uint32_t i = 0; i < ncode; i++) {
+          NEEDB(3);
+          const uint32_t v = peek(3);
+          drop(3);
+          if (lane == 0) lens[c_clorder[i]] = (uint16_t)v;
+        }
+        Huff chh;
+        if (build(chh, lens, 19, 0)) FAIL(7, pos);
+        uint32_t have = 0;
+        const uint32_t total = nlen + ndist;
+        uint64_t need;
+        for (int i = lane; i < 320; i += 64) lens[i] = 0;
+        uint32_t prevlen = 0;
+        while (have < total) {
+          const int sym = decode(chh, true, need);
+          if (sym == -2) return R_NEED;
+          if (sym < 16) { if (lane == 0) lens[have] = (uint16_t)sym; prevlen = (uint32_t)sym; have++; continue; }
+          uint32_t copy, len = 0, eb;
+          if (sym == 16) eb = 2; else if (sym == 17) eb = 3; else eb = 7;
+          NEEDB(eb);
+          if (sym == 16) {
+            if (have == 0) FAIL(8, pos + eb);
+            len = prevlen;
+            copy = 3 + peek(2);
+          } else if (sym == 17) {
+            copy = 3 + peek(3);
+          } else {
+            copy = 11 + peek(7);
+          }
+          drop(eb);
+          if (have + copy > total) FAIL(8, pos);
+          for (uint32_t k = lane; k < copy; k += 64) lens[have + k] = (uint16_t)len;
+          prevlen = len;
+          have += copy;
+        }
+        if (iuni(lens[256]) == 0) FAIL(9, pos);
+        Huff lh, dh;
+        if (build(lh, lens, (int)nlen, 1)) FAIL(9, pos);
+        if (build(dh, lens + nlen, (int)ndist, 2)) FAIL(9, pos);
+        const int rr = codes(lh, dh);
+        if (rr != R_OK) return rr;
+      } else {
+        FAIL(15, pos);                                      // invalid block type
+      }
+    } while (!last);
+    // CHECK (Z/inflate.c:1174-1195)
+    const uint32_t al = (uint32_t)((8 - (pos & 7)) & 7);
+    drop(al);
+    NEEDB(32);
+    const uint32_t t = peek(32);
+    const uint32_t want = ((t & 0xff) << 24) | ((t & 0xff00) << 8) | ((t >> 8) & 0xff00) | (t >> 24);
+    drop(32);
+    flush();
+    const uint32_t adler = (ad_b << 16) | ad_a;
+    if (want != adler) FAIL(16, pos);
+    return R_OK;
+  };
+#undef NEEDB
+#undef FAIL
+
+  seek(8 * skip);
+  const int rr = body();
+  InfRes o;
+  o.produced = prod;
+  o.err = errcode;
+  if (rr == R_OK && !overflow) {
+    o.status = INF_END;
+    o.consumed = (pos - skip_bits) >> 3;
   } else if (rr == R_NEED) {
-    out.status = INF_NEED;
-    out.consumed = job.in_len;
+    o.status = INF_NEED;
+    o.consumed = job.in_len;
   } else {
-    out.status = INF_ERROR;
-    if (c.o.overflow) out.err = 17;
-    uint64_t need = c.errneed > c.r.skip_bits ? c.errneed - c.r.skip_bits : 0;
-    uint64_t cons = (need + 7) >> 3;
-    out.consumed = cons > job.in_len ? job.in_len : cons;
+    o.status = INF_ERROR;
+    if (overflow) o.err = 17;
+    const uint64_t need = errneed > skip_bits ? errneed - skip_bits : 0;
+    const uint64_t cons = (need + 7) >> 3;
+    o.consumed = cons > job.in_len ? job.in_len : cons;
   }
-  if (lane == 0) res[j] = out;
+  if (lane == 0) res[j] = o;
 }
 
 }  // namespace atz
