@@ -28,6 +28,11 @@
 #include <hip/hip_runtime.h>
 #include "atz_device.h"
 
+// LDS-typed references make the non-inlined block-flush helpers use ds_* instructions (a generic
+// reference would compile to flat accesses with longer latency and vmcnt coupling).
+#define LDS __attribute__((address_space(3)))
+#define CONSTANT __attribute__((address_space(4)))
+
 namespace atz {
 
 // ---------------------------------------------------------------------------------------------
@@ -203,16 +208,34 @@ static constexpr uint32_t LOOKMIN = 262;
 static constexpr uint32_t BITMAP_BITS = 65536;  // fast-mode insertion ring (positions mod 65536)
 static constexpr uint32_t HOLE_SLOTS = HOLE_SLOTS_M;   // fast mode: latest skipped position per hash slot
 
-struct TreeWork {      // one tree under construction (zlib ct_data split into arrays)
-  uint16_t freq[HEAPN];
+struct TreeWork {      // one tree under construction (zlib's ct_data / heap / depth in LDS)
+  uint32_t heap[HEAPN + 1];  // packed keys (freq:16 | depth:5 | node:10) in [1, heap_len]; node ids from heap_max
   uint16_t dad[HEAPN];
-  uint16_t heap[HEAPN];
-  uint8_t len[HEAPN];
-  uint8_t depth[HEAPN];
+  uint16_t anc[2][HEAPN];    // pointer-jumping scratch (depth computation)
+  uint8_t dep[2][HEAPN];
+  uint16_t freq[NLC];        // leaf frequencies (forced leaves set to 1)
+  uint8_t len[NLC];          // leaf code lengths
   uint16_t bl_count[16];
 };
 
+struct BitOut {
+  uint8_t* out;
+  uint64_t cap;
+  uint64_t pos;      // bytes written
+  uint64_t bb;       // pending bits (< 8 after every flush)
+  uint32_t bc;
+  // comparison against the original
+  const uint8_t* orig;
+  uint64_t clen;     // C_s
+  uint64_t shortcut; // shortcut length, 0 if the shortcut does not apply
+  uint64_t eq_all;   // equal bytes at positions < min(pos, C_s)
+  uint64_t eq_sc;    // equal bytes at positions < min(pos, shortcut)
+  int overflow;
+  uint64_t cyc_tree, cyc_emit, blocks;   // diagnostics (shader clock)
+};
+
 struct TrialShared {
+  BitOut b;              // output / compare state of the trial (in LDS: the flush helpers take it by LDS reference)
   uint32_t lfreq[NLC];
   uint32_t dfreq[NDC];
   uint16_t lcode[NLC]; uint8_t llen[NLC + 2];
@@ -244,22 +267,6 @@ struct SweepArgs {
   uint32_t ntrials;
 };
 
-struct BitOut {
-  uint8_t* out;
-  uint64_t cap;
-  uint64_t pos;      // bytes written
-  uint64_t bb;       // pending bits (< 8 after every flush)
-  uint32_t bc;
-  // comparison against the original
-  const uint8_t* orig;
-  uint64_t clen;     // C_s
-  uint64_t shortcut; // shortcut length, 0 if the shortcut does not apply
-  uint64_t eq_all;   // equal bytes at positions < min(pos, C_s)
-  uint64_t eq_sc;    // equal bytes at positions < min(pos, shortcut)
-  int overflow;
-  uint64_t cyc_tree, cyc_emit, blocks;   // diagnostics (shader clock)
-};
-
 __device__ inline uint64_t wsum64(uint64_t v) {
   for (int d = 32; d >= 1; d >>= 1) {
     uint32_t lo = __shfl_xor((uint32_t)v, d, 64), hi = __shfl_xor((uint32_t)(v >> 32), d, 64);
@@ -270,7 +277,7 @@ __device__ inline uint64_t wsum64(uint64_t v) {
 
 // write `nb` bytes (lane k supplies byte k via getter semantics: bytes[] in LDS words) -- used by
 // both scalar and lane-parallel emitters.  Compares against the original on the fly.
-__device__ inline void emit_bytes_from_stage(BitOut& b, const uint32_t* stage, uint32_t nb, int lane) {
+__device__ inline void emit_bytes_from_stage(LDS BitOut& b, const LDS uint32_t* stage, uint32_t nb, int lane) {
   uint64_t eqa = 0, eqs = 0;
   for (uint32_t k = lane; k < nb; k += 64) {
     uint8_t x = (uint8_t)(stage[k >> 2] >> (8 * (k & 3)));
@@ -290,7 +297,7 @@ __device__ inline void emit_bytes_from_stage(BitOut& b, const uint32_t* stage, u
 
 // scalar emission (block headers, tree descriptions): bits accumulate in bb; whole bytes go out in
 // groups through the staging words.
-__device__ inline void put_bits(BitOut& b, uint32_t* stage, uint32_t v, uint32_t n, int lane) {
+__device__ inline void put_bits(LDS BitOut& b, LDS uint32_t* stage, uint32_t v, uint32_t n, int lane) {
   b.bb |= (uint64_t)v << b.bc;
   b.bc += n;
   if (b.bc >= 32) {
@@ -300,7 +307,7 @@ __device__ inline void put_bits(BitOut& b, uint32_t* stage, uint32_t v, uint32_t
     b.bc -= 32;
   }
 }
-__device__ inline void flush_bits_bytes(BitOut& b, uint32_t* stage, int lane) {  // whole bytes only
+__device__ inline void flush_bits_bytes(LDS BitOut& b, LDS uint32_t* stage, int lane) {  // whole bytes only
   uint32_t nb = b.bc >> 3;
   if (!nb) return;
   if (lane == 0) { stage[0] = (uint32_t)b.bb; stage[1] = (uint32_t)(b.bb >> 32); }
@@ -308,7 +315,7 @@ __device__ inline void flush_bits_bytes(BitOut& b, uint32_t* stage, int lane) { 
   b.bb = nb >= 8 ? 0 : (b.bb >> (8 * nb));
   b.bc -= 8 * nb;
 }
-__device__ inline void windup(BitOut& b, uint32_t* stage, int lane) {  // bi_windup
+__device__ inline void windup(LDS BitOut& b, LDS uint32_t* stage, int lane) {  // bi_windup
   flush_bits_bytes(b, stage, lane);
   if (b.bc) {
     if (lane == 0) stage[0] = (uint32_t)b.bb;
@@ -317,114 +324,191 @@ __device__ inline void windup(BitOut& b, uint32_t* stage, int lane) {  // bi_win
   }
 }
 
-// ---- Huffman tree construction, Z/trees.c:453-699 (wave-uniform scalar code) ----
-__device__ inline bool t_smaller(const TreeWork& w, int n, int m) {
-  return w.freq[n] < w.freq[m] || (w.freq[n] == w.freq[m] && w.depth[n] <= w.depth[m]);
-}
-__device__ void pq_down(TreeWork& w, int heap_len, int k) {
-  int v = w.heap[k];
+// ---- Huffman tree construction, Z/trees.c:453-699 ----
+// zlib's heap algorithm is kept step for step (its tie-breaks decide the code lengths).  Heap
+// entries are packed keys freq:16 | depth:5 | node:10, so zlib's smaller() (freq, then depth <=)
+// is one compare of key >> 10 and a sift-down level is one ds_read2 of the sibling pair.
+__device__ __forceinline__ uint32_t tkey(uint32_t f, uint32_t d, uint32_t n) { return (f << 15) | (d << 10) | n; }
+
+// pqdownheap (Z/trees.c:453-476)
+__device__ __forceinline__ void pq_down(LDS uint32_t* heap, int heap_len, int k) {
+  const uint32_t v = uni(heap[k]);
+  const uint32_t vk = v >> 10;
   int j = k << 1;
   while (j <= heap_len) {
-    if (j < heap_len && t_smaller(w, w.heap[j + 1], w.heap[j])) j++;
-    if (t_smaller(w, v, w.heap[j])) break;
-    w.heap[k] = w.heap[j];
+    uint32_t hj = uni(heap[j]);
+    if (j < heap_len) {
+      const uint32_t hj1 = uni(heap[j + 1]);
+      if ((hj1 >> 10) <= (hj >> 10)) { j++; hj = hj1; }
+    }
+    if (vk <= (hj >> 10)) break;
+    heap[k] = hj;
     k = j;
     j <<= 1;
   }
-  w.heap[k] = (uint16_t)v;
+  heap[k] = v;
 }
 
-// Builds a tree from w.freq[0..elems).  Leaves' lengths land in w.len; returns max_code.
-// opt/stat accumulate as in gen_bitlen.  stlen: static lengths (or nullptr).
-__device__ int build_tree(TreeWork& w, int elems, int max_length, const uint8_t* xbits, int xbase,
-                          const uint8_t* stlen, uint64_t& opt_len, uint64_t& static_len) {
-  int heap_len = 0, heap_max = HEAPN, max_code = -1, node;
-  for (int n = 0; n < elems; n++) {
-    if (w.freq[n] != 0) { w.heap[++heap_len] = (uint16_t)n; max_code = n; w.depth[n] = 0; }
-    else w.len[n] = 0;
+// build_tree + gen_bitlen (Z/trees.c:488-565, 617-699) from w.freq[0..elems).  Leaves' lengths land
+// in w.len, bl_count in w.bl_count; opt_len / static_len accumulate as in zlib.  Returns max_code.
+__device__ __noinline__ int build_tree(LDS TreeWork& w, int elems, int max_length, const uint8_t* xbits, int xbase,
+                                       const uint8_t* stlen, uint64_t& opt_len, uint64_t& static_len, int lane) {
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  LDS uint32_t* const heap = w.heap;
+  // leaves enter heap[1..] in increasing symbol order (Z/trees.c:631-638)
+  int heap_len = 0, max_code = -1;
+  for (int g = 0; g < elems; g += 64) {
+    const int n = g + lane;
+    const uint32_t f = n < elems ? w.freq[n] : 0u;
+    const uint64_t m = __ballot(f != 0);
+    if (f) heap[heap_len + 1 + __popcll(m & lt)] = tkey(f, 0, (uint32_t)n);
+    else if (n < elems) w.len[n] = 0;
+    if (m) max_code = g + 63 - __clzll((long long)m);
+    heap_len += __popcll(m);
   }
+  // force at least two codes (Z/trees.c:645-653)
   while (heap_len < 2) {
-    node = (max_code < 2 ? ++max_code : 0);
-    w.heap[++heap_len] = (uint16_t)node;
-    w.freq[node] = 1;
-    w.depth[node] = 0;
+    const int node = max_code < 2 ? ++max_code : 0;
+    ++heap_len;
+    if (lane == 0) { heap[heap_len] = tkey(1, 0, (uint32_t)node); w.freq[node] = 1; }
     opt_len--;
     if (stlen) static_len -= stlen[node];
   }
-  for (int n = heap_len / 2; n >= 1; n--) pq_down(w, heap_len, n);
-  node = elems;
+  for (int n = heap_len / 2; n >= 1; n--) pq_down(heap, heap_len, n);
+  // combine the two least frequent nodes until one is left (Z/trees.c:663-690)
+  int heap_max = HEAPN;
+  uint32_t node = (uint32_t)elems;
   do {
-    int n = w.heap[1];
-    w.heap[1] = w.heap[heap_len--];
-    pq_down(w, heap_len, 1);
-    int m = w.heap[1];
-    w.heap[--heap_max] = (uint16_t)n;
-    w.heap[--heap_max] = (uint16_t)m;
-    w.freq[node] = (uint16_t)(w.freq[n] + w.freq[m]);
-    w.depth[node] = (uint8_t)((w.depth[n] >= w.depth[m] ? w.depth[n] : w.depth[m]) + 1);
-    w.dad[n] = w.dad[m] = (uint16_t)node;
-    w.heap[1] = (uint16_t)node++;
-    pq_down(w, heap_len, 1);
+    const uint32_t kn = uni(heap[1]);
+    heap[1] = uni(heap[heap_len]);
+    heap_len--;
+    pq_down(heap, heap_len, 1);
+    const uint32_t km = uni(heap[1]);
+    const uint32_t dn = (kn >> 10) & 31u, dm = (km >> 10) & 31u;
+    if (lane == 0) {
+      heap[--heap_max] = kn & 1023u;
+      heap[--heap_max] = km & 1023u;
+      w.dad[kn & 1023u] = (uint16_t)node;
+      w.dad[km & 1023u] = (uint16_t)node;
+    } else {
+      heap_max -= 2;
+    }
+    heap[1] = tkey((kn >> 15) + (km >> 15), (dn >= dm ? dn : dm) + 1u, node);
+    node++;
+    pq_down(heap, heap_len, 1);
   } while (heap_len >= 2);
-  w.heap[--heap_max] = w.heap[1];
-  // gen_bitlen
-  for (int bits = 0; bits <= 15; bits++) w.bl_count[bits] = 0;
-  w.len[w.heap[heap_max]] = 0;
-  int overflow = 0, h;
-  for (h = heap_max + 1; h < HEAPN; h++) {
-    int n = w.heap[h];
-    int bits = w.len[w.dad[n]] + 1;
-    if (bits > max_length) { bits = max_length; overflow++; }
-    w.len[n] = (uint8_t)bits;
-    if (n > max_code) continue;
-    w.bl_count[bits]++;
-    int xb = (xbits && n >= xbase) ? xbits[n - xbase] : 0;
-    opt_len += (uint64_t)w.freq[n] * (uint64_t)(bits + xb);
-    if (stlen) static_len += (uint64_t)w.freq[n] * (uint64_t)(stlen[n] + xb);
+  const uint32_t root = uni(heap[1]) & 1023u;
+  --heap_max;
+  if (lane == 0) heap[heap_max] = root;
+  // gen_bitlen: every node's depth by pointer jumping over dad[] (lane-parallel, depth <= 31 so
+  // five rounds), bits = min(depth, max_length); zlib counts the nodes it had to cap (overflow).
+  const int nn = (int)node;   // node ids 0..nn-1 (leaves not in the tree are never read)
+  for (int i = lane; i < nn; i += 64) {
+    const bool in_tree = i >= elems || (i <= max_code && w.freq[i] != 0);
+    const bool r = (uint32_t)i == root || !in_tree;   // leaves outside the tree: never followed
+    w.anc[0][i] = r ? (uint16_t)root : w.dad[i];
+    w.dep[0][i] = r ? 0 : 1;
   }
-  if (overflow) {
-    int bits;
+  int cur = 0;
+  for (int round = 0; round < 5; round++) {
+    for (int i = lane; i < nn; i += 64) {
+      const uint32_t a = w.anc[cur][i];
+      w.dep[cur ^ 1][i] = (uint8_t)(w.dep[cur][i] + w.dep[cur][a]);
+      w.anc[cur ^ 1][i] = w.anc[cur][a];
+    }
+    cur ^= 1;
+  }
+  uint32_t blc = 0;   // lane b: bl_count[b]
+  int overflow = 0;
+  for (int g = 0; g < nn; g += 64) {
+    const int i = g + lane;
+    bool in_tree = false;
+    uint32_t bits = 0;
+    if (i < nn) {
+      in_tree = i >= elems || (i <= max_code && w.freq[i] != 0);   // internal node or leaf in the heap
+      bits = w.dep[cur][i];
+    }
+    const bool capped = in_tree && (uint32_t)i != root && bits > (uint32_t)max_length;
+    overflow += __popcll(__ballot(capped));
+    if (bits > (uint32_t)max_length) bits = (uint32_t)max_length;
+    const bool leaf = in_tree && i <= max_code;
+    if (leaf) w.len[i] = (uint8_t)bits;
+    for (int b = 1; b <= 15; b++) {
+      const uint32_t c = (uint32_t)__popcll(__ballot(leaf && bits == (uint32_t)b));
+      if (lane == b) blc += c;
+    }
+  }
+  if (overflow) {   // Z/trees.c:531-564 (rare): sequential, as zlib
+    auto bl = [&](int b) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)blc, b); };
+    auto blset = [&](int b, uint32_t v) { blc = lane == b ? v : blc; };
     do {
-      bits = max_length - 1;
-      while (w.bl_count[bits] == 0) bits--;
-      w.bl_count[bits]--;
-      w.bl_count[bits + 1] += 2;
-      w.bl_count[max_length]--;
+      int bits = max_length - 1;
+      while (bl(bits) == 0) bits--;
+      blset(bits, bl(bits) - 1);
+      blset(bits + 1, bl(bits + 1) + 2);
+      blset(max_length, bl(max_length) - 1);
       overflow -= 2;
     } while (overflow > 0);
-    for (bits = max_length; bits != 0; bits--) {
-      int n = w.bl_count[bits];
-      while (n != 0) {
-        int m = w.heap[--h];
-        if (m > max_code) continue;
-        if (w.len[m] != bits) {
-          opt_len += (uint64_t)((int64_t)bits - (int64_t)w.len[m]) * (uint64_t)w.freq[m];
-          w.len[m] = (uint8_t)bits;
-        }
-        n--;
+    int h = HEAPN;
+    for (int bits = max_length; bits != 0; bits--) {
+      uint32_t cnt = bl(bits);
+      while (cnt != 0) {
+        const uint32_t m = uni(heap[--h]);
+        if ((int)m > max_code) continue;
+        if (lane == 0) w.len[m] = (uint8_t)bits;
+        cnt--;
       }
     }
   }
+  if (lane < 16) w.bl_count[lane] = (uint16_t)blc;
+  // opt_len / static_len over the final lengths (= zlib's running sums + fix-up terms)
+  uint64_t o = 0, st = 0;
+  for (int n = lane; n < elems && n <= max_code; n += 64) {
+    const uint32_t f = w.freq[n];
+    if (f) {
+      const uint32_t l = w.len[n];
+      const uint32_t xb = (xbits && n >= xbase) ? xbits[n - xbase] : 0u;
+      o += (uint64_t)f * (l + xb);
+      if (stlen) st += (uint64_t)f * (stlen[n] + xb);
+    }
+  }
+  opt_len += wsum64(o);
+  if (stlen) static_len += wsum64(st);
   return max_code;
 }
 
-// gen_codes (Z/trees.c:575-607) from w.len/w.bl_count into codes/lens
-__device__ void gen_codes(const TreeWork& w, int max_code, uint16_t* codes, uint8_t* lens) {
-  uint32_t next[16];
-  uint32_t code = 0;
-  next[0] = 0;
-  for (int bits = 1; bits <= 15; bits++) { code = (code + w.bl_count[bits - 1]) << 1; next[bits] = code; }
-  for (int n = 0; n <= max_code; n++) {
-    int l = w.len[n];
-    lens[n] = (uint8_t)l;
-    if (!l) continue;
-    codes[n] = (uint16_t)(__builtin_bitreverse32(next[l]++) >> (32 - l));
+// gen_codes (Z/trees.c:575-607), lane-parallel: the codes of one length are consecutive in
+// symbol order, so a ballot per length ranks the symbols.
+__device__ __noinline__ void gen_codes(const LDS TreeWork& w, int max_code, LDS uint16_t* codes, LDS uint8_t* lens,
+                                       int lane) {
+  uint32_t nc = 0;   // lane b: next_code[b]
+  {
+    uint32_t code = 0;
+    for (int bits = 1; bits <= 15; bits++) {
+      code = (code + w.bl_count[bits - 1]) << 1;
+      if (lane == bits) nc = code;
+    }
+  }
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int g = 0; g <= max_code; g += 64) {
+    const int n = g + lane;
+    const uint32_t l = n <= max_code ? w.len[n] : 0u;
+    if (n <= max_code) lens[n] = (uint8_t)l;
+    uint32_t mine = 0;
+    for (int b = 1; b <= 15; b++) {
+      const uint64_t m = __ballot(l == (uint32_t)b);
+      if (!m) continue;
+      const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)nc, b);
+      if (l == (uint32_t)b) mine = base + (uint32_t)__popcll(m & lt);
+      if (lane == b) nc += (uint32_t)__popcll(m);
+    }
+    if (n <= max_code && l) codes[n] = (uint16_t)(__builtin_bitreverse32(mine) >> (32 - l));
   }
 }
 
-__device__ inline int tl(const uint8_t* ln, int n, int guard) { return n == guard ? 0xffff : ln[n]; }
+__device__ inline int tl(const LDS uint8_t* ln, int n, int guard) { return n == guard ? 0xffff : ln[n]; }
 
-__device__ void scan_tree(uint32_t* bfreq, const uint8_t* ln, int max_code) {  // Z/trees.c:705-748
+__device__ void scan_tree(LDS uint32_t* bfreq, const LDS uint8_t* ln, int max_code) {  // Z/trees.c:705-748
   int prevlen = -1, curlen, nextlen = ln[0], count = 0, max_count = 7, min_count = 4;
   int guard = max_code + 1;
   if (nextlen == 0) { max_count = 138; min_count = 3; }
@@ -442,7 +526,7 @@ __device__ void scan_tree(uint32_t* bfreq, const uint8_t* ln, int max_code) {  /
   }
 }
 
-__device__ void send_tree(BitOut& b, TrialShared& s, const uint8_t* ln, int max_code, int lane) {
+__device__ void send_tree(LDS BitOut& b, LDS TrialShared& s, const LDS uint8_t* ln, int max_code, int lane) {
   int prevlen = -1, curlen, nextlen = ln[0], count = 0, max_count = 7, min_count = 4;
   int guard = max_code + 1;
   if (nextlen == 0) { max_count = 138; min_count = 3; }
@@ -472,8 +556,9 @@ __device__ void send_tree(BitOut& b, TrialShared& s, const uint8_t* ln, int max_
 __device__ inline uint32_t d_code(uint32_t d) { return d < 256 ? c_t.dcode[d] : c_t.dcode[256 + (d >> 7)]; }
 
 // Lane-parallel compress_block (Z/trees.c:1060-1105): 64 symbols per step.
-__device__ void compress_block(BitOut& b, TrialShared& s, const uint32_t* syms, uint32_t nsym,
-                               const uint16_t* lc, const uint8_t* ll, const uint16_t* dc, const uint8_t* dl,
+template <typename C16, typename C8>
+__device__ void compress_block(LDS BitOut& b, LDS TrialShared& s, const uint32_t* syms, uint32_t nsym,
+                               C16 lc, C8 ll, C16 dc, C8 dl,
                                int lane) {
   // the symbols were stored by lane 0 during the parse: order those HBM stores before the reads
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
@@ -516,9 +601,9 @@ __device__ void compress_block(BitOut& b, TrialShared& s, const uint32_t* syms, 
       uint32_t wi = off >> 5, sh = off & 31;
       uint64_t lo = v << sh;                       // bits 0..63 of the shifted value
       uint32_t hi = sh ? (uint32_t)(v >> (64 - sh)) : 0;
-      atomicOr(&s.stage[wi], (uint32_t)lo);
-      if ((uint32_t)(lo >> 32)) atomicOr(&s.stage[wi + 1], (uint32_t)(lo >> 32));
-      if (hi) atomicOr(&s.stage[wi + 2], hi);
+      __atomic_fetch_or(&s.stage[wi], (uint32_t)lo, __ATOMIC_RELAXED);
+      if ((uint32_t)(lo >> 32)) __atomic_fetch_or(&s.stage[wi + 1], (uint32_t)(lo >> 32), __ATOMIC_RELAXED);
+      if (hi) __atomic_fetch_or(&s.stage[wi + 2], hi, __ATOMIC_RELAXED);
     }
     uint32_t all = b.bc + total;
     uint32_t full = all >> 3;
@@ -666,7 +751,7 @@ __device__ __forceinline__ uint32_t longest_match(Lz& z, const uint8_t* in, cons
 // _tr_flush_block (Z/trees.c:907-1004) + FLUSH_BLOCK_ONLY bookkeeping
 // The parse state is passed by value so that it never leaves registers (a reference to it here
 // would put the whole parse state in scratch memory).  Returns the overlay-hazard bit.
-__device__ __noinline__ uint32_t flush_block(TrialShared& s, BitOut& b, const uint32_t* syms, const uint8_t* in,
+__device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, const uint32_t* syms, const uint8_t* in,
                                              int64_t block_start, uint64_t p, uint64_t S, uint32_t last_lit,
                                              uint32_t level, uint32_t lbs, int last, int lane) {
   uint32_t hazard = 0;
@@ -678,20 +763,20 @@ __device__ __noinline__ uint32_t flush_block(TrialShared& s, BitOut& b, const ui
   if (level > 0) {
     // literal/length tree
     for (int i = lane; i < NLC; i += 64) s.w.freq[i] = (uint16_t)s.lfreq[i];
-    lmax = build_tree(s.w, NLC, 15, c_xlb, 257, c_t.st_llen, opt_len, static_len);
-    gen_codes(s.w, lmax, s.lcode, s.llen);
+    lmax = build_tree(s.w, NLC, 15, c_xlb, 257, c_t.st_llen, opt_len, static_len, lane);
+    gen_codes(s.w, lmax, s.lcode, s.llen, lane);
     for (int i = lmax + 1 + lane; i < NLC + 2; i += 64) s.llen[i] = 0;
     // distance tree
     for (int i = lane; i < NDC; i += 64) s.w.freq[i] = (uint16_t)s.dfreq[i];
-    dmax = build_tree(s.w, NDC, 15, c_xdb, 0, c_t.st_dlen, opt_len, static_len);
-    gen_codes(s.w, dmax, s.dcode, s.dlen);
+    dmax = build_tree(s.w, NDC, 15, c_xdb, 0, c_t.st_dlen, opt_len, static_len, lane);
+    gen_codes(s.w, dmax, s.dcode, s.dlen, lane);
     for (int i = dmax + 1 + lane; i < NDC + 2; i += 64) s.dlen[i] = 0;
     // bit length tree
     for (int i = lane; i < NBLC; i += 64) s.bfreq[i] = 0;
     if (lane == 0) { scan_tree(s.bfreq, s.llen, lmax); scan_tree(s.bfreq, s.dlen, dmax); }
     for (int i = lane; i < NBLC; i += 64) s.w.freq[i] = (uint16_t)s.bfreq[i];
-    int bmax = build_tree(s.w, NBLC, 7, c_xblb, 0, nullptr, opt_len, static_len);
-    gen_codes(s.w, bmax, s.bcode, s.blen);
+    int bmax = build_tree(s.w, NBLC, 7, c_xblb, 0, nullptr, opt_len, static_len, lane);
+    gen_codes(s.w, bmax, s.bcode, s.blen, lane);
     for (int i = bmax + 1 + lane; i < NBLC + 2; i += 64) s.blen[i] = 0;
     for (max_blindex = NBLC - 1; max_blindex >= 3; max_blindex--)
       if (s.blen[c_blorder[max_blindex]] != 0) break;
@@ -727,7 +812,8 @@ __device__ __noinline__ uint32_t flush_block(TrialShared& s, BitOut& b, const ui
     }
   } else if (static_lenb == opt_lenb) {
     put_bits(b, s.stage, (1u << 1) + (uint32_t)last, 3, lane);
-    compress_block(b, s, syms, last_lit, c_t.st_lcode, c_t.st_llen, c_t.st_dcode, c_t.st_dlen, lane);
+    compress_block(b, s, syms, last_lit, (const CONSTANT uint16_t*)c_t.st_lcode, (const CONSTANT uint8_t*)c_t.st_llen,
+                   (const CONSTANT uint16_t*)c_t.st_dcode, (const CONSTANT uint8_t*)c_t.st_dlen, lane);
   } else {
     int lcodes = lmax + 1, dcodes = dmax + 1, blcodes = max_blindex + 1;
     put_bits(b, s.stage, (2u << 1) + (uint32_t)last, 3, lane);
@@ -738,7 +824,8 @@ __device__ __noinline__ uint32_t flush_block(TrialShared& s, BitOut& b, const ui
     send_tree(b, s, s.llen, lcodes - 1, lane);
     send_tree(b, s, s.dlen, dcodes - 1, lane);
     flush_bits_bytes(b, s.stage, lane);
-    compress_block(b, s, syms, last_lit, s.lcode, s.llen, s.dcode, s.dlen, lane);
+    compress_block(b, s, syms, last_lit, (const LDS uint16_t*)s.lcode, (const LDS uint8_t*)s.llen,
+                   (const LDS uint16_t*)s.dcode, (const LDS uint8_t*)s.dlen, lane);
   }
   // 1.2.8 pending_buf/d_buf overlay condition (conservative, cf. oracle/ora_deflate.c)
   if (b.pos - blk_start_bytes > (uint64_t)lbs + 2ull * last_lit && last_lit) hazard = 1;
@@ -752,7 +839,7 @@ __device__ __noinline__ uint32_t flush_block(TrialShared& s, BitOut& b, const ui
 }
 
 // Early-exit test after output progress: returns TR_* state to stop with, or ~0u to continue.
-__device__ inline uint32_t early_exit(const BitOut& b, const SweepOpts& o, uint64_t best_ident, bool full_needed) {
+__device__ inline uint32_t early_exit(const LDS BitOut& b, const SweepOpts& o, uint64_t best_ident, bool full_needed) {
   if (b.overflow) return TR_OVERFLOW;
   if (full_needed) return ~0u;
   if (b.shortcut) {
@@ -769,7 +856,7 @@ __device__ inline uint32_t early_exit(const BitOut& b, const SweepOpts& o, uint6
 
 template <int KIND, typename SH>
 __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
-  TrialShared& s = shm.t;
+  LDS TrialShared& s = *(LDS TrialShared*)&shm.t;
   const uint32_t t = blockIdx.x;
   const Trial tr = A.trials[t];
   const StreamDev sd = A.streams[tr.stream];
@@ -785,7 +872,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   z.n = sd.infl_len; z.p = 0; z.lookahead = 0; z.S = 0; z.block_start = 0;
   z.match_start = 0; z.prev_match = 0; z.match_length = 2; z.prev_length = 2; z.match_available = 0;
   z.last_lit = 0; z.ins_cleared = 0; z.nsym = 0;
-  BitOut b;
+  LDS BitOut& b = s.b;
   b.out = A.out + tr.out_off; b.cap = tr.out_cap; b.pos = 0; b.bb = 0; b.bc = 0;
   b.orig = A.file + sd.orig_off; b.clen = sd.comp_len;
   b.shortcut = sd.comp_len > A.o.shortcut_len ? A.o.shortcut_len : 0;
