@@ -235,7 +235,7 @@ struct atz_ctx {
   hipStream_t st = nullptr;
   DBuf d_file, d_pos, d_cnt, d_jobs, d_res, d_virt, d_infl, d_chains, d_heads, d_streams, d_trials,
       d_tres, d_out, d_syms, d_adler, d_meta, d_segs, d_atz, d_diffjobs, d_diffpos, d_diffval, d_diffcnt,
-      d_cjobs, d_tmp, d_R, d_mjobs;
+      d_cjobs, d_tmp, d_R, d_mjobs, d_ins;
   // last scan
   std::vector<Rec> recs;
   std::vector<uint64_t> infl_off;   // per record offset in d_infl
@@ -681,6 +681,8 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
       if (m.p1 > m.p0) mj.push_back(m);
     }
   if (int r = c->d_R.reserve(r_tot * sizeof(uint2) + 4096)) return r;
+  for (size_t q = 0; q < tr[1].size(); q++) tr[1][q].ins_off = 2048ull * q;
+  if (int r = c->d_ins.reserve(2048ull * 4 * tr[1].size() + 4096)) return r;
   if (int r = launch_match(c, mj)) return r;
   const size_t tot_trials = tr[0].size() + tr[1].size() + tr[2].size();
   if (int r = c->d_trials.reserve(2 * tot_trials * sizeof(Trial) + 64)) return r;
@@ -690,6 +692,7 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
     SweepArgs A;
     A.file = d_cmp; A.infl = c->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint16_t>();
     A.R = c->d_R.as<uint2>();
+    A.ins = c->d_ins.as<uint32_t>();
     A.streams = c->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
     A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
     A.adler = c->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)cnt;

@@ -36,6 +36,7 @@ struct Trial {
   uint64_t chain_off;   // chain-link table of (stream, memlevel) (uint16 units); unused for level 0
   uint64_t r_off;       // match table of this trial (uint2 units, indexed by absolute position)
   uint64_t x_lim;       // match-table entries exist for positions < x_lim (else the trial stops: TR_NEED_R)
+  uint64_t ins_off;     // fast levels: insertion ring (uint32 words, 2048 per trial)
 };
 
 // ---- match tables (k_match) ----------------------------------------------------------------

@@ -33,6 +33,16 @@
 #define LDS __attribute__((address_space(3)))
 #define CONSTANT __attribute__((address_space(4)))
 
+// Per-step shader-clock counters in the parse loop (diagnostics; s_memtime also forces lgkmcnt waits).
+#ifndef ATZ_STEP_CLOCKS
+#define ATZ_STEP_CLOCKS 0
+#endif
+#if ATZ_STEP_CLOCKS
+#define STEP_CLOCK() clock64()
+#else
+#define STEP_CLOCK() 0ull
+#endif
+
 namespace atz {
 
 // ---------------------------------------------------------------------------------------------
@@ -142,7 +152,7 @@ __global__ __launch_bounds__(64) void k_chains(const uint8_t* __restrict__ infl,
 // (NIL after the slide), which the parse checks.  nice_match is clamped to the lookahead, i.e.
 // to n - p near the end; bytes beyond the input can only extend candidates that already reach
 // n - p, which break at nice_match first.
-static constexpr uint32_t HOLE_SLOTS_M = 4096;   // == HOLE_SLOTS (fast-level hash slots)
+static constexpr uint32_t HOLE_SLOTS_M = 2048;   // == HOLE_SLOTS (fast-level hash slots)
 
 __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl, const uint16_t* __restrict__ chains,
                                               uint2* __restrict__ R, const MatchJob* __restrict__ jobs) {
@@ -205,7 +215,7 @@ __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl,
 // k_trial
 static constexpr int NLC = 286, NDC = 30, NBLC = 19, HEAPN = 2 * NLC + 1;
 static constexpr uint32_t LOOKMIN = 262;
-static constexpr uint32_t BITMAP_BITS = 65536;  // fast-mode insertion ring (positions mod 65536)
+static constexpr uint32_t BITMAP_BITS = 65536;  // fast-mode insertion ring (positions mod 65536), in HBM/L2
 static constexpr uint32_t HOLE_SLOTS = HOLE_SLOTS_M;   // fast mode: latest skipped position per hash slot
 
 struct TreeWork {      // one tree under construction (zlib's ct_data / heap / depth in LDS)
@@ -248,7 +258,6 @@ struct TrialShared {
 
 struct TrialSharedFast {
   TrialShared t;
-  uint32_t ins[BITMAP_BITS / 32];
   uint32_t holes[HOLE_SLOTS];   // position + 1 of the latest non-inserted position with hash & (SLOTS-1)
 };
 
@@ -257,6 +266,7 @@ struct SweepArgs {
   const uint8_t* infl;          // inflated bytes
   const uint16_t* chains;       // chain links
   const uint2* R;               // match tables (k_match)
+  uint32_t* ins;                // fast levels: per-trial insertion rings (Trial::ins_off)
   const StreamDev* streams;
   const Trial* trials;
   TrialRes* res;
@@ -862,8 +872,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   const StreamDev sd = A.streams[tr.stream];
   const uint8_t* in = A.infl + sd.infl_off;
   const uint16_t* ch = KIND == 0 ? nullptr : A.chains + tr.chain_off;
-  uint32_t* ins = nullptr;
-  if constexpr (KIND == 1) ins = shm.ins;
+  uint32_t* ins = nullptr;   // fast levels: insertion ring (read only by the exact chain walk)
+  if constexpr (KIND == 1) ins = A.ins + tr.ins_off;
   const bool full_needed = tr.mode & 1;
   Lz z;
   z.level = tr.clevel; z.kind = KIND;
@@ -883,7 +893,6 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   for (int i = lane; i < NLC; i += 64) s.lfreq[i] = 0;
   for (int i = lane; i < NDC; i += 64) s.dfreq[i] = 0;
   if (lane == 0) s.lfreq[256] = 1;
-  if constexpr (KIND == 1) { for (int i = lane; i < (int)(BITMAP_BITS / 32); i += 64) ins[i] = 0; }
   uint32_t hazard = 0;
   // Block statistics live in VGPRs across lanes (lfreq[c] in lane c & 63, register c >> 6) and
   // symbols are staged one per lane, 64 per coalesced store: the scalar parse issues no LDS
@@ -987,7 +996,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         for (int i = lane; i < 32; i += 64) ins[(wbase + i) & (BITMAP_BITS / 32 - 1)] = 0;
         z.ins_cleared += 1024;
       }
-      const uint64_t cl0 = clock64();
+      const uint64_t cl0 = STEP_CLOCK();
       const uint2 e = pw.get(z.p, lane);
       if (z.lookahead >= 3) {
         if (lane == 0) { uint32_t bq = (uint32_t)(z.p & (BITMAP_BITS - 1)); atomicOr(&ins[bq >> 5], 1u << (bq & 31)); }
@@ -1000,7 +1009,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           }
         } else {
           fallbacks++;
-          const uint64_t cf0 = clock64();
+          const uint64_t cf0 = STEP_CLOCK();
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // this wave's insertion atomics are visible
           // head[] = most recent inserted same-hash position
           uint64_t q = z.p, hh = 0;
           bool hv = false;
@@ -1015,10 +1025,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
             z.match_length = uni(longest_match<1>(z, in, ch, ins, hh, lane));
             z.match_start = uni(z.match_start);
           }
-          cyc_fb += clock64() - cf0;
+          cyc_fb += STEP_CLOCK() - cf0;
         }
       }
-      cyc_lookup += clock64() - cl0;
+      cyc_lookup += STEP_CLOCK() - cl0;
       bool bflush;
       if (z.match_length >= 3) {
         const uint32_t ml = z.match_length;
@@ -1058,7 +1068,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     for (;;) {
       if (z.lookahead < LOOKMIN) { fill(z); if (z.lookahead == 0) break; }
       if (z.p >= tr.x_lim) { state = TR_NEED_R; break; }
-      const uint64_t cl0 = clock64();
+      const uint64_t cl0 = STEP_CLOCK();
       const uint2 e = pw.get(z.p, lane);
       const bool hv = z.lookahead >= 3 && (e.y & 1u) && !head_is_S();
       z.prev_length = z.match_length; z.prev_match = z.match_start;
@@ -1070,7 +1080,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         else z.match_length = z.prev_length <= z.lookahead ? z.prev_length : (uint32_t)z.lookahead;
         if (z.match_length == 3 && z.p - z.match_start > 4096) z.match_length = 2;
       }
-      cyc_lookup += clock64() - cl0;
+      cyc_lookup += STEP_CLOCK() - cl0;
       if (z.prev_length >= 3 && z.match_length <= z.prev_length) {
         bool bflush = tally_dist((uint32_t)(z.p - 1 - z.prev_match), z.prev_length - 3);
         z.lookahead -= z.prev_length - 1;
