@@ -706,16 +706,37 @@ __device__ inline uint32_t common_len(const uint8_t* in, uint64_t a, uint64_t b,
   return cap;
 }
 
+// deflate_fast insertion state: positions >= w0 live in a uniform 64-bit mask, older ones in a
+// 65536-bit ring in HBM written one whole word per 32 positions (plain stores, no atomics).  The
+// ring is read back only with wave-uniform loads, i.e. by the lane that wrote it.
+struct InsRing {
+  uint32_t* ring;
+  uint64_t w0;     // multiple of 32
+  uint64_t mask;   // bit k: position w0 + k inserted
+  __device__ __forceinline__ void set(uint64_t q) { mask |= 1ull << (q - w0); }
+  __device__ __forceinline__ void advance(uint64_t p) {   // keep p < w0 + 32
+    while (p >= w0 + 32) {
+      ring[(w0 >> 5) & (BITMAP_BITS / 32 - 1)] = (uint32_t)mask;
+      mask >>= 32;
+      w0 += 32;
+    }
+  }
+  __device__ __forceinline__ bool get(uint64_t q) const {
+    if (q >= w0) return (mask >> (q - w0)) & 1;
+    const uint32_t w = uni(ring[(q >> 5) & (BITMAP_BITS / 32 - 1)]);
+    return (w >> (q & 31)) & 1;
+  }
+};
+
 template <int KIND>
-__device__ inline bool is_inserted(const uint32_t* ins, uint64_t q) {
-  if (KIND != 1) return true;
-  uint32_t b = (uint32_t)(q & (BITMAP_BITS - 1));
-  return (ins[b >> 5] >> (b & 31)) & 1;
+__device__ __forceinline__ bool is_inserted(const InsRing* ins, uint64_t q) {
+  if constexpr (KIND != 1) return true;
+  else return ins->get(q);
 }
 
 // longest_match on the shared chains (Z/deflate.c:1148-1289).  Returns match length; sets z.match_start.
 template <int KIND>
-__device__ __forceinline__ uint32_t longest_match(Lz& z, const uint8_t* in, const uint16_t* ch, const uint32_t* ins,
+__device__ __forceinline__ uint32_t longest_match(Lz& z, const uint8_t* in, const uint16_t* ch, const InsRing* ins,
                                   uint64_t cur, int lane) {
   uint32_t chain = z.chain;
   const uint64_t p = z.p;
@@ -872,8 +893,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   const StreamDev sd = A.streams[tr.stream];
   const uint8_t* in = A.infl + sd.infl_off;
   const uint16_t* ch = KIND == 0 ? nullptr : A.chains + tr.chain_off;
-  uint32_t* ins = nullptr;   // fast levels: insertion ring (read only by the exact chain walk)
-  if constexpr (KIND == 1) ins = A.ins + tr.ins_off;
+  InsRing insr;   // fast levels: insertion state (read only by the exact chain walk)
+  insr.ring = KIND == 1 ? A.ins + tr.ins_off : nullptr;
+  insr.w0 = 0; insr.mask = 0;
+  const InsRing* ins = &insr;
   const bool full_needed = tr.mode & 1;
   Lz z;
   z.level = tr.clevel; z.kind = KIND;
@@ -938,7 +961,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     z.block_start = (int64_t)z.p;
   };
   uint32_t state = ~0u;
-  uint64_t fallbacks = 0, cyc_lookup = 0, cyc_fb = 0;
+  uint64_t fallbacks = 0, cyc_lookup = 0, cyc_fb = 0, fb_changed = 0, fsteps = 0;
   PosWin pw;
   pw.init(A.R + tr.r_off);
   // zlib header (Z/deflate.c:738-759)
@@ -990,16 +1013,12 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     for (;;) {
       if (z.lookahead < LOOKMIN) { fill(z); if (z.lookahead == 0) break; }
       if (z.p >= tr.x_lim) { state = TR_NEED_R; break; }
-      // clear the insertion ring ahead of the positions about to be inserted
-      while (z.ins_cleared < z.p + 300) {
-        uint32_t wbase = (uint32_t)((z.ins_cleared & (BITMAP_BITS - 1)) >> 5);
-        for (int i = lane; i < 32; i += 64) ins[(wbase + i) & (BITMAP_BITS / 32 - 1)] = 0;
-        z.ins_cleared += 1024;
-      }
+      insr.advance(z.p);
       const uint64_t cl0 = STEP_CLOCK();
       const uint2 e = pw.get(z.p, lane);
+      fsteps++;
       if (z.lookahead >= 3) {
-        if (lane == 0) { uint32_t bq = (uint32_t)(z.p & (BITMAP_BITS - 1)); atomicOr(&ins[bq >> 5], 1u << (bq & 31)); }
+        insr.set(z.p);
         const uint32_t hl = uni(holes[(e.y >> 1) & (HOLE_SLOTS - 1)]);
         if (hl == 0 || (uint64_t)(hl - 1) < z.p - (e.y >> 16)) {
           if ((e.y & 1u) && !head_is_S()) {
@@ -1010,7 +1029,6 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         } else {
           fallbacks++;
           const uint64_t cf0 = STEP_CLOCK();
-          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // this wave's insertion atomics are visible
           // head[] = most recent inserted same-hash position
           uint64_t q = z.p, hh = 0;
           bool hv = false;
@@ -1025,6 +1043,13 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
             z.match_length = uni(longest_match<1>(z, in, ch, ins, hh, lane));
             z.match_start = uni(z.match_start);
           }
+          {  // diagnostics: did the exact walk differ from the all-positions table entry?
+            const uint32_t rl = e.x >> 23;
+            const bool rhv = (e.y & 1u) != 0;
+            const bool same = (hv == rhv) && (!hv || ((rl > 2 ? rl : 2u) == z.match_length &&
+                               (rl <= 2 || z.p - ((e.x >> 8) & 0x7fffu) == z.match_start)));
+            fb_changed += same ? 0 : 1;
+          }
           cyc_fb += STEP_CLOCK() - cf0;
         }
       }
@@ -1035,10 +1060,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         bflush = tally_dist((uint32_t)(z.p - z.match_start), ml - 3);
         z.lookahead -= ml;
         if (ml <= z.lazy && z.lookahead >= 3) {
-          if (lane >= 1 && (uint32_t)lane < ml) {
-            uint32_t bq = (uint32_t)((z.p + lane) & (BITMAP_BITS - 1));
-            atomicOr(&ins[bq >> 5], 1u << (bq & 31));
-          }
+          for (uint32_t k = 1; k < ml; k++) insr.set(z.p + k);
         } else {
           // p+1 .. p+ml-1 are not inserted: record them per hash slot
           for (uint32_t k0 = 1; k0 < ml; k0 += 64) {
@@ -1144,8 +1166,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     r.cyc_tree = b.cyc_tree;
     r.cyc_emit = b.cyc_emit;
     r.blocks = b.blocks;
-    r.cyc_lookup = cyc_lookup;
-    r.cyc_fallback = cyc_fb;
+    r.cyc_lookup = fsteps;      // fast levels: parse steps (diagnostic)
+    r.cyc_fallback = fb_changed;  // fast levels: fallbacks whose exact walk differed from the table
     A.res[t] = r;
   }
 }
