@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl,
   const uint64_t n = jb.n, maxdist = (1u << jb.window) - 262;
   const uint32_t hbits = jb.memlevel + 7u, hmask = (1u << hbits) - 1u, hshift = (hbits + 2u) / 3u;
   for (uint64_t p = jb.p0 + threadIdx.x; p < jb.p1; p += 256) {
-    uint32_t bf = 2, df = 0, bq = 2, dq = 0, valid = 0, slot = 0;
+    uint32_t bf = 2, df = 0, bq = 2, dq = 0, valid = 0, slot = 0, budget_out = 0;
     uint64_t reach = p;
     const uint32_t s0 = in[p];
     if (p + 3 <= n) {
@@ -192,7 +192,11 @@ __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl,
               if (len >= nn) break;
             }
           }
-          if (++i == B) break;
+          if (++i == B) {   // budget spent: only here can skipped positions let deflate_fast see more nodes
+            const uint32_t dd = ch[cur];
+            budget_out = (dd && cur >= dd && cur - dd > lim) ? 1u : 0u;
+            break;
+          }
           const uint32_t dd = ch[cur];
           if (!dd || cur < dd) break;
           cur -= dd;
@@ -202,10 +206,10 @@ __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl,
     }
     // .x = len_full:9 | dist_full:15 | input byte:8
     // .y = slow: len_quarter:9 | dist_quarter:15 | 0:7 | head valid:1
-    //      fast: (p - lowest visited node):16 | 0:3 | hash slot:12 | head valid:1
+    //      fast: (p - lowest visited node):16 | 0:3 | budget spent with nodes left:1 | hash slot:11 | head valid:1
     uint2 e;
     e.x = (bf > 2 ? (bf << 23) | (df << 8) : 0u) | s0;
-    if (jb.fast) e.y = ((uint32_t)(p - reach) << 16) | (slot << 1) | valid;
+    if (jb.fast) e.y = ((uint32_t)(p - reach) << 16) | (budget_out << 12) | (slot << 1) | valid;
     else e.y = (bq > 2 ? (bq << 23) | (dq << 8) : 0u) | valid;
     r[p] = e;
   }
@@ -961,7 +965,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     z.block_start = (int64_t)z.p;
   };
   uint32_t state = ~0u;
-  uint64_t fallbacks = 0, cyc_lookup = 0, cyc_fb = 0, fb_changed = 0, fsteps = 0;
+  uint64_t fallbacks = 0, cyc_lookup = 0, cyc_fb = 0;
   PosWin pw;
   pw.init(A.R + tr.r_off);
   // zlib header (Z/deflate.c:738-759)
@@ -1016,11 +1020,23 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       insr.advance(z.p);
       const uint64_t cl0 = STEP_CLOCK();
       const uint2 e = pw.get(z.p, lane);
-      fsteps++;
       if (z.lookahead >= 3) {
         insr.set(z.p);
         const uint32_t hl = uni(holes[(e.y >> 1) & (HOLE_SLOTS - 1)]);
-        if (hl == 0 || (uint64_t)(hl - 1) < z.p - (e.y >> 16)) {
+        // The table entry is deflate_fast's exact result unless a skipped position with this hash
+        // lies in the walked range AND it can matter: skipped nodes only shrink the visited set,
+        // so a walk that ended by nice_match or by the end of the chain keeps its winner W if W
+        // itself was inserted (and with no winner the step emits a literal either way); only a
+        // walk that spent its budget with nodes left can see new nodes (bit 12).
+        bool exact = hl == 0 || (uint64_t)(hl - 1) < z.p - (e.y >> 16);
+        if (!exact && !((e.y >> 12) & 1u)) {
+          if ((e.x >> 23) <= 2) exact = true;
+          else {
+            const uint64_t wpos = z.p - ((e.x >> 8) & 0x7fffu);
+            exact = wpos > z.S && insr.get(wpos);
+          }
+        }
+        if (exact) {
           if ((e.y & 1u) && !head_is_S()) {
             const uint32_t len = e.x >> 23;
             if (len > 2) { z.match_length = len; z.match_start = z.p - ((e.x >> 8) & 0x7fffu); }
@@ -1042,13 +1058,6 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           if (hv && z.p - hh <= z.maxdist) {
             z.match_length = uni(longest_match<1>(z, in, ch, ins, hh, lane));
             z.match_start = uni(z.match_start);
-          }
-          {  // diagnostics: did the exact walk differ from the all-positions table entry?
-            const uint32_t rl = e.x >> 23;
-            const bool rhv = (e.y & 1u) != 0;
-            const bool same = (hv == rhv) && (!hv || ((rl > 2 ? rl : 2u) == z.match_length &&
-                               (rl <= 2 || z.p - ((e.x >> 8) & 0x7fffu) == z.match_start)));
-            fb_changed += same ? 0 : 1;
           }
           cyc_fb += STEP_CLOCK() - cf0;
         }
@@ -1166,8 +1175,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     r.cyc_tree = b.cyc_tree;
     r.cyc_emit = b.cyc_emit;
     r.blocks = b.blocks;
-    r.cyc_lookup = fsteps;      // fast levels: parse steps (diagnostic)
-    r.cyc_fallback = fb_changed;  // fast levels: fallbacks whose exact walk differed from the table
+    r.cyc_lookup = cyc_lookup;
+    r.cyc_fallback = cyc_fb;
     A.res[t] = r;
   }
 }
