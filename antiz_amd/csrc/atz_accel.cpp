@@ -346,8 +346,21 @@ static void chunk_bytes(const uint8_t* f, const Chunk& ch, std::vector<uint8_t>&
   v.insert(v.end(), f + ch.co + 1, f + ch.co + ch.len);
 }
 
+static bool timing_on() {
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_TIMING"); v = e && *e == '1'; }
+  return v == 1;
+}
+// ATZ_TIMING=1: host phase timings on stderr
+#define TMARK(name)                                                                        \
+  do {                                                                                     \
+    if (timing_on()) std::fprintf(stderr, "atz: %-28s %9.2f ms\n", name, ms_since(tm_));   \
+    tm_ = std::chrono::steady_clock::now();                                                \
+  } while (0)
+
 static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64_t F) {
   auto t0 = std::chrono::steady_clock::now();
+  auto tm_ = t0;
   c->recs.clear();
   const uint64_t cs = c->o.chunksize;
   if (cs < 2) return ATZ_E_REF_UB;      // main.cpp:410-415 never reaches eof with chunksize 1
@@ -385,6 +398,7 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
     kend(c);
     KCHECK("k_find_headers");
   }
+  TMARK("scan: layout+find launch");
   uint64_t npairs = 0;
   HIPCHK(hipMemcpyAsync(&npairs, c->d_cnt.p, 8, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
@@ -395,6 +409,7 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
     HIPCHK(hipMemcpy(pairs.data(), c->d_pos.p, npairs * 8, hipMemcpyDeviceToHost));
     std::sort(pairs.begin(), pairs.end());
   }
+  TMARK("scan: pairs d2h+sort");
   // ---- candidates per chunk: i >= 1 are file pairs, i == 0 uses buffer[0] ----
   struct Cand { uint32_t chunk; uint64_t i; int type; uint64_t job; };
   std::vector<Cand> cands;
@@ -439,6 +454,7 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       }
     }
   }
+  TMARK("scan: candidate jobs");
   std::vector<InfRes> res;
   {
     std::vector<InfJob> fjobs;
@@ -455,6 +471,7 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
     for (size_t k = 0; k < jobs.size(); k++) if (vjob_of[k]) res[k] = vr[vjob_of[k] - 1];
   }
   c->stats.n_candidates = jobs.size();
+  TMARK("scan: candidate inflate");
   // ---- per-chunk candidate index ranges ----
   std::vector<size_t> cbeg(chunks.size() + 1, cands.size());
   for (size_t k = cands.size(); k-- > 0;) cbeg[cands[k].chunk] = k;
@@ -481,7 +498,13 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
   std::vector<long> pend0(chunks.size(), -1);
   std::vector<InfRes> cont0(chunks.size());
   {
-    std::vector<uint8_t> cv;
+    // continuation inputs (pending bytes of chunk j + the whole buffer of chunk j+1) assembled in
+    // HBM by k_gather from file ranges and the chunks' buffer[0] bytes
+    std::vector<Seg> segs;
+    std::vector<uint8_t> meta;
+    uint64_t out = 0;
+    auto add_file = [&](uint64_t off, uint64_t len) { if (len) segs.push_back({2, 0, off, out, len}); out += len; };
+    auto add_byte = [&](uint8_t b) { segs.push_back({0, 0, meta.size(), out, 1}); meta.push_back(b); out += 1; };
     std::vector<InfJob> cj;
     std::vector<uint32_t> cj_chunk;
     for (uint32_t j = 0; j + 1 < chunks.size(); j++) {
@@ -490,25 +513,36 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       if (k < 0) continue;
       const Cand& cd = cands[k];
       const Chunk& ch = chunks[j];
+      const Chunk& nx = chunks[j + 1];
       InfJob jb;
-      jb.in_off = cv.size();
-      if (cd.i == 0) { std::vector<uint8_t> v; chunk_bytes(h, ch, v); cv.insert(cv.end(), v.begin(), v.end()); }
-      else cv.insert(cv.end(), h + ch.co + cd.i, h + ch.co + ch.len);
-      std::vector<uint8_t> v; chunk_bytes(h, chunks[j + 1], v);
-      cv.insert(cv.end(), v.begin(), v.end());
-      jb.in_len = cv.size() - jb.in_off; jb.out_off = NO_OUT; jb.out_cap = 0;
+      jb.in_off = out;
+      if (cd.i == 0) { add_byte(ch.b0); add_file(ch.co + 1, ch.len - 1); }
+      else add_file(ch.co + cd.i, ch.len - cd.i);
+      add_byte(nx.b0);
+      add_file(nx.co + 1, nx.len - 1);
+      jb.in_len = out - jb.in_off; jb.out_off = NO_OUT; jb.out_cap = 0;
       cj.push_back(jb);
       cj_chunk.push_back(j);
-      cv.resize((cv.size() + 3) & ~(size_t)3);
+      out = (out + 3) & ~3ull;
     }
     if (!cj.empty()) {
-      if (int r = upload(c, c->d_virt, cv.data(), cv.size())) return r;
+      if (int r = upload(c, c->d_meta, meta.data(), meta.size())) return r;
+      if (int r = upload(c, c->d_segs, segs.data(), segs.size() * sizeof(Seg))) return r;
+      if (int r = c->d_virt.reserve(out + 4096)) return r;
+      const uint32_t nseg = (uint32_t)segs.size();
+      const uint32_t blocks = std::min<uint32_t>((nseg + 3) / 4, 65535u);
+      kbeg(c, 3);
+      hipLaunchKernelGGL(k_gather, dim3(blocks), dim3(256), 0, c->st, c->d_meta.as<uint8_t>(), nullptr, d_file,
+                         c->d_virt.as<uint8_t>(), c->d_segs.as<Seg>(), nseg);
+      kend(c);
+      KCHECK("k_gather");
       std::vector<InfRes> cr;
       if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, cj, cr)) return r;
       for (size_t q = 0; q < cj.size(); q++) cont0[cj_chunk[q]] = cr[q];
     }
     c->stats.n_continuations = cj.size();
   }
+  TMARK("scan: continuations");
   // ---- sequential replay (main.cpp:205-246 over searchInfile's chunk sequence) ----
   bool need_more = false;
   struct Pend { uint64_t off; int type; int state; std::vector<uint8_t> bytes; uint64_t in, out; long spec_chunk; int refills; } pd{};
@@ -558,6 +592,7 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       }
     }
   }
+  TMARK("scan: replay");
   c->stats.scan_ms = ms_since(t0);
   return 0;
 }

@@ -32,6 +32,7 @@
 // reference would compile to flat accesses with longer latency and vmcnt coupling).
 #define LDS __attribute__((address_space(3)))
 #define CONSTANT __attribute__((address_space(4)))
+#define GLOBAL __attribute__((address_space(1)))
 
 // Per-step shader-clock counters in the parse loop (diagnostics; s_memtime also forces lgkmcnt waits).
 #ifndef ATZ_STEP_CLOCKS
@@ -59,7 +60,9 @@ __device__ __constant__ DeflTables c_t;
 __device__ __constant__ uint8_t c_xlb[29] = {0,0,0,0,0,0,0,0,1,1,1,1,2,2,2,2,3,3,3,3,4,4,4,4,5,5,5,5,0};
 __device__ __constant__ uint8_t c_xdb[30] = {0,0,0,0,1,1,2,2,3,3,4,4,5,5,6,6,7,7,8,8,9,9,10,10,11,11,12,12,13,13};
 __device__ __constant__ uint8_t c_xblb[19] = {0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,2,3,7};
-__device__ __constant__ uint8_t c_blorder[19] = {16,17,18,0,8,7,9,6,10,5,11,4,12,3,13,2,14,1,15};
+__device__ __forceinline__ uint32_t bl_order(uint32_t i) {   // {16,17,18,0,8,7,...,1,15}, 5 bits each
+  return (uint32_t)((i < 12 ? (0x22caa324e804a30ull >> (5 * i)) : (0x3c2e1346cull >> (5 * (i - 12)))) & 31);
+}
 // configuration_table, Z/deflate.c:131-143: good, lazy, nice, chain
 __device__ __constant__ uint16_t c_cfg[10][4] = {{0,0,0,0},{4,4,8,4},{4,5,16,8},{4,6,32,32},{4,4,16,16},
     {8,16,32,32},{8,16,128,128},{8,32,128,256},{32,128,258,1024},{32,258,258,4096}};
@@ -233,13 +236,13 @@ struct TreeWork {      // one tree under construction (zlib's ct_data / heap / d
 };
 
 struct BitOut {
-  uint8_t* out;
+  GLOBAL uint8_t* out;
   uint64_t cap;
   uint64_t pos;      // bytes written
   uint64_t bb;       // pending bits (< 8 after every flush)
   uint32_t bc;
   // comparison against the original
-  const uint8_t* orig;
+  const GLOBAL uint8_t* orig;
   uint64_t clen;     // C_s
   uint64_t shortcut; // shortcut length, 0 if the shortcut does not apply
   uint64_t eq_all;   // equal bytes at positions < min(pos, C_s)
@@ -365,8 +368,9 @@ __device__ __forceinline__ void pq_down(LDS uint32_t* heap, int heap_len, int k)
 
 // build_tree + gen_bitlen (Z/trees.c:488-565, 617-699) from w.freq[0..elems).  Leaves' lengths land
 // in w.len, bl_count in w.bl_count; opt_len / static_len accumulate as in zlib.  Returns max_code.
-__device__ __noinline__ int build_tree(LDS TreeWork& w, int elems, int max_length, const uint8_t* xbits, int xbase,
-                                       const uint8_t* stlen, uint64_t& opt_len, uint64_t& static_len, int lane) {
+__device__ __noinline__ int build_tree(LDS TreeWork& w, int elems, int max_length, const CONSTANT uint8_t* xbits,
+                                       int xbase, const CONSTANT uint8_t* stlen, uint64_t& opt_len,
+                                       uint64_t& static_len, int lane) {
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   LDS uint32_t* const heap = w.heap;
   // leaves enter heap[1..] in increasing symbol order (Z/trees.c:631-638)
@@ -567,11 +571,29 @@ __device__ void send_tree(LDS BitOut& b, LDS TrialShared& s, const LDS uint8_t* 
   }
 }
 
-__device__ inline uint32_t d_code(uint32_t d) { return d < 256 ? c_t.dcode[d] : c_t.dcode[256 + (d >> 7)]; }
+__device__ __forceinline__ uint32_t len_code(uint32_t len) {   // _length_code[len], len = length - 3
+  if (len < 8) return len;
+  if (len == 255) return 28;
+  const uint32_t lg = 31u - (uint32_t)__clz(len);
+  return 4u * (lg - 1u) + ((len >> (lg - 2u)) & 3u);
+}
+__device__ __forceinline__ uint32_t dist_code(uint32_t d) {    // d_code(d), d = distance - 1
+  if (d < 4) return d;
+  const uint32_t lg = 31u - (uint32_t)__clz(d);
+  return 2u * lg + ((d >> (lg - 1u)) & 1u);
+}
+// RFC 1951 extra bits / bases in closed form (no table loads per symbol)
+__device__ __forceinline__ uint32_t lcode_extra(uint32_t c) { return (c < 8 || c == 28) ? 0u : (c - 4) >> 2; }
+__device__ __forceinline__ uint32_t lcode_base(uint32_t c) {   // base_length[c] (length - 3)
+  return c < 8 ? c : c == 28 ? 255u : ((4 + (c & 3)) << lcode_extra(c));
+}
+__device__ __forceinline__ uint32_t dcode_extra(uint32_t d) { return d < 2 ? 0u : (d >> 1) - 1; }
+__device__ __forceinline__ uint32_t dcode_base(uint32_t d) { return d < 2 ? d : ((2 + (d & 1)) << dcode_extra(d)); }  // base_dist[d]
+
 
 // Lane-parallel compress_block (Z/trees.c:1060-1105): 64 symbols per step.
 template <typename C16, typename C8>
-__device__ void compress_block(LDS BitOut& b, LDS TrialShared& s, const uint32_t* syms, uint32_t nsym,
+__device__ void compress_block(LDS BitOut& b, LDS TrialShared& s, const GLOBAL uint32_t* syms, uint32_t nsym,
                                C16 lc, C8 ll, C16 dc, C8 dl,
                                int lane) {
   // the symbols were stored by lane 0 during the parse: order those HBM stores before the reads
@@ -586,15 +608,15 @@ __device__ void compress_block(LDS BitOut& b, LDS TrialShared& s, const uint32_t
       if (dist == 0) {
         v = lc[c]; nb = ll[c];
       } else {
-        uint32_t code = c_t.lcode[c];
+        uint32_t code = len_code(c);
         v = lc[code + 257]; nb = ll[code + 257];
-        uint32_t xe = c_xlb[code];
-        if (xe) { v |= (uint64_t)(c - c_t.lbase[code]) << nb; nb += xe; }
+        uint32_t xe = lcode_extra(code);
+        if (xe) { v |= (uint64_t)(c - lcode_base(code)) << nb; nb += xe; }
         dist--;
-        uint32_t dcd = d_code(dist);
+        uint32_t dcd = dist_code(dist);
         v |= (uint64_t)dc[dcd] << nb; nb += dl[dcd];
-        uint32_t xd = c_xdb[dcd];
-        if (xd) { v |= (uint64_t)(dist - c_t.dbase[dcd]) << nb; nb += xd; }
+        uint32_t xd = dcode_extra(dcd);
+        if (xd) { v |= (uint64_t)(dist - dcode_base(dcd)) << nb; nb += xd; }
       }
     } else if (k == nsym) {
       v = lc[256]; nb = ll[256];   // END_BLOCK
@@ -668,17 +690,6 @@ struct PosWin {
   }
 };
 
-__device__ __forceinline__ uint32_t len_code(uint32_t len) {   // _length_code[len], len = length - 3
-  if (len < 8) return len;
-  if (len == 255) return 28;
-  const uint32_t lg = 31u - (uint32_t)__clz(len);
-  return 4u * (lg - 1u) + ((len >> (lg - 2u)) & 3u);
-}
-__device__ __forceinline__ uint32_t dist_code(uint32_t d) {    // d_code(d), d = distance - 1
-  if (d < 4) return d;
-  const uint32_t lg = 31u - (uint32_t)__clz(d);
-  return 2u * lg + ((d >> (lg - 1u)) & 1u);
-}
 
 // fill_window bookkeeping (Z/deflate.c:1390-1532) on absolute positions
 __device__ __forceinline__ void fill(Lz& z) {
@@ -786,7 +797,8 @@ __device__ __forceinline__ uint32_t longest_match(Lz& z, const uint8_t* in, cons
 // _tr_flush_block (Z/trees.c:907-1004) + FLUSH_BLOCK_ONLY bookkeeping
 // The parse state is passed by value so that it never leaves registers (a reference to it here
 // would put the whole parse state in scratch memory).  Returns the overlay-hazard bit.
-__device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, const uint32_t* syms, const uint8_t* in,
+__device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, const GLOBAL uint32_t* syms,
+                                             const GLOBAL uint8_t* in,
                                              int64_t block_start, uint64_t p, uint64_t S, uint32_t last_lit,
                                              uint32_t level, uint32_t lbs, int last, int lane) {
   uint32_t hazard = 0;
@@ -798,23 +810,25 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, 
   if (level > 0) {
     // literal/length tree
     for (int i = lane; i < NLC; i += 64) s.w.freq[i] = (uint16_t)s.lfreq[i];
-    lmax = build_tree(s.w, NLC, 15, c_xlb, 257, c_t.st_llen, opt_len, static_len, lane);
+    lmax = build_tree(s.w, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
+                      opt_len, static_len, lane);
     gen_codes(s.w, lmax, s.lcode, s.llen, lane);
     for (int i = lmax + 1 + lane; i < NLC + 2; i += 64) s.llen[i] = 0;
     // distance tree
     for (int i = lane; i < NDC; i += 64) s.w.freq[i] = (uint16_t)s.dfreq[i];
-    dmax = build_tree(s.w, NDC, 15, c_xdb, 0, c_t.st_dlen, opt_len, static_len, lane);
+    dmax = build_tree(s.w, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
+                      opt_len, static_len, lane);
     gen_codes(s.w, dmax, s.dcode, s.dlen, lane);
     for (int i = dmax + 1 + lane; i < NDC + 2; i += 64) s.dlen[i] = 0;
     // bit length tree
     for (int i = lane; i < NBLC; i += 64) s.bfreq[i] = 0;
     if (lane == 0) { scan_tree(s.bfreq, s.llen, lmax); scan_tree(s.bfreq, s.dlen, dmax); }
     for (int i = lane; i < NBLC; i += 64) s.w.freq[i] = (uint16_t)s.bfreq[i];
-    int bmax = build_tree(s.w, NBLC, 7, c_xblb, 0, nullptr, opt_len, static_len, lane);
+    int bmax = build_tree(s.w, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, opt_len, static_len, lane);
     gen_codes(s.w, bmax, s.bcode, s.blen, lane);
     for (int i = bmax + 1 + lane; i < NBLC + 2; i += 64) s.blen[i] = 0;
     for (max_blindex = NBLC - 1; max_blindex >= 3; max_blindex--)
-      if (s.blen[c_blorder[max_blindex]] != 0) break;
+      if (s.blen[bl_order((uint32_t)max_blindex)] != 0) break;
     opt_len += 3 * ((uint64_t)max_blindex + 1) + 5 + 5 + 4;
     opt_lenb = (opt_len + 3 + 7) >> 3;
     static_lenb = (static_len + 3 + 7) >> 3;
@@ -832,7 +846,7 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, 
     uint32_t len = (uint32_t)stored_len;
     put_bits(b, s.stage, (len & 0xffff) | ((~len & 0xffff) << 16), 32, lane);
     // copy the block's input bytes (now byte aligned, bc == 0)
-    const uint8_t* src = in + block_start;
+    const GLOBAL uint8_t* src = in + block_start;
     for (uint64_t o = 0; o < stored_len; o += 256) {
       uint32_t nb = stored_len - o < 256 ? (uint32_t)(stored_len - o) : 256u;
       for (uint32_t k = lane; k < 64; k += 64) {
@@ -855,7 +869,7 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, 
     put_bits(b, s.stage, (uint32_t)(lcodes - 257), 5, lane);
     put_bits(b, s.stage, (uint32_t)(dcodes - 1), 5, lane);
     put_bits(b, s.stage, (uint32_t)(blcodes - 4), 4, lane);
-    for (int r = 0; r < blcodes; r++) put_bits(b, s.stage, s.blen[c_blorder[r]], 3, lane);
+    for (int r = 0; r < blcodes; r++) put_bits(b, s.stage, s.blen[bl_order((uint32_t)r)], 3, lane);
     send_tree(b, s, s.llen, lcodes - 1, lane);
     send_tree(b, s, s.dlen, dcodes - 1, lane);
     flush_bits_bytes(b, s.stage, lane);
@@ -910,8 +924,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   z.match_start = 0; z.prev_match = 0; z.match_length = 2; z.prev_length = 2; z.match_available = 0;
   z.last_lit = 0; z.ins_cleared = 0; z.nsym = 0;
   LDS BitOut& b = s.b;
-  b.out = A.out + tr.out_off; b.cap = tr.out_cap; b.pos = 0; b.bb = 0; b.bc = 0;
-  b.orig = A.file + sd.orig_off; b.clen = sd.comp_len;
+  b.out = (GLOBAL uint8_t*)(A.out + tr.out_off); b.cap = tr.out_cap; b.pos = 0; b.bb = 0; b.bc = 0;
+  b.orig = (const GLOBAL uint8_t*)(A.file + sd.orig_off); b.clen = sd.comp_len;
   b.shortcut = sd.comp_len > A.o.shortcut_len ? A.o.shortcut_len : 0;
   b.eq_all = 0; b.eq_sc = 0; b.overflow = 0;
   uint32_t* const syms = A.syms + tr.sym_off;
@@ -959,7 +973,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     s.lfreq[lane] = lf0; s.lfreq[64 + lane] = lf1; s.lfreq[128 + lane] = lf2; s.lfreq[192 + lane] = lf3;
     if (lane < NLC - 256) s.lfreq[256 + lane] = lf4;
     if (lane < NDC) s.dfreq[lane] = dfr;
-    hazard |= uni(flush_block(s, b, syms, in, z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, lane));
+    hazard |= uni(flush_block(s, b, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, lane));
     lf0 = lf1 = lf2 = lf3 = 0; lf4 = lane == 0 ? 1u : 0u; dfr = 0;
     z.last_lit = 0;
     z.block_start = (int64_t)z.p;

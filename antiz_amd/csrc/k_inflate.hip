@@ -88,16 +88,18 @@ __global__ __launch_bounds__(256) void k_find_headers(const uint8_t* __restrict_
 
 __device__ __forceinline__ uint32_t iuni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
-__device__ __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
-                                                35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__device__ __constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
-                                              2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__device__ __constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
-                                                193, 257, 385, 513, 769, 1025, 1537, 2049, 3073,
-                                                4097, 6145, 8193, 12289, 16385, 24577};
-__device__ __constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
-                                              6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
-__device__ __constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+// RFC 1951 length / distance tables in closed form (an indexed __constant__ table compiles to a
+// global load per symbol).
+__device__ __forceinline__ uint32_t len_extra(uint32_t s) { return (s < 8 || s == 28) ? 0u : (s - 4) >> 2; }
+__device__ __forceinline__ uint32_t len_base(uint32_t s) {
+  return s < 8 ? 3 + s : s == 28 ? 258u : ((4 + (s & 3)) << len_extra(s)) + 3;
+}
+__device__ __forceinline__ uint32_t dist_extra(uint32_t d) { return d < 2 ? 0u : (d >> 1) - 1; }
+__device__ __forceinline__ uint32_t dist_base(uint32_t d) { return d < 2 ? d + 1 : ((2 + (d & 1)) << dist_extra(d)) + 1; }
+// code-length code order {16,17,18,0,8,7,9,6,10,5,11,4,12,3,13,2,14,1,15}, 5 bits each
+__device__ __forceinline__ uint32_t cl_order(uint32_t i) {
+  return (uint32_t)((i < 12 ? (0x22caa324e804a30ull >> (5 * i)) : (0x3c2e1346cull >> (5 * (i - 12)))) & 31);
+}
 
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   for (int d = 32; d >= 1; d >>= 1) {
@@ -151,22 +153,19 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
   const uint8_t* p0 = in_base + job.in_off;
   const uintptr_t ap = reinterpret_cast<uintptr_t>(p0);
   const uint64_t skip = ap & 3;
-  const uint32_t* const abase = reinterpret_cast<const uint32_t*>(ap - skip);
+  // global address space explicitly: a flat load would also count in lgkmcnt and make every LDS
+  // wait drain the input prefetch
+  const __attribute__((address_space(1))) uint32_t* const abase =
+      (const __attribute__((address_space(1))) uint32_t*)(ap - skip);
   const uint64_t skip_bits = 8 * skip;
   const uint64_t limit = 8 * (skip + job.in_len);   // bit limit (aligned coordinates)
-  const uint64_t lim_b = limit >> 3;
   uint64_t pos = 0, bb = 0, next_dw = 0, wbase = 1ull << 62;
   uint32_t bc = 0, cw = 0, nw = 0;
-  auto load_dw = [&](uint64_t dw) __attribute__((always_inline)) -> uint32_t {
-    const uint64_t byte0 = dw * 4;
-    uint32_t v = 0;
-    if (byte0 < lim_b) {
-      v = abase[dw];
-      const uint64_t valid = lim_b - byte0;
-      if (valid < 4) v &= (1u << (8 * valid)) - 1;
-    }
-    return v;
-  };
+  // Bits past `limit` are never consumed (every consumption is preceded by has()), and a canonical
+  // code found within the available bits is the true code whatever follows (prefix-free), so
+  // the window is loaded unmasked -- the load stays asynchronous until its first readlane.  The
+  // input buffers carry >= 4 KiB of slack for the <= 512-byte over-read.
+  auto load_dw = [&](uint64_t dw) __attribute__((always_inline)) -> uint32_t { return abase[dw]; };
   auto refill = [&]() __attribute__((always_inline)) {
     while (bc <= 32) {
       const uint64_t k = next_dw;
@@ -317,17 +316,17 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
       if (sym == 256) return R_OK;
       sym -= 257;
       if (sym >= 29) FAIL(11, need);                       // fixed codes 286/287
-      const uint32_t le = c_lext[sym];
+      const uint32_t le = len_extra((uint32_t)sym);
       NEEDB(le);
-      const uint32_t len = c_lbase[sym] + peek(le);
+      const uint32_t len = len_base((uint32_t)sym) + peek(le);
       drop(le);
       const int ds = decode(dh, false, need);
       if (ds == -2) return R_NEED;
       if (ds == -1) FAIL(12, need);
       if (ds >= 30) FAIL(13, need);                        // fixed distance 30/31
-      const uint32_t de = c_dext[ds];
+      const uint32_t de = dist_extra((uint32_t)ds);
       NEEDB(de);
-      const uint32_t dist = c_dbase[ds] + peek(de);
+      const uint32_t dist = dist_base((uint32_t)ds) + peek(de);
       drop(de);
       if ((uint64_t)dist > prod) FAIL(14, pos);            // invalid distance too far back
       // copy: read the whole source first (a period of `dist` repeats for overlapping copies)
@@ -371,7 +370,8 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
         // copy `len` bytes straight from the input (byte aligned now)
         const uint64_t avail = (limit - pos) >> 3;
         const uint64_t take = len < avail ? len : avail;
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(abase) + (pos >> 3);
+        const __attribute__((address_space(1))) uint8_t* src =
+            (const __attribute__((address_space(1))) uint8_t*)(ap - skip) + (pos >> 3);
         uint64_t done = 0;
         while (done < take) {
           uint64_t step = take - done;
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
           NEEDB(3);
           const uint32_t v = peek(3);
           drop(3);
-          if (lane == 0) lens[c_clorder[i]] = (uint16_t)v;
+          if (lane == 0) lens[cl_order(i)] = (uint16_t)v;
         }
         Huff chh;
         if (build(chh, lens, 19, 0)) FAIL(7, pos);
