@@ -117,6 +117,7 @@ struct Rec {
   uint64_t offset, comp_len, infl_len;
   int type;
   uint32_t flags;
+  uint64_t arena_off = ~0ull;   // scan output kept in the arena (complete), else ~0
 };
 
 struct StreamState {
@@ -235,7 +236,7 @@ struct atz_ctx {
   hipStream_t st = nullptr;
   DBuf d_file, d_pos, d_cnt, d_jobs, d_res, d_virt, d_infl, d_chains, d_heads, d_streams, d_trials,
       d_tres, d_out, d_syms, d_adler, d_meta, d_segs, d_atz, d_diffjobs, d_diffpos, d_diffval, d_diffcnt,
-      d_cjobs, d_tmp, d_R, d_mjobs, d_ins;
+      d_cjobs, d_tmp, d_R, d_mjobs, d_ins, d_arena, d_arena_used;
   // last scan
   std::vector<Rec> recs;
   std::vector<uint64_t> infl_off;   // per record offset in d_infl
@@ -310,16 +311,24 @@ struct Chunk {
   bool b0_file;   // buffer[0] == file[co] (buffer is contiguous file data)
 };
 
+static constexpr uint64_t ARENA_SLOT = 65536;   // arena slot per scan candidate (longer outputs are re-inflated)
+
 static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, const std::vector<InfJob>& jobs,
-                            std::vector<InfRes>& res) {
+                            std::vector<InfRes>& res, uint64_t arena_cap = 0) {
   res.resize(jobs.size());
   if (jobs.empty()) return 0;
   if (int r = upload(c, c->d_jobs, jobs.data(), jobs.size() * sizeof(InfJob))) return r;
   if (int r = c->d_res.reserve(jobs.size() * sizeof(InfRes))) return r;
+  if (int r = c->d_arena_used.reserve(64)) return r;
+  if (arena_cap) {
+    if (int r = c->d_arena.reserve(arena_cap)) return r;
+    HIPCHK(hipMemsetAsync(c->d_arena_used.p, 0, 8, c->st));
+  }
   uint32_t n = (uint32_t)jobs.size();
   kbeg(c, 1);
   hipLaunchKernelGGL(k_inflate, dim3(n), dim3(64), 0, c->st, d_in,
-                     d_out, c->d_jobs.as<InfJob>(), c->d_res.as<InfRes>(), n);
+                     d_out, c->d_jobs.as<InfJob>(), c->d_res.as<InfRes>(), n, c->d_arena.as<uint8_t>(),
+                     c->d_arena_used.as<unsigned long long>(), arena_cap);
   kend(c);
   KCHECK("k_inflate");
   HIPCHK(hipMemcpyAsync(res.data(), c->d_res.p, n * sizeof(InfRes), hipMemcpyDeviceToHost, c->st));
@@ -459,9 +468,16 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
   {
     std::vector<InfJob> fjobs;
     std::vector<size_t> fidx;
-    for (size_t k = 0; k < jobs.size(); k++) if (!vjob_of[k]) { fjobs.push_back(jobs[k]); fidx.push_back(k); }
+    for (size_t k = 0; k < jobs.size(); k++)
+      if (!vjob_of[k]) {
+        fjobs.push_back(jobs[k]);
+        fjobs.back().out_off = ARENA_OUT;     // keep the output of candidates that are streams
+        fjobs.back().out_cap = ARENA_SLOT;
+        fidx.push_back(k);
+      }
     std::vector<InfRes> fr, vr;
-    if (int r = run_inflate_jobs(c, d_file, nullptr, fjobs, fr)) return r;
+    const uint64_t arena_cap = std::min<uint64_t>(16ull << 30, std::max<uint64_t>(256ull << 20, 6 * F));
+    if (int r = run_inflate_jobs(c, d_file, nullptr, fjobs, fr, arena_cap)) return r;
     if (!vjobs.empty()) {
       if (int r = upload(c, c->d_virt, virt.data(), virt.size())) return r;
       if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, vjobs, vr)) return r;
@@ -486,7 +502,7 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       const InfRes& r = res[cd.job];
       if (r.consumed <= 16) continue;
       if (r.status == INF_END) {
-        if (out) out->push_back({cd.i + ch.co, r.consumed, r.produced, cd.type, 0});
+        if (out) out->push_back({cd.i + ch.co, r.consumed, r.produced, cd.type, 0, r.arena_off});
         i = cd.i + r.consumed;
       } else if (r.consumed == ch.len - cd.i) {
         return (long)k;
@@ -603,25 +619,53 @@ static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F) {
   c->infl_off.resize(n);
   c->adler.resize(n);
   uint64_t tot = 0;
-  std::vector<InfJob> jobs(n);
+  // Streams whose scan decode kept its full output in the arena are copied; the others are
+  // inflated again from the file with their exact length (doInflate, main.cpp:461-486) -- the
+  // same bytes from the same offset, so both give the same result.
+  std::vector<InfJob> jobs;
+  std::vector<size_t> job_rec;
+  std::vector<Seg> segs;
   for (size_t s = 0; s < n; s++) {
     const Rec& r = c->recs[s];
     if (r.offset + r.comp_len > F) return ATZ_E_REF_UB;   // reads past EOF (uninitialised rBuffer)
     c->infl_off[s] = tot;
-    jobs[s].in_off = r.offset; jobs[s].in_len = r.comp_len; jobs[s].out_off = tot; jobs[s].out_cap = r.infl_len;
+    if (r.arena_off != ~0ull) {
+      segs.push_back({0, 0, r.arena_off, tot, r.infl_len});
+    } else {
+      InfJob jb;
+      jb.in_off = r.offset; jb.in_len = r.comp_len; jb.out_off = tot; jb.out_cap = r.infl_len;
+      jobs.push_back(jb);
+      job_rec.push_back(s);
+    }
     tot += (r.infl_len + 255) & ~255ull;
   }
   if (int r = c->d_infl.reserve(tot + 65536)) return r;
+  if (!segs.empty()) {
+    if (int r = upload(c, c->d_segs, segs.data(), segs.size() * sizeof(Seg))) return r;
+    const uint32_t nseg = (uint32_t)segs.size();
+    const uint32_t blocks = std::min<uint32_t>((nseg + 3) / 4, 65535u);
+    kbeg(c, 3);
+    hipLaunchKernelGGL(k_gather, dim3(blocks), dim3(256), 0, c->st, c->d_arena.as<uint8_t>(), nullptr, nullptr,
+                       c->d_infl.as<uint8_t>(), c->d_segs.as<Seg>(), nseg);
+    kend(c);
+    KCHECK("k_gather");
+  }
   std::vector<InfRes> res;
   if (int r = run_inflate_jobs(c, d_file, c->d_infl.as<uint8_t>(), jobs, res)) return r;
+  for (size_t q = 0; q < jobs.size(); q++) {
+    const size_t s = job_rec[q];
+    if (res[q].status != INF_END) return ATZ_E_REF_ABORT;          // main.cpp:450-452
+    if (res[q].produced != c->recs[s].infl_len || res[q].consumed != c->recs[s].comp_len) return ATZ_E_REF_UB;
+  }
+  c->stats.n_reinflated = jobs.size();
   for (size_t s = 0; s < n; s++) {
-    if (res[s].status != INF_END) return ATZ_E_REF_ABORT;          // main.cpp:450-452
-    if (res[s].produced != c->recs[s].infl_len) return ATZ_E_REF_UB;
     // Adler-32 of the inflated bytes = the verified trailer
-    const uint64_t e = c->recs[s].offset + res[s].consumed;
+    const uint64_t e = c->recs[s].offset + c->recs[s].comp_len;
     c->adler[s] = ((uint32_t)c->hfile[e - 4] << 24) | ((uint32_t)c->hfile[e - 3] << 16) |
                   ((uint32_t)c->hfile[e - 2] << 8) | c->hfile[e - 1];
   }
+  HIPCHK(hipStreamSynchronize(c->st));
+  kcollect(c);
   return 0;
 }
 

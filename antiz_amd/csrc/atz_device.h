@@ -15,6 +15,8 @@ struct InfJob {
   uint64_t out_cap;  // output capacity (ignored when NO_OUT)
 };
 static constexpr uint64_t NO_OUT = ~0ull;
+static constexpr uint64_t ARENA_OUT = ~1ull;   // output into the arena: a slot of out_cap bytes claimed at first flush
+static constexpr uint64_t ARENA_NONE = ~0ull;
 
 enum : uint32_t { INF_END = 0, INF_ERROR = 1, INF_NEED = 2 };
 
@@ -23,6 +25,7 @@ struct InfRes {
   uint32_t err;       // diagnostic code of the failing check
   uint64_t consumed;  // zlib total_in at the stop
   uint64_t produced;  // zlib total_out at the stop
+  uint64_t arena_off; // ARENA_OUT jobs: offset of the output slot (ARENA_NONE: none / incomplete)
 };
 
 // ---- deflate trial (k_trial) ---------------------------------------------------------------

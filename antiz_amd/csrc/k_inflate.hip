@@ -140,7 +140,8 @@ struct InfShared {
 
 __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_base, uint8_t* __restrict__ out_base,
                                                const InfJob* __restrict__ jobs, InfRes* __restrict__ res,
-                                               uint32_t njobs) {
+                                               uint32_t njobs, uint8_t* __restrict__ arena,
+                                               unsigned long long* __restrict__ arena_used, uint64_t arena_cap) {
   __shared__ InfShared sh;
   const int lane = threadIdx.x;
   const uint32_t j = blockIdx.x;
@@ -194,14 +195,27 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
   auto has = [&](uint64_t k) __attribute__((always_inline)) -> bool { return pos + k <= limit; };
 
   // ---- output: LDS history ring, flushed to HBM (if kept) and folded into Adler-32 every 16 KiB
-  uint8_t* const out = job.out_off == NO_OUT ? nullptr : out_base + job.out_off;
+  // output: to out_base + out_off, nowhere (NO_OUT), or to an arena slot of out_cap bytes claimed
+  // at the first flush (ARENA_OUT: scan candidates keep their output if they turn out to be streams)
+  const bool to_arena = job.out_off == ARENA_OUT;
+  uint8_t* out = (job.out_off == NO_OUT || to_arena) ? nullptr : out_base + job.out_off;
+  uint64_t arena_off = ARENA_NONE;
+  bool arena_tried = false;
   const uint64_t out_cap = job.out_cap;
   uint64_t prod = 0, flushed = 0;
   uint32_t ad_a = 1, ad_b = 0;
   int overflow = 0;
-  auto flush = [&]() __attribute__((always_inline)) {
+  auto flush = [&](bool final) __attribute__((always_inline)) {
     const uint64_t n = prod - flushed;
     if (!n) return;
+    if (to_arena && !arena_tried) {
+      arena_tried = true;
+      const uint64_t want = final ? ((prod + 255) & ~255ull) : out_cap;
+      unsigned long long o = 0;
+      if (lane == 0) o = atomicAdd(arena_used, (unsigned long long)want);
+      o = __shfl(o, 0, 64);
+      if (o + want <= arena_cap && (final || prod <= out_cap)) { arena_off = o; out = arena + o; }
+    }
     uint64_t S = 0, W = 0;
     for (uint64_t k = lane; k < n; k += 64) {
       const uint32_t x = ring[(flushed + k) & RMASK];
@@ -215,7 +229,10 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
     b = (b + (n % 65521) * a + W) % 65521;
     a = (a + S) % 65521;
     ad_a = iuni((uint32_t)a); ad_b = iuni((uint32_t)b);
-    if (out && prod > out_cap) overflow = 1;
+    if (out && prod > out_cap) {
+      overflow = to_arena ? 0 : 1;   // an arena slot that overflows is just dropped
+      if (to_arena) { arena_off = ARENA_NONE; out = nullptr; }
+    }
     flushed = prod;
   };
 
@@ -310,7 +327,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
       if (sym < 256) {
         if (lane == 0) ring[prod & RMASK] = (uint8_t)sym;
         prod++;
-        if (prod - flushed >= FLUSH_AT) flush();
+        if (prod - flushed >= FLUSH_AT) flush(false);
         continue;
       }
       if (sym == 256) return R_OK;
@@ -339,7 +356,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
         if (i < len) ring[(prod + i) & RMASK] = v;
       }
       prod += len;
-      if (prod - flushed >= FLUSH_AT) flush();
+      if (prod - flushed >= FLUSH_AT) flush(false);
     }
   };
 
@@ -377,11 +394,11 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
           uint64_t step = take - done;
           if (step > 4096) step = 4096;
           const uint64_t room = RING - (prod - flushed);
-          if (step > room) { flush(); continue; }
+          if (step > room) { flush(false); continue; }
           for (uint64_t k = lane; k < step; k += 64) ring[(prod + k) & RMASK] = src[done + k];
           prod += step;
           done += step;
-          if (prod - flushed >= FLUSH_AT) flush();
+          if (prod - flushed >= FLUSH_AT) flush(false);
         }
         seek(pos + 8 * take);
         if (take < len) return R_NEED;
@@ -453,7 +470,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
     const uint32_t t = peek(32);
     const uint32_t want = ((t & 0xff) << 24) | ((t & 0xff00) << 8) | ((t >> 8) & 0xff00) | (t >> 24);
     drop(32);
-    flush();
+    flush(true);
     const uint32_t adler = (ad_b << 16) | ad_a;
     if (want != adler) FAIL(16, pos);
     return R_OK;
@@ -464,6 +481,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
   seek(8 * skip);
   const int rr = body();
   InfRes o;
+  o.arena_off = (rr == R_OK && to_arena) ? arena_off : ARENA_NONE;
   o.produced = prod;
   o.err = errcode;
   if (rr == R_OK && !overflow) {
