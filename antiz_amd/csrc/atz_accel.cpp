@@ -748,6 +748,13 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
                       std::vector<TrialRes>* res) {
   uint64_t r_tot = 0;
   std::vector<MatchJob> mj;
+  for (int k = 0; k < 3; k++)
+    for (const Trial& t : tr[k])
+      if (c->recs[t.stream].infl_len >= (1ull << 31)) {   // trial kernels keep 32-bit positions
+        std::fprintf(stderr, "atz: stream of %llu inflated bytes exceeds the 2 GiB trial limit\n",
+                     (unsigned long long)c->recs[t.stream].infl_len);
+        return ATZ_E_ARG;
+      }
   for (int k = 1; k < 3; k++)
     for (Trial& t : tr[k]) {
       const uint64_t n = c->recs[t.stream].infl_len;

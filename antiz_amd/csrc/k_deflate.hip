@@ -655,17 +655,18 @@ struct Lz {
   // parameters
   uint32_t level, kind, wsize, maxdist, lbs, good, lazy, nice, chain;
   // absolute-position state
-  uint64_t n;           // I_s
-  uint64_t p;           // strstart
-  uint64_t lookahead;
-  uint64_t S;           // total window slide
-  int64_t block_start;  // absolute
-  uint64_t match_start, prev_match;
+  // 32-bit positions (streams < 2 GiB, checked on the host): the scalar unit has no 64-bit
+  // ordered compares, so 64-bit positions would turn every comparison into VALU + VCC round trips
+  uint32_t n;           // I_s
+  uint32_t p;           // strstart
+  uint32_t lookahead;
+  uint32_t S;           // total window slide
+  uint32_t block_start; // absolute
+  uint32_t match_start, prev_match;
   uint32_t match_length, prev_length;
   int match_available;
   uint32_t last_lit;
-  uint64_t ins_cleared;  // fast mode: bitmap cleared up to (exclusive)
-  uint64_t nsym;
+  uint32_t nsym;
 };
 
 // Double-buffered lane-resident window over the trial's match table: lane l holds the entry of
@@ -673,10 +674,10 @@ struct Lz {
 // per-position data with v_readlane and the next HBM round trip overlaps ~64 positions of work.
 struct PosWin {
   const uint2* R;
-  uint64_t rb;
+  uint32_t rb;
   uint32_t cx, cy, nx, ny;
-  __device__ __forceinline__ void init(const uint2* r) { R = r; rb = 1ull << 62; cx = cy = nx = ny = 0; }
-  __device__ __forceinline__ uint2 get(uint64_t p, int lane) {
+  __device__ __forceinline__ void init(const uint2* r) { R = r; rb = 1u << 31; cx = cy = nx = ny = 0; }
+  __device__ __forceinline__ uint2 get(uint32_t p, int lane) {
     if (p - rb >= 64) {
       if (p - rb < 128) { cx = nx; cy = ny; rb += 64; }
       else { rb = p; const uint2 e = R[rb + lane]; cx = e.x; cy = e.y; }
@@ -694,12 +695,12 @@ struct PosWin {
 // fill_window bookkeeping (Z/deflate.c:1390-1532) on absolute positions
 __device__ __forceinline__ void fill(Lz& z) {
   do {
-    uint64_t sw = z.p - z.S;
-    uint64_t more = 2ull * z.wsize - z.lookahead - sw;
-    if (sw >= (uint64_t)z.wsize + z.maxdist) { z.S += z.wsize; more += z.wsize; }
-    uint64_t rd = z.p + z.lookahead;
+    uint32_t sw = z.p - z.S;
+    uint32_t more = 2u * z.wsize - z.lookahead - sw;
+    if (sw >= z.wsize + z.maxdist) { z.S += z.wsize; more += z.wsize; }
+    uint32_t rd = z.p + z.lookahead;
     if (rd >= z.n) break;
-    uint64_t k = z.n - rd;
+    uint32_t k = z.n - rd;
     if (k > more) k = more;
     z.lookahead += k;
   } while (z.lookahead < LOOKMIN && z.p + z.lookahead < z.n);
@@ -726,17 +727,17 @@ __device__ inline uint32_t common_len(const uint8_t* in, uint64_t a, uint64_t b,
 // ring is read back only with wave-uniform loads, i.e. by the lane that wrote it.
 struct InsRing {
   uint32_t* ring;
-  uint64_t w0;     // multiple of 32
+  uint32_t w0;     // multiple of 32
   uint64_t mask;   // bit k: position w0 + k inserted
-  __device__ __forceinline__ void set(uint64_t q) { mask |= 1ull << (q - w0); }
-  __device__ __forceinline__ void advance(uint64_t p) {   // keep p < w0 + 32
+  __device__ __forceinline__ void set(uint32_t q) { mask |= 1ull << (q - w0); }
+  __device__ __forceinline__ void advance(uint32_t p) {   // keep p < w0 + 32
     while (p >= w0 + 32) {
       ring[(w0 >> 5) & (BITMAP_BITS / 32 - 1)] = (uint32_t)mask;
       mask >>= 32;
       w0 += 32;
     }
   }
-  __device__ __forceinline__ bool get(uint64_t q) const {
+  __device__ __forceinline__ bool get(uint32_t q) const {
     if (q >= w0) return (mask >> (q - w0)) & 1;
     const uint32_t w = uni(ring[(q >> 5) & (BITMAP_BITS / 32 - 1)]);
     return (w >> (q & 31)) & 1;
@@ -744,7 +745,7 @@ struct InsRing {
 };
 
 template <int KIND>
-__device__ __forceinline__ bool is_inserted(const InsRing* ins, uint64_t q) {
+__device__ __forceinline__ bool is_inserted(const InsRing* ins, uint32_t q) {
   if constexpr (KIND != 1) return true;
   else return ins->get(q);
 }
@@ -752,17 +753,17 @@ __device__ __forceinline__ bool is_inserted(const InsRing* ins, uint64_t q) {
 // longest_match on the shared chains (Z/deflate.c:1148-1289).  Returns match length; sets z.match_start.
 template <int KIND>
 __device__ __forceinline__ uint32_t longest_match(Lz& z, const uint8_t* in, const uint16_t* ch, const InsRing* ins,
-                                  uint64_t cur, int lane) {
+                                  uint32_t cur, int lane) {
   uint32_t chain = z.chain;
-  const uint64_t p = z.p;
+  const uint32_t p = z.p;
   uint32_t best = z.prev_length;
   uint32_t nice = z.nice;
   if (z.prev_length >= z.good) chain >>= 2;
   if (nice > z.lookahead) nice = (uint32_t)z.lookahead;
   // continue while next > limit (window limit translated to absolute positions)
-  const uint64_t sw = p - z.S;
-  const uint64_t limit = sw > z.maxdist ? p - z.maxdist : z.S;
-  const uint64_t avail = z.n - p;                       // bytes left in the input
+  const uint32_t sw = p - z.S;
+  const uint32_t limit = sw > z.maxdist ? p - z.maxdist : z.S;
+  const uint32_t avail = z.n - p;                       // bytes left in the input
   const uint32_t cap = avail < 258 ? (uint32_t)avail : 258u;
   for (;;) {
     // quick reject: match[best], match[best-1], match[0], match[1] (bytes past the input read as 0)
@@ -779,7 +780,7 @@ __device__ __forceinline__ uint32_t longest_match(Lz& z, const uint8_t* in, cons
       }
     }
     // next link on the chain (skipping positions deflate_fast did not insert)
-    uint64_t nx = cur;
+    uint32_t nx = cur;
     bool stop = false;
     for (;;) {
       uint32_t d = uni((uint32_t)ch[nx]);
@@ -922,7 +923,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   z.good = c_cfg[z.level][0]; z.lazy = c_cfg[z.level][1]; z.nice = c_cfg[z.level][2]; z.chain = c_cfg[z.level][3];
   z.n = sd.infl_len; z.p = 0; z.lookahead = 0; z.S = 0; z.block_start = 0;
   z.match_start = 0; z.prev_match = 0; z.match_length = 2; z.prev_length = 2; z.match_available = 0;
-  z.last_lit = 0; z.ins_cleared = 0; z.nsym = 0;
+  z.last_lit = 0; z.nsym = 0;
   LDS BitOut& b = s.b;
   b.out = (GLOBAL uint8_t*)(A.out + tr.out_off); b.cap = tr.out_cap; b.pos = 0; b.bb = 0; b.bc = 0;
   b.orig = (const GLOBAL uint8_t*)(A.file + sd.orig_off); b.clen = sd.comp_len;
@@ -973,10 +974,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     s.lfreq[lane] = lf0; s.lfreq[64 + lane] = lf1; s.lfreq[128 + lane] = lf2; s.lfreq[192 + lane] = lf3;
     if (lane < NLC - 256) s.lfreq[256 + lane] = lf4;
     if (lane < NDC) s.dfreq[lane] = dfr;
-    hazard |= uni(flush_block(s, b, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, lane));
+    hazard |= uni(flush_block(s, b, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, lane));
     lf0 = lf1 = lf2 = lf3 = 0; lf4 = lane == 0 ? 1u : 0u; dfr = 0;
     z.last_lit = 0;
-    z.block_start = (int64_t)z.p;
+    z.block_start = z.p;
   };
   uint32_t state = ~0u;
   uint64_t fallbacks = 0, cyc_lookup = 0, cyc_fb = 0;
@@ -1005,7 +1006,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       if (z.lookahead <= 1) { fill(z); if (z.lookahead == 0) break; }
       z.p += z.lookahead;
       z.lookahead = 0;
-      uint64_t max_start = (uint64_t)z.block_start + max_block;
+      const uint32_t max_start = z.block_start + (uint32_t)max_block;
       if (z.p == 0 || z.p >= max_start) {
         z.lookahead = z.p - max_start;
         z.p = max_start;
@@ -1013,7 +1014,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
         if (state != ~0u) break;
       }
-      if (z.p - (uint64_t)z.block_start >= z.maxdist) {
+      if (z.p - z.block_start >= z.maxdist) {
         FLUSH(0);
         state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
         if (state != ~0u) break;
@@ -1042,11 +1043,11 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         // so a walk that ended by nice_match or by the end of the chain keeps its winner W if W
         // itself was inserted (and with no winner the step emits a literal either way); only a
         // walk that spent its budget with nodes left can see new nodes (bit 12).
-        bool exact = hl == 0 || (uint64_t)(hl - 1) < z.p - (e.y >> 16);
+        bool exact = hl == 0 || hl - 1 < z.p - (e.y >> 16);
         if (!exact && !((e.y >> 12) & 1u)) {
           if ((e.x >> 23) <= 2) exact = true;
           else {
-            const uint64_t wpos = z.p - ((e.x >> 8) & 0x7fffu);
+            const uint32_t wpos = z.p - ((e.x >> 8) & 0x7fffu);
             exact = wpos > z.S && insr.get(wpos);
           }
         }
@@ -1060,7 +1061,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           fallbacks++;
           const uint64_t cf0 = STEP_CLOCK();
           // head[] = most recent inserted same-hash position
-          uint64_t q = z.p, hh = 0;
+          uint32_t q = z.p, hh = 0;
           bool hv = false;
           for (;;) {
             uint32_t d = uni((uint32_t)ch[q]);
@@ -1087,7 +1088,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         } else {
           // p+1 .. p+ml-1 are not inserted: record them per hash slot
           for (uint32_t k0 = 1; k0 < ml; k0 += 64) {
-            const uint64_t q = z.p + k0 + lane;
+            const uint32_t q = z.p + k0 + lane;
             if (k0 + lane < ml && q + 3 <= z.n) {
               const uint32_t hq = (((uint32_t)in[q] << (2 * hshift)) ^ ((uint32_t)in[q + 1] << hshift) ^ in[q + 2]) & hmask;
               atomicMax(&holes[hq & (HOLE_SLOTS - 1)], (uint32_t)(q + 1));
