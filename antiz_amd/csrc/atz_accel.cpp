@@ -919,6 +919,21 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
         // trial input read + compare read (bytes emitted and compared against the original)
         c->stats.k_trial_alg_bytes += c->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
       }
+    if (timing_on()) {   // slowest trials of the round (diagnostics)
+      std::vector<std::pair<uint64_t, std::pair<int, size_t>>> top;
+      for (int k = 0; k < 3; k++)
+        for (size_t q = 0; q < tr[k].size(); q++) top.push_back({trres[k][q].cyc_total, {k, q}});
+      std::sort(top.begin(), top.end(), [](auto& a, auto& b) { return a.first > b.first; });
+      for (size_t i = 0; i < top.size() && i < 3; i++) {
+        const Trial& t = tr[top[i].second.first][top[i].second.second];
+        const TrialRes& r = trres[top[i].second.first][top[i].second.second];
+        std::fprintf(stderr, "atz: round %llu slow trial: stream %u I=%llu c%u w%u m%u state %u cyc %.1fM syms %llu blocks %llu "
+                     "fallbacks %llu tree %.1fM emit %.1fM\n", (unsigned long long)rounds, t.stream,
+                     (unsigned long long)c->recs[t.stream].infl_len, t.clevel, t.window, t.memlevel, r.state,
+                     r.cyc_total / 1e6, (unsigned long long)r.symbols, (unsigned long long)r.blocks,
+                     (unsigned long long)r.fallbacks, r.cyc_tree / 1e6, r.cyc_emit / 1e6);
+      }
+    }
     // apply the reference's sequential rule per stream, in list order
     std::vector<DiffJob> dj;
     std::vector<uint32_t> dj_stream;   // ~0u: superseded by a later improvement of the same stream
