@@ -671,7 +671,19 @@ static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F) {
 
 // ---------------------------------------------------------------------------------------------
 // Phase 3
+// Hash buckets per (stream, memLevel), built on demand by k_buckets and cached in HBM for the
+// sweep (8 bytes per position).  When a round would push the cache past its cap the cache is
+// dropped and the round's tables are rebuilt.
+static constexpr uint64_t CHAIN_CACHE_CAP = 48ull << 30;
 static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>& need) {
+  auto words = [&](uint32_t s) { return 2 * ((c->recs[s].infl_len + 63) & ~63ull); };
+  uint64_t add = 0;
+  for (auto& q : need)
+    if (c->chain_off[q.first][q.second] == ~0ull) add += words(q.first);
+  if ((c->chain_used + add) * 4 > CHAIN_CACHE_CAP) {   // drop the cache
+    for (auto& a : c->chain_off) a.fill(~0ull);
+    c->chain_used = 0;
+  }
   std::vector<ChainJob> jobs;
   for (auto& q : need) {
     uint32_t s = q.first;
@@ -684,40 +696,40 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
     jb.memlevel = (uint32_t)m;
     jb.slot = 0;
     c->chain_off[s][m] = c->chain_used;
-    c->chain_used += (jb.n + 63) & ~63ull;
+    c->chain_used += words(s);
     jobs.push_back(jb);
   }
   if (jobs.empty()) return 0;
-  // grow the chain cache (keeps contents)
-  size_t need_bytes = c->chain_used * 2 + 4096;
+  // grow the cache (keeps contents)
+  size_t need_bytes = c->chain_used * 4 + 4096;
   if (need_bytes > c->d_chains.n) {
     void* np = nullptr;
-    size_t cap = need_bytes + need_bytes / 2 + (64 << 20);
+    size_t cap = std::min<size_t>(need_bytes + need_bytes / 2 + (64 << 20), CHAIN_CACHE_CAP + (1ull << 30));
+    if (cap < need_bytes) cap = need_bytes;
     if (hipMalloc(&np, cap) != hipSuccess) return ATZ_E_NOMEM;
     if (c->d_chains.p) {
       HIPCHK(hipMemcpyAsync(np, c->d_chains.p, c->d_chains.n, hipMemcpyDeviceToDevice, c->st));
       HIPCHK(hipStreamSynchronize(c->st));
-      hipFree(c->d_chains.p);
+      (void)hipFree(c->d_chains.p);
     }
     c->d_chains.p = np;
     c->d_chains.n = cap;
   }
-  const uint64_t slot_words = 1u << 16;
-  const size_t batch = 4096;
-  if (int r = c->d_heads.reserve(batch * slot_words * 4)) return r;
+  const size_t batch = 1024;   // scratch: 2 x 65536 words per job
+  if (int r = c->d_heads.reserve(batch * 131072 * 4)) return r;
   for (size_t b0 = 0; b0 < jobs.size(); b0 += batch) {
     size_t nb = std::min(batch, jobs.size() - b0);
     for (size_t k = 0; k < nb; k++) jobs[b0 + k].slot = (uint32_t)k;
     if (int r = upload(c, c->d_cjobs, jobs.data() + b0, nb * sizeof(ChainJob))) return r;
     kbeg(c, 2);
-    hipLaunchKernelGGL(k_chains, dim3((uint32_t)nb), dim3(64), 0, c->st, c->d_infl.as<uint8_t>(),
-                       c->d_cjobs.as<ChainJob>(), c->d_chains.as<uint16_t>(), c->d_heads.as<uint32_t>(),
-                       slot_words, (uint32_t)nb);
+    hipLaunchKernelGGL(k_buckets, dim3((uint32_t)nb), dim3(64), 0, c->st, c->d_infl.as<uint8_t>(),
+                       c->d_cjobs.as<ChainJob>(), c->d_chains.as<uint32_t>(), c->d_heads.as<uint32_t>(),
+                       (uint32_t)nb);
     kend(c);
-    KCHECK("k_chains");
+    KCHECK("k_buckets");
     HIPCHK(hipStreamSynchronize(c->st));
     kcollect(c);
-    for (size_t k = 0; k < nb; k++) c->stats.k_chains_alg_bytes += 3 * jobs[b0 + k].n;  // read I_s, write 2*I_s
+    for (size_t k = 0; k < nb; k++) c->stats.k_chains_alg_bytes += 9 * jobs[b0 + k].n;  // read I_s, write 8*I_s
   }
   return 0;
 }
@@ -734,7 +746,7 @@ static int launch_match(atz_ctx* c, const std::vector<MatchJob>& mj) {
   if (int r = upload(c, c->d_mjobs, mj.data(), mj.size() * sizeof(MatchJob))) return r;
   kbeg(c, 4);
   hipLaunchKernelGGL(k_match, dim3((uint32_t)mj.size()), dim3(256), 0, c->st, c->d_infl.as<uint8_t>(),
-                     c->d_chains.as<uint16_t>(), c->d_R.as<uint2>(), c->d_mjobs.as<MatchJob>());
+                     c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(), c->d_mjobs.as<MatchJob>());
   kend(c);
   KCHECK("k_match");
   for (const MatchJob& m : mj) c->stats.k_match_positions += m.p1 - m.p0;
@@ -767,8 +779,6 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
       if (m.p1 > m.p0) mj.push_back(m);
     }
   if (int r = c->d_R.reserve(r_tot * sizeof(uint2) + 4096)) return r;
-  for (size_t q = 0; q < tr[1].size(); q++) tr[1][q].ins_off = 2048ull * q;
-  if (int r = c->d_ins.reserve(2048ull * 4 * tr[1].size() + 4096)) return r;
   if (int r = launch_match(c, mj)) return r;
   const size_t tot_trials = tr[0].size() + tr[1].size() + tr[2].size();
   if (int r = c->d_trials.reserve(2 * tot_trials * sizeof(Trial) + 64)) return r;
@@ -776,9 +786,8 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
   auto launch = [&](int k, const Trial* h, size_t cnt, size_t base) -> int {
     HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + base, h, cnt * sizeof(Trial), hipMemcpyHostToDevice, c->st));
     SweepArgs A;
-    A.file = d_cmp; A.infl = c->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint16_t>();
+    A.file = d_cmp; A.infl = c->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint32_t>();
     A.R = c->d_R.as<uint2>();
-    A.ins = c->d_ins.as<uint32_t>();
     A.streams = c->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
     A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
     A.adler = c->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)cnt;

@@ -36,10 +36,9 @@ struct Trial {
   uint64_t out_off;     // scratch output offset for this trial (bytes)
   uint64_t out_cap;     // scratch output capacity (bytes)
   uint64_t sym_off;     // symbol-buffer offset (uint32 units), capacity 1 << (memlevel + 6)
-  uint64_t chain_off;   // chain-link table of (stream, memlevel) (uint16 units); unused for level 0
+  uint64_t chain_off;   // hash buckets of (stream, memlevel) (uint32 units, k_buckets); unused for level 0
   uint64_t r_off;       // match table of this trial (uint2 units, indexed by absolute position)
   uint64_t x_lim;       // match-table entries exist for positions < x_lim (else the trial stops: TR_NEED_R)
-  uint64_t ins_off;     // fast levels: insertion ring (uint32 words, 2048 per trial)
 };
 
 // ---- match tables (k_match) ----------------------------------------------------------------
@@ -50,7 +49,7 @@ struct Trial {
 // result = len:9 | dist:15 (0 = no match longer than MIN_MATCH-1); see k_match for the packing.
 struct MatchJob {
   uint64_t infl_off, n;   // stream bytes
-  uint64_t chain_off;     // u16 units
+  uint64_t chain_off;     // u32 units (hash buckets)
   uint64_t r_off;         // uint2 units
   uint64_t p0, p1;        // positions [p0, p1)
   uint32_t level, window;

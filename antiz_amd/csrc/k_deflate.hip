@@ -79,65 +79,91 @@ extern "C" hipError_t atz_upload_defl_tables(const void* host_tables) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_chains
+// k_buckets: zlib's hash chains (INSERT_STRING, Z/deflate.c:181-190) for every position of a stream,
+// as hash buckets: bpos[] = the positions sorted by (hash, position), sidx[p] = p's index in bpos.
+// The chain of p is then the descending run bpos[sidx[p]-1], bpos[sidx[p]-2], ... down to the
+// bucket's first entry (bit 31 set) -- contiguous memory instead of a linked list, so walks issue
+// independent loads.  zlib's rolling hash is a pure function of 3 bytes (3*hash_shift >= hash_bits)
+// and deflate_slow inserts every position, so the buckets depend only on (stream, memLevel) and
+// are shared by every trial; deflate_fast's partial insertion is handled in the trial.
+// Layout at chain_off (u32 units): sidx[npad] then bpos[npad], npad = n rounded up to 64.
 struct ChainJob {
   uint64_t infl_off;   // stream bytes in the inflated buffer
   uint64_t n;          // I_s
-  uint64_t chain_off;  // output offset in u16 units in the chain buffer
+  uint64_t chain_off;  // u32 units in the chain buffer
   uint32_t memlevel;
-  uint32_t slot;       // head-table scratch slot
+  uint32_t slot;       // scratch slot (2 x 65536 words)
 };
+static constexpr uint32_t BUCKET_FIRST = 0x80000000u;
 
-__global__ __launch_bounds__(64) void k_chains(const uint8_t* __restrict__ infl, const ChainJob* __restrict__ jobs,
-                                              uint16_t* __restrict__ chains, uint32_t* __restrict__ heads,
-                                              uint64_t head_slot_words, uint32_t njobs) {
+__global__ __launch_bounds__(64) void k_buckets(const uint8_t* __restrict__ infl, const ChainJob* __restrict__ jobs,
+                                               uint32_t* __restrict__ chains, uint32_t* __restrict__ scratch,
+                                               uint32_t njobs) {
   const uint32_t j = blockIdx.x;
   if (j >= njobs) return;
   const int lane = threadIdx.x;
   const ChainJob jb = jobs[j];
   const uint8_t* in = infl + jb.infl_off;
-  uint16_t* out = chains + jb.chain_off;
-  const uint32_t hbits = jb.memlevel + 7, hmask = (1u << hbits) - 1, hshift = (hbits + 2) / 3;
-  uint32_t* head = heads + (uint64_t)jb.slot * head_slot_words;   // stores position+1 (0 = empty)
-  for (uint32_t i = lane; i <= hmask; i += 64) head[i] = 0;
+  const uint32_t n = (uint32_t)jb.n;
+  const uint32_t npad = (n + 63) & ~63u;
+  uint32_t* sidx = chains + jb.chain_off;
+  uint32_t* bpos = sidx + npad;
+  const uint32_t hbits = jb.memlevel + 7, hsize = 1u << hbits, hmask = hsize - 1, hshift = (hbits + 2) / 3;
+  uint32_t* cnt = scratch + (uint64_t)jb.slot * 131072;   // per hash: count, then "assigned so far"
+  uint32_t* base = cnt + 65536;                            // per hash: first index in bpos
+  for (uint32_t i = lane; i < hsize; i += 64) cnt[i] = 0;
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-  const uint64_t n = jb.n;
-  for (uint64_t base = 0; base < n; base += 64) {
-    const uint64_t p = base + lane;
-    const bool valid = p + 2 < n;
-    uint32_t h = 0x3ffffff;
-    if (valid) h = ((((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask);
-    // bitonic sort of (hash, lane) across the wave
+  const uint32_t nh = n >= 3 ? n - 2 : 0;                 // positions with a hash (p + 3 <= n)
+  auto hash = [&](uint32_t p) -> uint32_t {
+    return (((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask;
+  };
+  for (uint32_t p = lane; p < nh; p += 64) atomicAdd(&cnt[hash(p)], 1u);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  // exclusive scan of the counts
+  uint32_t run = 0;
+  for (uint32_t g = 0; g < hsize; g += 64) {
+    const uint32_t c = cnt[g + lane];
+    uint32_t incl = c;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += t;
+    }
+    base[g + lane] = run + incl - c;
+    cnt[g + lane] = 0;
+    run += __shfl(incl, 63, 64);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  // assignment in position order: 64 positions at a time, bitonic-sorted by (hash, lane)
+  for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
+    const uint32_t p = b0 + lane;
+    const uint32_t h = p < nh ? hash(p) : 0x3ffffffu;
     uint32_t key = (h << 6) | (uint32_t)lane;
-    for (int k = 2; k <= 64; k <<= 1) {
-      for (int s = k >> 1; s > 0; s >>= 1) {
-        uint32_t o = __shfl_xor(key, s, 64);
-        bool up = (lane & k) == 0;
-        bool lower = (lane & s) == 0;
-        uint32_t mn = key < o ? key : o, mx = key < o ? o : key;
+    for (int k = 2; k <= 64; k <<= 1)
+      for (int st = k >> 1; st > 0; st >>= 1) {
+        const uint32_t o = __shfl_xor(key, st, 64);
+        const bool up = (lane & k) == 0, lower = (lane & st) == 0;
+        const uint32_t mn = key < o ? key : o, mx = key < o ? o : key;
         key = (lower == up) ? mn : mx;
       }
-    }
     const uint32_t kh = key >> 6;
-    const uint64_t mypos = base + (key & 63);
-    uint32_t pk = __shfl_up(key, 1, 64);
-    uint32_t nk = __shfl_down(key, 1, 64);
-    const bool first_of_group = lane == 0 || (pk >> 6) != kh;
-    const bool last_of_group = lane == 63 || (nk >> 6) != kh;
-    const bool real = kh != 0x3ffffff;
-    uint64_t prevpos = 0;  // +1 encoded
+    const uint32_t mypos = b0 + (key & 63);
+    const uint32_t pk = __shfl_up(key, 1, 64), nk = __shfl_down(key, 1, 64);
+    const bool first = lane == 0 || (pk >> 6) != kh;
+    const bool last = lane == 63 || (nk >> 6) != kh;
+    const bool real = kh != 0x3ffffffu;
+    // rank inside the group = lane - (lane of the group's first member)
+    const uint64_t fm = __ballot(first);
+    const uint64_t below = fm & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+    const uint32_t gstart = 63 - (uint32_t)__clzll((long long)below);
+    uint32_t a = 0, bs = 0;
+    if (real) { a = cnt[kh]; bs = base[kh]; }
+    const uint32_t r = a + (uint32_t)lane - gstart;
     if (real) {
-      if (first_of_group) prevpos = head[kh];
-      else prevpos = base + (pk & 63) + 1;
-      uint64_t d = prevpos ? mypos - (prevpos - 1) : 0;
-      out[mypos] = (uint16_t)(d && d <= 32768 ? (d == 32768 ? 32768 : d) : 0);
-    } else if (mypos < n) {
-      out[mypos] = 0;
+      sidx[mypos] = bs + r;
+      bpos[bs + r] = mypos | (r == 0 ? BUCKET_FIRST : 0u);
     }
-    // head updates after all loads of this batch (loads above read the pre-batch heads); the
-    // workgroup-scope acq_rel fences order this wave's HBM store -> later load of another lane
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    if (real && last_of_group) head[kh] = (uint32_t)(mypos + 1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // all loads of cnt before the updates
+    if (real && last) cnt[kh] = r + 1;
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   }
 }
@@ -157,64 +183,71 @@ __global__ __launch_bounds__(64) void k_chains(const uint8_t* __restrict__ infl,
 // n - p, which break at nice_match first.
 static constexpr uint32_t HOLE_SLOTS_M = 2048;   // == HOLE_SLOTS (fast-level hash slots)
 
-__global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl, const uint16_t* __restrict__ chains,
+__global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl, const uint32_t* __restrict__ chains,
                                               uint2* __restrict__ R, const MatchJob* __restrict__ jobs) {
   const MatchJob jb = jobs[blockIdx.x];
   const uint8_t* in = infl + jb.infl_off;
-  const uint16_t* ch = chains + jb.chain_off;
+  const uint32_t n = (uint32_t)jb.n, npad = (n + 63) & ~63u;
+  const uint32_t* sidx = chains + jb.chain_off;
+  const uint32_t* bpos = sidx + npad;
   uint2* r = R + jb.r_off;
   const uint32_t B = c_cfg[jb.level][3], nice = c_cfg[jb.level][2], Bq = B >> 2;
-  const uint64_t n = jb.n, maxdist = (1u << jb.window) - 262;
+  const uint32_t maxdist = (1u << jb.window) - 262;
   const uint32_t hbits = jb.memlevel + 7u, hmask = (1u << hbits) - 1u, hshift = (hbits + 2u) / 3u;
-  for (uint64_t p = jb.p0 + threadIdx.x; p < jb.p1; p += 256) {
+  for (uint32_t p = (uint32_t)jb.p0 + threadIdx.x; p < (uint32_t)jb.p1; p += 256) {
     uint32_t bf = 2, df = 0, bq = 2, dq = 0, valid = 0, slot = 0, budget_out = 0;
-    uint64_t reach = p;
+    uint32_t reach = p;
     const uint32_t s0 = in[p];
     if (p + 3 <= n) {
       const uint32_t s1 = in[p + 1];
       slot = (((s0 << (2 * hshift)) ^ (s1 << hshift) ^ (uint32_t)in[p + 2]) & hmask) & (HOLE_SLOTS_M - 1);
-      const uint32_t d = ch[p];
-      const uint64_t lim = p > maxdist ? p - maxdist : 0;   // walk continues to q only if q > lim
-      const uint64_t cur0 = p - d;
-      uint64_t cur = cur0;
-      if (d && d <= p && cur0 >= 1 && cur0 + maxdist >= p) {  // hash_head valid
-        valid = 1;
-        const uint64_t left = n - p;
-        const uint32_t cap = left < 258 ? (uint32_t)left : 258u;
-        const uint32_t nn = nice < cap ? nice : cap;
-        for (uint32_t i = 0;;) {
-          reach = cur;
-          // quick reject (bf < nn <= cap, so every read is inside the input)
-          if (in[cur + bf] == in[p + bf] && in[cur + bf - 1] == in[p + bf - 1] && in[cur] == s0 &&
-              in[cur + 1] == s1) {
-            uint32_t len = 2;
-            while (len < cap && in[cur + len] == in[p + len]) len++;
-            if (len > bf) {
-              bf = len; df = (uint32_t)(p - cur);
-              if (i < Bq) { bq = len; dq = df; }
-              if (len >= nn) break;
+      const uint32_t lim = p > maxdist ? p - maxdist : 0u;   // walk continues to q only if q > lim
+      uint32_t idx = sidx[p];
+      uint32_t e = bpos[idx];
+      if (!(e & BUCKET_FIRST)) {
+        e = bpos[--idx];
+        uint32_t cur = e & ~BUCKET_FIRST;
+        if (cur >= 1 && cur + maxdist >= p) {                 // hash_head valid
+          valid = 1;
+          const uint32_t left = n - p;
+          const uint32_t cap = left < 258 ? left : 258u;
+          const uint32_t nn = nice < cap ? nice : cap;
+          for (uint32_t i = 0;;) {
+            reach = cur;
+            const bool more = !(e & BUCKET_FIRST);
+            const uint32_t en = more ? bpos[idx - 1] : 0u;    // next node, loaded ahead of the compare
+            // quick reject (bf < nn <= cap, so every read is inside the input)
+            if (in[cur + bf] == in[p + bf] && in[cur + bf - 1] == in[p + bf - 1] && in[cur] == s0 &&
+                in[cur + 1] == s1) {
+              uint32_t len = 2;
+              while (len < cap && in[cur + len] == in[p + len]) len++;
+              if (len > bf) {
+                bf = len; df = p - cur;
+                if (i < Bq) { bq = len; dq = df; }
+                if (len >= nn) break;
+              }
             }
+            if (++i == B) {   // budget spent: only here can skipped positions let deflate_fast see more nodes
+              budget_out = (more && (en & ~BUCKET_FIRST) > lim) ? 1u : 0u;
+              break;
+            }
+            if (!more) break;
+            e = en;
+            idx--;
+            cur = e & ~BUCKET_FIRST;
+            if (cur <= lim) break;
           }
-          if (++i == B) {   // budget spent: only here can skipped positions let deflate_fast see more nodes
-            const uint32_t dd = ch[cur];
-            budget_out = (dd && cur >= dd && cur - dd > lim) ? 1u : 0u;
-            break;
-          }
-          const uint32_t dd = ch[cur];
-          if (!dd || cur < dd) break;
-          cur -= dd;
-          if (cur <= lim) break;
         }
       }
     }
     // .x = len_full:9 | dist_full:15 | input byte:8
     // .y = slow: len_quarter:9 | dist_quarter:15 | 0:7 | head valid:1
     //      fast: (p - lowest visited node):16 | 0:3 | budget spent with nodes left:1 | hash slot:11 | head valid:1
-    uint2 e;
-    e.x = (bf > 2 ? (bf << 23) | (df << 8) : 0u) | s0;
-    if (jb.fast) e.y = ((uint32_t)(p - reach) << 16) | (budget_out << 12) | (slot << 1) | valid;
-    else e.y = (bq > 2 ? (bq << 23) | (dq << 8) : 0u) | valid;
-    r[p] = e;
+    uint2 o;
+    o.x = (bf > 2 ? (bf << 23) | (df << 8) : 0u) | s0;
+    if (jb.fast) o.y = ((p - reach) << 16) | (budget_out << 12) | (slot << 1) | valid;
+    else o.y = (bq > 2 ? (bq << 23) | (dq << 8) : 0u) | valid;
+    r[p] = o;
   }
 }
 
@@ -265,15 +298,15 @@ struct TrialShared {
 
 struct TrialSharedFast {
   TrialShared t;
+  uint32_t ins[BITMAP_BITS / 32];   // insertion ring (InsRing)
   uint32_t holes[HOLE_SLOTS];   // position + 1 of the latest non-inserted position with hash & (SLOTS-1)
 };
 
 struct SweepArgs {
   const uint8_t* file;          // original compressed bytes
   const uint8_t* infl;          // inflated bytes
-  const uint16_t* chains;       // chain links
+  const uint32_t* chains;       // hash buckets (k_buckets)
   const uint2* R;               // match tables (k_match)
-  uint32_t* ins;                // fast levels: per-trial insertion rings (Trial::ins_off)
   const StreamDev* streams;
   const Trial* trials;
   TrialRes* res;
@@ -723,10 +756,9 @@ __device__ inline uint32_t common_len(const uint8_t* in, uint64_t a, uint64_t b,
 }
 
 // deflate_fast insertion state: positions >= w0 live in a uniform 64-bit mask, older ones in a
-// 65536-bit ring in HBM written one whole word per 32 positions (plain stores, no atomics).  The
-// ring is read back only with wave-uniform loads, i.e. by the lane that wrote it.
+// 65536-bit ring in LDS written one whole word per 32 positions.
 struct InsRing {
-  uint32_t* ring;
+  LDS uint32_t* ring;
   uint32_t w0;     // multiple of 32
   uint64_t mask;   // bit k: position w0 + k inserted
   __device__ __forceinline__ void set(uint32_t q) { mask |= 1ull << (q - w0); }
@@ -737,63 +769,11 @@ struct InsRing {
       w0 += 32;
     }
   }
-  __device__ __forceinline__ bool get(uint32_t q) const {
+  __device__ __forceinline__ bool get(uint32_t q) const {   // per lane (q may differ between lanes)
     if (q >= w0) return (mask >> (q - w0)) & 1;
-    const uint32_t w = uni(ring[(q >> 5) & (BITMAP_BITS / 32 - 1)]);
-    return (w >> (q & 31)) & 1;
+    return (ring[(q >> 5) & (BITMAP_BITS / 32 - 1)] >> (q & 31)) & 1;
   }
 };
-
-template <int KIND>
-__device__ __forceinline__ bool is_inserted(const InsRing* ins, uint32_t q) {
-  if constexpr (KIND != 1) return true;
-  else return ins->get(q);
-}
-
-// longest_match on the shared chains (Z/deflate.c:1148-1289).  Returns match length; sets z.match_start.
-template <int KIND>
-__device__ __forceinline__ uint32_t longest_match(Lz& z, const uint8_t* in, const uint16_t* ch, const InsRing* ins,
-                                  uint32_t cur, int lane) {
-  uint32_t chain = z.chain;
-  const uint32_t p = z.p;
-  uint32_t best = z.prev_length;
-  uint32_t nice = z.nice;
-  if (z.prev_length >= z.good) chain >>= 2;
-  if (nice > z.lookahead) nice = (uint32_t)z.lookahead;
-  // continue while next > limit (window limit translated to absolute positions)
-  const uint32_t sw = p - z.S;
-  const uint32_t limit = sw > z.maxdist ? p - z.maxdist : z.S;
-  const uint32_t avail = z.n - p;                       // bytes left in the input
-  const uint32_t cap = avail < 258 ? (uint32_t)avail : 258u;
-  for (;;) {
-    // quick reject: match[best], match[best-1], match[0], match[1] (bytes past the input read as 0)
-    uint8_t se0 = p + best < z.n ? in[p + best] : 0;
-    uint8_t se1 = p + best - 1 < z.n ? in[p + best - 1] : 0;
-    uint8_t m0 = cur + best < z.n ? in[cur + best] : 0;
-    uint8_t m1 = cur + best - 1 < z.n ? in[cur + best - 1] : 0;
-    if (uni((uint32_t)(m0 == se0 && m1 == se1 && in[cur] == in[p] && in[cur + 1] == in[p + 1]))) {
-      uint32_t len = uni(common_len(in, cur, p, 2, cap, lane));
-      if (len > best) {
-        z.match_start = cur;
-        best = len;
-        if (len >= nice) break;
-      }
-    }
-    // next link on the chain (skipping positions deflate_fast did not insert)
-    uint32_t nx = cur;
-    bool stop = false;
-    for (;;) {
-      uint32_t d = uni((uint32_t)ch[nx]);
-      if (!d || nx < d) { stop = true; break; }
-      nx -= d;
-      if (nx <= limit) { stop = true; break; }
-      if (uni((uint32_t)is_inserted<KIND>(ins, nx))) break;
-    }
-    if (stop || --chain == 0) break;
-    cur = nx;
-  }
-  return best <= z.lookahead ? best : (uint32_t)z.lookahead;
-}
 
 // _tr_flush_block (Z/trees.c:907-1004) + FLUSH_BLOCK_ONLY bookkeeping
 // The parse state is passed by value so that it never leaves registers (a reference to it here
@@ -911,11 +891,14 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   const Trial tr = A.trials[t];
   const StreamDev sd = A.streams[tr.stream];
   const uint8_t* in = A.infl + sd.infl_off;
-  const uint16_t* ch = KIND == 0 ? nullptr : A.chains + tr.chain_off;
-  InsRing insr;   // fast levels: insertion state (read only by the exact chain walk)
-  insr.ring = KIND == 1 ? A.ins + tr.ins_off : nullptr;
+  // hash buckets of (stream, memLevel): sidx[npad] then bpos[npad]
+  const uint32_t npad = (sd.infl_len + 63) & ~63ull;
+  const uint32_t* sidx = KIND == 0 ? nullptr : A.chains + tr.chain_off;
+  const uint32_t* bpos = KIND == 0 ? nullptr : sidx + npad;
+  InsRing insr;   // fast levels: insertion state
+  if constexpr (KIND == 1) insr.ring = (LDS uint32_t*)shm.ins;
+  else insr.ring = nullptr;
   insr.w0 = 0; insr.mask = 0;
-  const InsRing* ins = &insr;
   const bool full_needed = tr.mode & 1;
   Lz z;
   z.level = tr.clevel; z.kind = KIND;
@@ -995,8 +978,9 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   // possible while p - S <= MAX_DIST (right at a slide); then the chain link is read directly.
   auto head_is_S = [&]() -> bool {
     if (z.S == 0 || z.p - z.S > z.maxdist) return false;
-    const uint32_t d = uni((uint32_t)ch[z.p]);
-    return d && z.p - d == z.S;
+    const uint32_t si = uni(sidx[z.p]);
+    if (uni(bpos[si]) & BUCKET_FIRST) return false;
+    return (uni(bpos[si - 1]) & ~BUCKET_FIRST) == z.S;
   };
   if constexpr (KIND == 0) {
     // deflate_stored (Z/deflate.c:1564-1619)
@@ -1048,7 +1032,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           if ((e.x >> 23) <= 2) exact = true;
           else {
             const uint32_t wpos = z.p - ((e.x >> 8) & 0x7fffu);
-            exact = wpos > z.S && insr.get(wpos);
+            exact = wpos > z.S && uni((uint32_t)insr.get(wpos));
           }
         }
         if (exact) {
@@ -1060,19 +1044,86 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         } else {
           fallbacks++;
           const uint64_t cf0 = STEP_CLOCK();
-          // head[] = most recent inserted same-hash position
-          uint32_t q = z.p, hh = 0;
-          bool hv = false;
-          for (;;) {
-            uint32_t d = uni((uint32_t)ch[q]);
-            if (!d || q < d) break;
-            q -= d;
-            if (z.p - q > z.maxdist) break;
-            if (uni((uint32_t)is_inserted<1>(ins, q))) { hh = q; hv = q > z.S; break; }
+          // Exact deflate_fast longest_match over the INSERTED same-hash positions
+          // (Z/deflate.c:1148-1289): 64 bucket entries per step, lanes test insertion and compare
+          // bytes in parallel; the walk order is the lane order.
+          const uint32_t si = uni(sidx[z.p]);
+          bool done = (uni(bpos[si]) & BUCKET_FIRST) != 0;   // first of its bucket: no chain
+          bool head_done = false, hv = false, won = false;
+          uint32_t examined = 0, best = 2, win = 0;
+          const uint32_t limit = z.p > z.maxdist ? z.p - z.maxdist : 0u;   // later nodes only while > limit
+          const uint32_t cap = z.n - z.p < 258u ? z.n - z.p : 258u;
+          const uint32_t nicec = z.nice < z.lookahead ? z.nice : z.lookahead;   // <= cap
+          const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+          int32_t top = (int32_t)si - 1;
+          while (!done) {
+            const int32_t k = top - lane;
+            const uint32_t e = k >= 0 ? bpos[k] : BUCKET_FIRST;
+            const uint64_t fm = __ballot((e & BUCKET_FIRST) != 0);
+            const int flane = fm ? __ffsll((unsigned long long)fm) - 1 : 64;   // bucket's first entry: last node
+            const uint32_t q = e & ~BUCKET_FIRST;
+            const bool ins = lane <= flane && k >= 0 && insr.get(q);
+            const uint64_t im = __ballot(ins);
+            int head_lane = -1, from = 0;
+            if (!head_done) {
+              if (!im) {   // no inserted node in this chunk yet
+                if (flane < 64) break;
+                top -= 64;
+                continue;
+              }
+              head_lane = __ffsll((unsigned long long)im) - 1;
+              const uint32_t hh = (uint32_t)__builtin_amdgcn_readlane((int)q, head_lane);
+              head_done = true;
+              hv = hh > z.S && z.p - hh <= z.maxdist;   // zlib calls longest_match only then
+              if (!hv) break;
+              from = head_lane;
+            }
+            // the walk stops at the first inserted node <= limit (the head is always examined)
+            const uint64_t sm = __ballot(ins && lane >= from && lane != head_lane && q <= limit);
+            const int slane = sm ? __ffsll((unsigned long long)sm) - 1 : 64;
+            bool cand = ins && lane >= from && lane < slane;
+            const uint32_t room = z.chain - examined;
+            cand = cand && (uint32_t)__popcll(__ballot(cand) & lt) < room;
+            const uint64_t cm = __ballot(cand);
+            examined += (uint32_t)__popcll(cm);
+            // match lengths capped at nice (8 bytes per round trip); the first candidate reaching
+            // nice ends the walk, so capped lengths decide the winner
+            uint32_t len = 0;
+            bool go = cand;
+            while (__ballot(go)) {
+              if (go) {
+                uint32_t m = 0;
+#pragma unroll
+                for (int j = 0; j < 8; j++) m |= (in[q + len + j] == in[z.p + len + j] ? 1u : 0u) << j;
+                const uint32_t run = (uint32_t)__builtin_ctz(~m);   // matching prefix of the 8
+                const uint32_t left = nicec - len;
+                len += run < left ? run : left;
+                go = run == 8 && len < nicec;
+              }
+            }
+            const uint64_t nm = __ballot(cand && len >= nicec);
+            if (nm) {
+              const int wl = __ffsll((unsigned long long)nm) - 1;
+              win = (uint32_t)__builtin_amdgcn_readlane((int)q, wl);
+              best = uni(common_len(in, win, z.p, nicec, cap, lane));   // full length of the winner
+              won = true;
+              break;
+            }
+            uint32_t mx = cand ? len : 0u;
+            for (int d = 32; d >= 1; d >>= 1) { const uint32_t o = __shfl_xor(mx, d, 64); mx = mx > o ? mx : o; }
+            mx = uni(mx);
+            if (mx > best) {
+              const uint64_t xm = __ballot(cand && len == mx);
+              win = (uint32_t)__builtin_amdgcn_readlane((int)q, __ffsll((unsigned long long)xm) - 1);
+              best = mx;
+              won = true;
+            }
+            done = examined >= z.chain || slane < 64 || flane < 64;
+            top -= 64;
           }
-          if (hv && z.p - hh <= z.maxdist) {
-            z.match_length = uni(longest_match<1>(z, in, ch, ins, hh, lane));
-            z.match_start = uni(z.match_start);
+          if (hv) {
+            z.match_length = best <= z.lookahead ? best : z.lookahead;
+            if (won) z.match_start = win;
           }
           cyc_fb += STEP_CLOCK() - cf0;
         }
