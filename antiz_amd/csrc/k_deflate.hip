@@ -183,10 +183,36 @@ __global__ __launch_bounds__(64) void k_buckets(const uint8_t* __restrict__ infl
 // n - p, which break at nice_match first.
 static constexpr uint32_t HOLE_SLOTS_M = 2048;   // == HOLE_SLOTS (fast-level hash slots)
 
+// 16 bytes at byte offset x of a 4-byte aligned buffer: 5 aligned dword loads (independent, one
+// round trip) joined with v_alignbyte.  Reads up to 4 bytes past x + 16 (buffers carry slack).
+__device__ __forceinline__ void load16(const uint32_t* in32, uint32_t x, uint32_t v[4]) {
+  const uint32_t w = x >> 2, sh = x & 3;
+  const uint32_t a0 = in32[w], a1 = in32[w + 1], a2 = in32[w + 2], a3 = in32[w + 3], a4 = in32[w + 4];
+  v[0] = __builtin_amdgcn_alignbyte(a1, a0, sh);
+  v[1] = __builtin_amdgcn_alignbyte(a2, a1, sh);
+  v[2] = __builtin_amdgcn_alignbyte(a3, a2, sh);
+  v[3] = __builtin_amdgcn_alignbyte(a4, a3, sh);
+}
+// number of equal leading bytes (0..16) of the 16 bytes at a and at b (pb: b's bytes if preloaded)
+__device__ __forceinline__ uint32_t match16(const uint32_t* in32, uint32_t a, uint32_t b, const uint32_t* pb,
+                                            int) {
+  uint32_t va[4], vb[4];
+  load16(in32, a, va);
+  if (pb) { vb[0] = pb[0]; vb[1] = pb[1]; vb[2] = pb[2]; vb[3] = pb[3]; }
+  else load16(in32, b, vb);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t x = va[k] ^ vb[k];
+    if (x) return 4 * k + ((uint32_t)__builtin_ctz(x) >> 3);
+  }
+  return 16;
+}
+
 __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl, const uint32_t* __restrict__ chains,
                                               uint2* __restrict__ R, const MatchJob* __restrict__ jobs) {
   const MatchJob jb = jobs[blockIdx.x];
   const uint8_t* in = infl + jb.infl_off;
+  const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);   // stream bases are 256-byte aligned
   const uint32_t n = (uint32_t)jb.n, npad = (n + 63) & ~63u;
   const uint32_t* sidx = chains + jb.chain_off;
   const uint32_t* bpos = sidx + npad;
@@ -212,20 +238,26 @@ __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl,
           const uint32_t left = n - p;
           const uint32_t cap = left < 258 ? left : 258u;
           const uint32_t nn = nice < cap ? nice : cap;
+          uint32_t pv[4];
+          load16(in32, p, pv);
           for (uint32_t i = 0;;) {
             reach = cur;
             const bool more = !(e & BUCKET_FIRST);
             const uint32_t en = more ? bpos[idx - 1] : 0u;    // next node, loaded ahead of the compare
-            // quick reject (bf < nn <= cap, so every read is inside the input)
-            if (in[cur + bf] == in[p + bf] && in[cur + bf - 1] == in[p + bf - 1] && in[cur] == s0 &&
-                in[cur + 1] == s1) {
-              uint32_t len = 2;
-              while (len < cap && in[cur + len] == in[p + len]) len++;
-              if (len > bf) {
-                bf = len; df = p - cur;
-                if (i < Bq) { bq = len; dq = df; }
-                if (len >= nn) break;
+            // exact common length, 16 bytes per round trip (any candidate that could beat bf gets
+            // its exact length; zlib's quick reject only skips candidates that cannot)
+            uint32_t len = match16(in32, cur, p, pv, 0);
+            if (len == 16)
+              while (len < cap) {
+                const uint32_t l2 = match16(in32, cur + len, p + len, nullptr, 0);
+                len += l2;
+                if (l2 < 16) break;
               }
+            if (len > cap) len = cap;
+            if (len > bf) {
+              bf = len; df = p - cur;
+              if (i < Bq) { bq = len; dq = df; }
+              if (len >= nn) break;
             }
             if (++i == B) {   // budget spent: only here can skipped positions let deflate_fast see more nodes
               budget_out = (more && (en & ~BUCKET_FIRST) > lim) ? 1u : 0u;
