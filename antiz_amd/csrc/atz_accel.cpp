@@ -715,20 +715,18 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
     c->d_chains.p = np;
     c->d_chains.n = cap;
   }
-  const size_t batch = 1024;   // scratch: 2 x 65536 words per job
-  if (int r = c->d_heads.reserve(batch * 131072 * 4)) return r;
-  for (size_t b0 = 0; b0 < jobs.size(); b0 += batch) {
+  const size_t batch = 4096;   // scratch: 65536 x 8-byte words per job slot
+  if (int r = c->d_heads.reserve(batch * 65536 * 8)) return r;
+  for (size_t k = 0; k < jobs.size(); k++) jobs[k].slot = (uint32_t)(k % batch);
+  if (int r = upload(c, c->d_cjobs, jobs.data(), jobs.size() * sizeof(ChainJob))) return r;
+  for (size_t b0 = 0; b0 < jobs.size(); b0 += batch) {   // launches on one stream reuse the slots in order
     size_t nb = std::min(batch, jobs.size() - b0);
-    for (size_t k = 0; k < nb; k++) jobs[b0 + k].slot = (uint32_t)k;
-    if (int r = upload(c, c->d_cjobs, jobs.data() + b0, nb * sizeof(ChainJob))) return r;
     kbeg(c, 2);
     hipLaunchKernelGGL(k_buckets, dim3((uint32_t)nb), dim3(64), 0, c->st, c->d_infl.as<uint8_t>(),
-                       c->d_cjobs.as<ChainJob>(), c->d_chains.as<uint32_t>(), c->d_heads.as<uint32_t>(),
+                       c->d_cjobs.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), c->d_heads.as<uint64_t>(),
                        (uint32_t)nb);
     kend(c);
     KCHECK("k_buckets");
-    HIPCHK(hipStreamSynchronize(c->st));
-    kcollect(c);
     for (size_t k = 0; k < nb; k++) c->stats.k_chains_alg_bytes += 9 * jobs[b0 + k].n;  // read I_s, write 8*I_s
   }
   return 0;
@@ -854,8 +852,10 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
   return 0;
 }
 
+static double g_t_list = 0, g_t_chains = 0, g_t_trials = 0, g_t_apply = 0;
 static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
   auto t0 = std::chrono::steady_clock::now();
+  g_t_list = g_t_chains = g_t_trials = g_t_apply = 0;
   const size_t n = c->recs.size();
   ss.assign(n, StreamState());
   c->chain_off.assign(n, {});
@@ -909,12 +909,18 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
         tr[kind].push_back(t);
       }
     }
+    auto ta = std::chrono::steady_clock::now();
     if (int r = ensure_chains(c, need)) return r;
+    HIPCHK(hipStreamSynchronize(c->st));
+    auto tb = std::chrono::steady_clock::now();
     for (int k = 1; k < 3; k++)
       for (Trial& t : tr[k]) t.chain_off = c->chain_off[t.stream][t.memlevel];
     if (int r = c->d_out.reserve(out_tot + 4096)) return r;
     if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
     if (int r = run_trials(c, d_file, tr, so, trres)) return r;
+    auto tc = std::chrono::steady_clock::now();
+    g_t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
+    g_t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
     for (int k = 0; k < 3; k++)
       for (size_t q = 0; q < tr[k].size(); q++) {
         const TrialRes& r = trres[k][q];
@@ -1028,7 +1034,11 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
     std::vector<uint32_t> next;
     for (uint32_t s : active) if (ss[s].phase != 2) next.push_back(s);
     active.swap(next);
+    g_t_apply += ms_since(tc);
   }
+  if (timing_on())
+    std::fprintf(stderr, "atz: sweep host: chains %.1f ms (incl. kernels), trials %.1f ms (incl. kernels), apply %.1f ms, total %.1f ms\n",
+                 g_t_chains, g_t_trials, g_t_apply, ms_since(t0));
   for (size_t s = 0; s < n; s++) {
     StreamState& st = ss[s];
     const uint64_t C = c->recs[s].comp_len;

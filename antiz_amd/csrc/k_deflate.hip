@@ -97,7 +97,7 @@ struct ChainJob {
 static constexpr uint32_t BUCKET_FIRST = 0x80000000u;
 
 __global__ __launch_bounds__(64) void k_buckets(const uint8_t* __restrict__ infl, const ChainJob* __restrict__ jobs,
-                                               uint32_t* __restrict__ chains, uint32_t* __restrict__ scratch,
+                                               uint32_t* __restrict__ chains, uint64_t* __restrict__ scratch,
                                                uint32_t njobs) {
   const uint32_t j = blockIdx.x;
   if (j >= njobs) return;
@@ -109,34 +109,43 @@ __global__ __launch_bounds__(64) void k_buckets(const uint8_t* __restrict__ infl
   uint32_t* sidx = chains + jb.chain_off;
   uint32_t* bpos = sidx + npad;
   const uint32_t hbits = jb.memlevel + 7, hsize = 1u << hbits, hmask = hsize - 1, hshift = (hbits + 2) / 3;
-  uint32_t* cnt = scratch + (uint64_t)jb.slot * 131072;   // per hash: count, then "assigned so far"
-  uint32_t* base = cnt + 65536;                            // per hash: first index in bpos
-  for (uint32_t i = lane; i < hsize; i += 64) cnt[i] = 0;
+  // per hash one 64-bit word: count during the histogram, then (first index << 32) | assigned
+  uint64_t* word = scratch + (uint64_t)jb.slot * 65536;
+  for (uint32_t i = lane; i < hsize; i += 64) word[i] = 0;
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   const uint32_t nh = n >= 3 ? n - 2 : 0;                 // positions with a hash (p + 3 <= n)
   auto hash = [&](uint32_t p) -> uint32_t {
     return (((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask;
   };
-  for (uint32_t p = lane; p < nh; p += 64) atomicAdd(&cnt[hash(p)], 1u);
+  for (uint32_t p = lane; p < nh; p += 64) atomicAdd((unsigned long long*)&word[hash(p)], 1ull);
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-  // exclusive scan of the counts
+  // exclusive scan of the counts -> first index of each bucket (8 chunks of loads in flight)
   uint32_t run = 0;
-  for (uint32_t g = 0; g < hsize; g += 64) {
-    const uint32_t c = cnt[g + lane];
-    uint32_t incl = c;
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t t = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += t;
+  for (uint32_t g0 = 0; g0 < hsize; g0 += 512) {
+    uint32_t c[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) c[u] = g0 + 64 * u < hsize ? (uint32_t)word[g0 + 64 * u + lane] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if (g0 + 64 * u >= hsize) break;
+      uint32_t incl = c[u];
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += t;
+      }
+      word[g0 + 64 * u + lane] = (uint64_t)(run + incl - c[u]) << 32;
+      run += __shfl(incl, 63, 64);
     }
-    base[g + lane] = run + incl - c;
-    cnt[g + lane] = 0;
-    run += __shfl(incl, 63, 64);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-  // assignment in position order: 64 positions at a time, bitonic-sorted by (hash, lane)
+  // assignment in position order: 64 positions at a time, bitonic-sorted by (hash, lane); one
+  // returning atomic per group gives (first index, assigned so far) -- same-address atomics of
+  // one wave complete in issue order, so no fence is needed between batches
+  uint32_t hn = lane < (int)nh ? hash((uint32_t)lane) : 0x3ffffffu;   // next batch's hashes, loaded ahead
   for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
-    const uint32_t p = b0 + lane;
-    const uint32_t h = p < nh ? hash(p) : 0x3ffffffu;
+    const uint32_t h = hn;
+    const uint32_t pn = b0 + 64 + lane;
+    hn = pn < nh ? hash(pn) : 0x3ffffffu;
     uint32_t key = (h << 6) | (uint32_t)lane;
     for (int k = 2; k <= 64; k <<= 1)
       for (int st = k >> 1; st > 0; st >>= 1) {
@@ -151,20 +160,20 @@ __global__ __launch_bounds__(64) void k_buckets(const uint8_t* __restrict__ infl
     const bool first = lane == 0 || (pk >> 6) != kh;
     const bool last = lane == 63 || (nk >> 6) != kh;
     const bool real = kh != 0x3ffffffu;
-    // rank inside the group = lane - (lane of the group's first member)
     const uint64_t fm = __ballot(first);
     const uint64_t below = fm & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
     const uint32_t gstart = 63 - (uint32_t)__clzll((long long)below);
-    uint32_t a = 0, bs = 0;
-    if (real) { a = cnt[kh]; bs = base[kh]; }
-    const uint32_t r = a + (uint32_t)lane - gstart;
+    const uint64_t lm = __ballot(last);
+    const uint64_t above = lm & (~0ull << lane);
+    const uint32_t gend = (uint32_t)__ffsll((unsigned long long)above) - 1;
+    uint64_t old = 0;
+    if (real && first) old = atomicAdd((unsigned long long*)&word[kh], (unsigned long long)(gend - gstart + 1));
+    const uint32_t olo = __shfl((uint32_t)old, (int)gstart, 64), ohi = __shfl((uint32_t)(old >> 32), (int)gstart, 64);
     if (real) {
-      sidx[mypos] = bs + r;
-      bpos[bs + r] = mypos | (r == 0 ? BUCKET_FIRST : 0u);
+      const uint32_t r = olo + (uint32_t)lane - gstart;
+      sidx[mypos] = ohi + r;
+      bpos[ohi + r] = mypos | (r == 0 ? BUCKET_FIRST : 0u);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // all loads of cnt before the updates
-    if (real && last) cnt[kh] = r + 1;
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   }
 }
 
