@@ -96,9 +96,13 @@ __global__ __launch_bounds__(64) void k_diffs(const uint8_t* __restrict__ out, c
     }                                                                 \
   } while (0)
 
-struct DBuf {
+struct DBuf {              // device buffer, freed with its owner (atz_close deletes the context)
   void* p = nullptr;
   size_t n = 0;
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  ~DBuf() { release(); }
   int reserve(size_t need) {
     if (need <= n) return 0;
     if (p) hipFree(p);
@@ -236,7 +240,7 @@ struct atz_ctx {
   hipStream_t st = nullptr;
   DBuf d_file, d_pos, d_cnt, d_jobs, d_res, d_virt, d_infl, d_chains, d_heads, d_streams, d_trials,
       d_tres, d_out, d_syms, d_adler, d_meta, d_segs, d_atz, d_diffjobs, d_diffpos, d_diffval, d_diffcnt,
-      d_cjobs, d_tmp, d_R, d_mjobs, d_ins, d_arena, d_arena_used;
+      d_cjobs, d_cjobs2, d_tmp, d_R, d_mjobs, d_ins, d_arena, d_arena_used;
   // last scan
   std::vector<Rec> recs;
   std::vector<uint64_t> infl_off;   // per record offset in d_infl
@@ -715,20 +719,32 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
     c->d_chains.p = np;
     c->d_chains.n = cap;
   }
+  // small hash tables (memLevel <= 7) and streams < 64 Ki positions: LDS kernel; the rest: HBM scratch
+  std::vector<ChainJob> small, big;
+  for (const ChainJob& jb : jobs)
+    ((1u << (jb.memlevel + 7)) <= BK_LDS_HASH && jb.n < 65536 ? small : big).push_back(jb);
+  if (!small.empty()) {
+    if (int r = upload(c, c->d_cjobs2, small.data(), small.size() * sizeof(ChainJob))) return r;
+    kbeg(c, 2);
+    hipLaunchKernelGGL(k_buckets_lds, dim3((uint32_t)small.size()), dim3(256), 0, c->st, c->d_infl.as<uint8_t>(),
+                       c->d_cjobs2.as<ChainJob>(), c->d_chains.as<uint32_t>(), (uint32_t)small.size());
+    kend(c);
+    KCHECK("k_buckets_lds");
+  }
   const size_t batch = 4096;   // scratch: 65536 x 8-byte words per job slot
-  if (int r = c->d_heads.reserve(batch * 65536 * 8)) return r;
-  for (size_t k = 0; k < jobs.size(); k++) jobs[k].slot = (uint32_t)(k % batch);
-  if (int r = upload(c, c->d_cjobs, jobs.data(), jobs.size() * sizeof(ChainJob))) return r;
-  for (size_t b0 = 0; b0 < jobs.size(); b0 += batch) {   // launches on one stream reuse the slots in order
-    size_t nb = std::min(batch, jobs.size() - b0);
+  if (!big.empty() && (int)c->d_heads.reserve(batch * 65536 * 8)) return ATZ_E_NOMEM;
+  for (size_t k = 0; k < big.size(); k++) big[k].slot = (uint32_t)(k % batch);
+  if (int r = upload(c, c->d_cjobs, big.data(), big.size() * sizeof(ChainJob))) return r;
+  for (size_t b0 = 0; b0 < big.size(); b0 += batch) {   // launches on one stream reuse the slots in order
+    size_t nb = std::min(batch, big.size() - b0);
     kbeg(c, 2);
     hipLaunchKernelGGL(k_buckets, dim3((uint32_t)nb), dim3(64), 0, c->st, c->d_infl.as<uint8_t>(),
                        c->d_cjobs.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), c->d_heads.as<uint64_t>(),
                        (uint32_t)nb);
     kend(c);
     KCHECK("k_buckets");
-    for (size_t k = 0; k < nb; k++) c->stats.k_chains_alg_bytes += 9 * jobs[b0 + k].n;  // read I_s, write 8*I_s
   }
+  for (const ChainJob& jb : jobs) c->stats.k_chains_alg_bytes += 9 * jb.n;  // read I_s, write 8*I_s
   return 0;
 }
 
@@ -1263,13 +1279,8 @@ int atz_open(atz_ctx_t** ctx, const atz_opts_t* opts) {
 void atz_close(atz_ctx_t* c) {
   if (!c) return;
   hipStreamSynchronize(c->st);
-  for (DBuf* b : {&c->d_file, &c->d_pos, &c->d_cnt, &c->d_jobs, &c->d_res, &c->d_virt, &c->d_infl, &c->d_chains,
-                  &c->d_heads, &c->d_streams, &c->d_trials, &c->d_tres, &c->d_out, &c->d_syms, &c->d_adler,
-                  &c->d_meta, &c->d_segs, &c->d_atz, &c->d_diffjobs, &c->d_diffpos, &c->d_diffval, &c->d_diffcnt,
-                  &c->d_cjobs, &c->d_tmp})
-    b->release();
   hipStreamDestroy(c->st);
-  delete c;
+  delete c;   // every DBuf member frees its device memory
 }
 
 int atz_scan(atz_ctx_t* c, const uint8_t* file, uint64_t len, atz_cand_t** out, uint64_t* n) {

@@ -177,6 +177,91 @@ __global__ __launch_bounds__(64) void k_buckets(const uint8_t* __restrict__ infl
   }
 }
 
+// LDS variant for hash tables of <= 16384 entries and streams < 65536 positions: one workgroup
+// (4 waves) per job, one 32-bit LDS word per hash = (first index << 16) | assigned.  Zeroing, the
+// histogram and the scan use all 256 threads; the in-order assignment runs on wave 0 with LDS
+// atomics (~100-cycle round trips instead of HBM ones).
+static constexpr uint32_t BK_LDS_HASH = 16384;
+__global__ __launch_bounds__(256) void k_buckets_lds(const uint8_t* __restrict__ infl,
+                                                    const ChainJob* __restrict__ jobs,
+                                                    uint32_t* __restrict__ chains, uint32_t njobs) {
+  __shared__ uint32_t word[BK_LDS_HASH];
+  __shared__ uint32_t wsum[4];
+  const uint32_t j = blockIdx.x;
+  if (j >= njobs) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const ChainJob jb = jobs[j];
+  const uint8_t* in = infl + jb.infl_off;
+  const uint32_t n = (uint32_t)jb.n;
+  const uint32_t npad = (n + 63) & ~63u;
+  uint32_t* sidx = chains + jb.chain_off;
+  uint32_t* bpos = sidx + npad;
+  const uint32_t hbits = jb.memlevel + 7, hsize = 1u << hbits, hmask = hsize - 1, hshift = (hbits + 2) / 3;
+  for (uint32_t i = tid; i < hsize; i += 256) word[i] = 0;
+  __syncthreads();
+  const uint32_t nh = n >= 3 ? n - 2 : 0;
+  auto hash = [&](uint32_t p) -> uint32_t {
+    return (((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask;
+  };
+  for (uint32_t p = tid; p < nh; p += 256) atomicAdd(&word[hash(p)], 1u);
+  __syncthreads();
+  // exclusive scan: each wave scans a quarter of the table, then the quarters are offset
+  const uint32_t q = hsize / 4;   // >= 64
+  uint32_t run = 0;
+  for (uint32_t g = wave * q; g < (wave + 1) * q; g += 64) {
+    const uint32_t c = word[g + lane];
+    uint32_t incl = c;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += t;
+    }
+    word[g + lane] = run + incl - c;
+    run += __shfl(incl, 63, 64);
+  }
+  if (lane == 0) wsum[wave] = run;
+  __syncthreads();
+  uint32_t off = 0;
+  for (int w = 0; w < wave; w++) off += wsum[w];
+  for (uint32_t g = wave * q; g < (wave + 1) * q; g += 64) word[g + lane] = (word[g + lane] + off) << 16;
+  __syncthreads();
+  if (wave != 0) return;
+  uint32_t hn = lane < (int)nh ? hash((uint32_t)lane) : 0x3ffffffu;
+  for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
+    const uint32_t h = hn;
+    const uint32_t pn = b0 + 64 + lane;
+    hn = pn < nh ? hash(pn) : 0x3ffffffu;
+    uint32_t key = (h << 6) | (uint32_t)lane;
+    for (int k = 2; k <= 64; k <<= 1)
+      for (int st = k >> 1; st > 0; st >>= 1) {
+        const uint32_t o = __shfl_xor(key, st, 64);
+        const bool up = (lane & k) == 0, lower = (lane & st) == 0;
+        const uint32_t mn = key < o ? key : o, mx = key < o ? o : key;
+        key = (lower == up) ? mn : mx;
+      }
+    const uint32_t kh = key >> 6;
+    const uint32_t mypos = b0 + (key & 63);
+    const uint32_t pk = __shfl_up(key, 1, 64), nk = __shfl_down(key, 1, 64);
+    const bool first = lane == 0 || (pk >> 6) != kh;
+    const bool last = lane == 63 || (nk >> 6) != kh;
+    const bool real = kh != 0x3ffffffu;
+    const uint64_t fm = __ballot(first);
+    const uint64_t below = fm & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+    const uint32_t gstart = 63 - (uint32_t)__clzll((long long)below);
+    const uint64_t lm = __ballot(last);
+    const uint64_t above = lm & (~0ull << lane);
+    const uint32_t gend = (uint32_t)__ffsll((unsigned long long)above) - 1;
+    uint32_t old = 0;
+    if (real && first) old = atomicAdd(&word[kh], gend - gstart + 1);
+    old = __shfl(old, (int)gstart, 64);
+    if (real) {
+      const uint32_t r = (old & 0xffffu) + (uint32_t)lane - gstart;
+      const uint32_t at = (old >> 16) + r;
+      sidx[mypos] = at;
+      bpos[at] = mypos | (r == 0 ? BUCKET_FIRST : 0u);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_match: longest_match (Z/deflate.c:1148-1289) for every position of a trial, lanes = positions.
 //
