@@ -719,17 +719,32 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
     c->d_chains.p = np;
     c->d_chains.n = cap;
   }
-  // small hash tables (memLevel <= 7) and streams < 64 Ki positions: LDS kernel; the rest: HBM scratch
-  std::vector<ChainJob> small, big;
-  for (const ChainJob& jb : jobs)
-    ((1u << (jb.memlevel + 7)) <= BK_LDS_HASH && jb.n < 65536 ? small : big).push_back(jb);
-  if (!small.empty()) {
-    if (int r = upload(c, c->d_cjobs2, small.data(), small.size() * sizeof(ChainJob))) return r;
-    kbeg(c, 2);
-    hipLaunchKernelGGL(k_buckets_lds, dim3((uint32_t)small.size()), dim3(256), 0, c->st, c->d_infl.as<uint8_t>(),
-                       c->d_cjobs2.as<ChainJob>(), c->d_chains.as<uint32_t>(), (uint32_t)small.size());
-    kend(c);
-    KCHECK("k_buckets_lds");
+  // hash tables of memLevel <= 8 and streams < 64 Ki positions: LDS kernels; memLevel 9: HBM scratch
+  std::vector<ChainJob> small, mid, big;
+  for (const ChainJob& jb : jobs) {
+    const uint32_t hs = 1u << (jb.memlevel + 7);
+    (jb.n >= 65536 || hs > 32768 ? big : hs <= 16384 ? small : mid).push_back(jb);
+  }
+  if (!small.empty() || !mid.empty()) {
+    std::vector<ChainJob> both(small);
+    both.insert(both.end(), mid.begin(), mid.end());
+    if (int r = upload(c, c->d_cjobs2, both.data(), both.size() * sizeof(ChainJob))) return r;
+    if (!small.empty()) {
+      kbeg(c, 2);
+      hipLaunchKernelGGL(k_buckets_lds<16384>, dim3((uint32_t)small.size()), dim3(256), 0, c->st,
+                         c->d_infl.as<uint8_t>(), c->d_cjobs2.as<ChainJob>(), c->d_chains.as<uint32_t>(),
+                         (uint32_t)small.size());
+      kend(c);
+      KCHECK("k_buckets_lds<16384>");
+    }
+    if (!mid.empty()) {
+      kbeg(c, 2);
+      hipLaunchKernelGGL(k_buckets_lds<32768>, dim3((uint32_t)mid.size()), dim3(256), 0, c->st,
+                         c->d_infl.as<uint8_t>(), c->d_cjobs2.as<ChainJob>() + small.size(),
+                         c->d_chains.as<uint32_t>(), (uint32_t)mid.size());
+      kend(c);
+      KCHECK("k_buckets_lds<32768>");
+    }
   }
   const size_t batch = 4096;   // scratch: 65536 x 8-byte words per job slot
   if (!big.empty() && (int)c->d_heads.reserve(batch * 65536 * 8)) return ATZ_E_NOMEM;

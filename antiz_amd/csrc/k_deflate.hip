@@ -177,15 +177,15 @@ __global__ __launch_bounds__(64) void k_buckets(const uint8_t* __restrict__ infl
   }
 }
 
-// LDS variant for hash tables of <= 16384 entries and streams < 65536 positions: one workgroup
+// LDS variant for hash tables of <= TABLE (16384 or 32768) entries and streams < 65536 positions: one workgroup
 // (4 waves) per job, one 32-bit LDS word per hash = (first index << 16) | assigned.  Zeroing, the
 // histogram and the scan use all 256 threads; the in-order assignment runs on wave 0 with LDS
 // atomics (~100-cycle round trips instead of HBM ones).
-static constexpr uint32_t BK_LDS_HASH = 16384;
+template <uint32_t TABLE>
 __global__ __launch_bounds__(256) void k_buckets_lds(const uint8_t* __restrict__ infl,
                                                     const ChainJob* __restrict__ jobs,
                                                     uint32_t* __restrict__ chains, uint32_t njobs) {
-  __shared__ uint32_t word[BK_LDS_HASH];
+  __shared__ uint32_t word[TABLE];
   __shared__ uint32_t wsum[4];
   const uint32_t j = blockIdx.x;
   if (j >= njobs) return;
