@@ -240,7 +240,7 @@ struct atz_ctx {
   hipStream_t st = nullptr;
   DBuf d_file, d_pos, d_cnt, d_jobs, d_res, d_virt, d_infl, d_chains, d_heads, d_streams, d_trials,
       d_tres, d_out, d_syms, d_adler, d_meta, d_segs, d_atz, d_diffjobs, d_diffpos, d_diffval, d_diffcnt,
-      d_cjobs, d_cjobs2, d_tmp, d_R, d_mjobs, d_ins, d_arena, d_arena_used;
+      d_cjobs, d_cjobs2, d_cjobs3, d_heads2, d_tmp, d_R, d_mjobs, d_ins, d_arena, d_arena_used;
   // last scan
   std::vector<Rec> recs;
   std::vector<uint64_t> infl_off;   // per record offset in d_infl
@@ -720,30 +720,48 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
     c->d_chains.n = cap;
   }
   // hash tables of memLevel <= 8 and streams < 64 Ki positions: LDS kernels; memLevel 9: HBM scratch
-  std::vector<ChainJob> small, mid, big;
+  std::vector<ChainJob> tiny, small, mid, big;
   for (const ChainJob& jb : jobs) {
     const uint32_t hs = 1u << (jb.memlevel + 7);
-    (jb.n >= 65536 || hs > 32768 ? big : hs <= 16384 ? small : mid).push_back(jb);
+    (jb.n >= 65536 || hs > 32768 ? big : hs <= 4096 ? tiny : hs <= 16384 ? small : mid).push_back(jb);
   }
-  if (!small.empty() || !mid.empty()) {
-    std::vector<ChainJob> both(small);
-    both.insert(both.end(), mid.begin(), mid.end());
-    if (int r = upload(c, c->d_cjobs2, both.data(), both.size() * sizeof(ChainJob))) return r;
-    if (!small.empty()) {
-      kbeg(c, 2);
-      hipLaunchKernelGGL(k_buckets_lds<16384>, dim3((uint32_t)small.size()), dim3(256), 0, c->st,
-                         c->d_infl.as<uint8_t>(), c->d_cjobs2.as<ChainJob>(), c->d_chains.as<uint32_t>(),
-                         (uint32_t)small.size());
-      kend(c);
-      KCHECK("k_buckets_lds<16384>");
+  {
+    std::vector<ChainJob> all(tiny);
+    all.insert(all.end(), small.begin(), small.end());
+    all.insert(all.end(), mid.begin(), mid.end());
+    if (!all.empty()) {
+      if (int r = upload(c, c->d_cjobs2, all.data(), all.size() * sizeof(ChainJob))) return r;
+      const ChainJob* dj = c->d_cjobs2.as<ChainJob>();
+      auto launch = [&](auto kern, size_t off, size_t cnt, const char* nm) -> int {
+        if (!cnt) return 0;
+        kbeg(c, 2);
+        hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(256), 0, c->st, c->d_infl.as<uint8_t>(), dj + off,
+                           c->d_chains.as<uint32_t>(), (uint32_t)cnt);
+        kend(c);
+        KCHECK(nm);
+        return 0;
+      };
+      if (int r = launch(k_buckets_lds<4096>, 0, tiny.size(), "k_buckets_lds<4096>")) return r;
+      if (int r = launch(k_buckets_lds<16384>, tiny.size(), small.size(), "k_buckets_lds<16384>")) return r;
+      if (int r = launch(k_buckets_lds<32768>, tiny.size() + small.size(), mid.size(), "k_buckets_lds<32768>")) return r;
     }
-    if (!mid.empty()) {
+  }
+  std::vector<ChainJob> nine, rest;   // memLevel 9 with n < 64 Ki: LDS counters + HBM bases
+  for (const ChainJob& jb : big) ((jb.memlevel == 9 && jb.n < 65536) ? nine : rest).push_back(jb);
+  big.swap(rest);
+  if (!nine.empty()) {
+    const size_t nb9 = 4096;
+    if (int r = c->d_heads2.reserve(nb9 * 65536 * 4)) return r;
+    for (size_t k = 0; k < nine.size(); k++) nine[k].slot = (uint32_t)(k % nb9);
+    if (int r = upload(c, c->d_cjobs3, nine.data(), nine.size() * sizeof(ChainJob))) return r;
+    for (size_t b0 = 0; b0 < nine.size(); b0 += nb9) {
+      const size_t nb = std::min(nb9, nine.size() - b0);
       kbeg(c, 2);
-      hipLaunchKernelGGL(k_buckets_lds<32768>, dim3((uint32_t)mid.size()), dim3(256), 0, c->st,
-                         c->d_infl.as<uint8_t>(), c->d_cjobs2.as<ChainJob>() + small.size(),
-                         c->d_chains.as<uint32_t>(), (uint32_t)mid.size());
+      hipLaunchKernelGGL(k_buckets_lds9, dim3((uint32_t)nb), dim3(256), 0, c->st, c->d_infl.as<uint8_t>(),
+                         c->d_cjobs3.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), c->d_heads2.as<uint32_t>(),
+                         (uint32_t)nb);
       kend(c);
-      KCHECK("k_buckets_lds<32768>");
+      KCHECK("k_buckets_lds9");
     }
   }
   const size_t batch = 4096;   // scratch: 65536 x 8-byte words per job slot

@@ -177,7 +177,7 @@ __global__ __launch_bounds__(64) void k_buckets(const uint8_t* __restrict__ infl
   }
 }
 
-// LDS variant for hash tables of <= TABLE (16384 or 32768) entries and streams < 65536 positions: one workgroup
+// LDS variant for hash tables of <= TABLE (4096, 16384 or 32768) entries and streams < 65536 positions: one workgroup
 // (4 waves) per job, one 32-bit LDS word per hash = (first index << 16) | assigned.  Zeroing, the
 // histogram and the scan use all 256 threads; the in-order assignment runs on wave 0 with LDS
 // atomics (~100-cycle round trips instead of HBM ones).
@@ -203,7 +203,13 @@ __global__ __launch_bounds__(256) void k_buckets_lds(const uint8_t* __restrict__
   auto hash = [&](uint32_t p) -> uint32_t {
     return (((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask;
   };
-  for (uint32_t p = tid; p < nh; p += 256) atomicAdd(&word[hash(p)], 1u);
+  for (uint32_t p0 = 0; p0 < nh; p0 += 1024) {   // 4 positions per thread in flight
+    uint32_t hs[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) { const uint32_t p = p0 + 256 * u + tid; hs[u] = p < nh ? hash(p) : 0xffffffffu; }
+#pragma unroll
+    for (int u = 0; u < 4; u++) if (hs[u] != 0xffffffffu) atomicAdd(&word[hs[u]], 1u);
+  }
   __syncthreads();
   // exclusive scan: each wave scans a quarter of the table, then the quarters are offset
   const uint32_t q = hsize / 4;   // >= 64
@@ -256,6 +262,110 @@ __global__ __launch_bounds__(256) void k_buckets_lds(const uint8_t* __restrict__
     if (real) {
       const uint32_t r = (old & 0xffffu) + (uint32_t)lane - gstart;
       const uint32_t at = (old >> 16) + r;
+      sidx[mypos] = at;
+      bpos[at] = mypos | (r == 0 ? BUCKET_FIRST : 0u);
+    }
+  }
+}
+
+// memLevel 9 (65536 hashes), streams < 65536 positions: two 16-bit counters per LDS word (128 KiB)
+// for the histogram and then "assigned so far"; the bucket bases go to HBM scratch (read-only after
+// the scan, loaded one batch ahead with the hashes).  No HBM atomics.
+__global__ __launch_bounds__(256) void k_buckets_lds9(const uint8_t* __restrict__ infl,
+                                                     const ChainJob* __restrict__ jobs,
+                                                     uint32_t* __restrict__ chains, uint32_t* __restrict__ scratch,
+                                                     uint32_t njobs) {
+  __shared__ uint32_t pair[32768];   // counters of hashes 2i (low half) and 2i+1 (high half)
+  __shared__ uint32_t wsum[4];
+  const uint32_t j = blockIdx.x;
+  if (j >= njobs) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const ChainJob jb = jobs[j];
+  const uint8_t* in = infl + jb.infl_off;
+  const uint32_t n = (uint32_t)jb.n;
+  const uint32_t npad = (n + 63) & ~63u;
+  uint32_t* sidx = chains + jb.chain_off;
+  uint32_t* bpos = sidx + npad;
+  uint32_t* base = scratch + (uint64_t)jb.slot * 65536;
+  const uint32_t hmask = 65535, hshift = 6;   // hash_bits 16
+  for (uint32_t i = tid; i < 32768; i += 256) pair[i] = 0;
+  __syncthreads();
+  const uint32_t nh = n >= 3 ? n - 2 : 0;
+  auto hash = [&](uint32_t p) -> uint32_t {
+    return (((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask;
+  };
+  for (uint32_t p = tid; p < nh; p += 256) {
+    const uint32_t h = hash(p);
+    atomicAdd(&pair[h >> 1], 1u << (16 * (h & 1)));
+  }
+  __syncthreads();
+  // exclusive scan over the 65536 counts (each wave a quarter; lane handles 2 counts per word)
+  uint32_t run = 0;
+  for (uint32_t g = wave * 8192; g < (wave + 1) * 8192; g += 64) {
+    const uint32_t w = pair[g + lane];
+    const uint32_t c = (w & 0xffffu) + (w >> 16);
+    uint32_t incl = c;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += t;
+    }
+    const uint32_t e0 = run + incl - c;
+    base[2 * (g + lane)] = e0;
+    base[2 * (g + lane) + 1] = e0 + (w & 0xffffu);
+    pair[g + lane] = 0;
+    run += __shfl(incl, 63, 64);
+  }
+  if (lane == 0) wsum[wave] = run;
+  __syncthreads();
+  uint32_t off = 0;
+  for (int w = 0; w < wave; w++) off += wsum[w];
+  if (off)
+    for (uint32_t g = wave * 8192; g < (wave + 1) * 8192; g += 64) {
+      base[2 * (g + lane)] += off;
+      base[2 * (g + lane) + 1] += off;
+    }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (wave != 0) return;
+  uint32_t hn = lane < (int)nh ? hash((uint32_t)lane) : 0xffffffffu;
+  uint32_t bn = hn != 0xffffffffu ? base[hn] : 0u;
+  for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
+    const uint32_t h = hn, bh = bn;
+    const uint32_t pn = b0 + 64 + lane;
+    hn = pn < nh ? hash(pn) : 0xffffffffu;
+    bn = hn != 0xffffffffu ? base[hn] : 0u;
+    const bool real = h != 0xffffffffu;
+    // sort (hash, lane) so equal hashes form groups in position order
+    uint64_t key = ((uint64_t)(real ? h : 0x1ffffu) << 6) | (uint32_t)lane;
+    for (int k = 2; k <= 64; k <<= 1)
+      for (int st = k >> 1; st > 0; st >>= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)key, st, 64), hi = __shfl_xor((uint32_t)(key >> 32), st, 64);
+        const uint64_t o = ((uint64_t)hi << 32) | lo;
+        const bool up = (lane & k) == 0, lower = (lane & st) == 0;
+        const uint64_t mn = key < o ? key : o, mx = key < o ? o : key;
+        key = (lower == up) ? mn : mx;
+      }
+    const uint32_t src = (uint32_t)(key & 63);
+    const uint32_t kh = (uint32_t)(key >> 6);
+    const uint32_t mypos = b0 + src;
+    const uint32_t mybase = __shfl(bh, (int)src, 64);
+    const uint32_t pk = __shfl_up(kh, 1, 64), nk = __shfl_down(kh, 1, 64);
+    const bool first = lane == 0 || pk != kh;
+    const bool last = lane == 63 || nk != kh;
+    const bool rl = kh != 0x1ffffu;
+    const uint64_t fm = __ballot(first);
+    const uint64_t below = fm & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+    const uint32_t gstart = 63 - (uint32_t)__clzll((long long)below);
+    const uint64_t lm = __ballot(last);
+    const uint64_t above = lm & (~0ull << lane);
+    const uint32_t gend = (uint32_t)__ffsll((unsigned long long)above) - 1;
+    uint32_t old = 0;
+    if (rl && first) old = atomicAdd(&pair[kh >> 1], (gend - gstart + 1) << (16 * (kh & 1)));
+    old = (__shfl(old, (int)gstart, 64) >> (16 * (kh & 1))) & 0xffffu;
+    if (rl) {
+      const uint32_t r = old + (uint32_t)lane - gstart;
+      const uint32_t at = mybase + r;
       sidx[mypos] = at;
       bpos[at] = mypos | (r == 0 ? BUCKET_FIRST : 0u);
     }
