@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libatz_accel.so")
+LIB_PATH = os.environ.get("ATZ_LIB") or os.path.join(HERE, "_build", "libatz_accel.so")   # ATZ_LIB: diagnostic builds
 CLI_PATH = os.path.join(HERE, "_build", "uncomp")
 
 u64 = C.c_uint64

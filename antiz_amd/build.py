@@ -36,7 +36,7 @@ def build(force=False, verbose=False):
     if force or _newer(LIB, srcs):
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-x", "hip",
                "-Wno-unused-result", "-Wno-unused-value",
-               os.path.join(CSRC, "atz_accel.cpp"), "-o", LIB]
+               os.path.join(CSRC, "atz_accel.cpp"), "-o", LIB] + os.environ.get("ATZ_HIPFLAGS", "").split()
         if verbose:
             print(" ".join(cmd))
         _run(cmd)

@@ -902,9 +902,12 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
 }
 
 static double g_t_list = 0, g_t_chains = 0, g_t_trials = 0, g_t_apply = 0;
+// per trial kind (stored/fast/slow) x level: count, cycles total/tree/emit/lookup/fallback, parsed bytes, symbols
+static uint64_t g_kind[3][10][8];
 static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
   auto t0 = std::chrono::steady_clock::now();
   g_t_list = g_t_chains = g_t_trials = g_t_apply = 0;
+  std::memset(g_kind, 0, sizeof(g_kind));
   const size_t n = c->recs.size();
   ss.assign(n, StreamState());
   c->chain_off.assign(n, {});
@@ -980,6 +983,9 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
         c->stats.trial_cyc_emit += r.cyc_emit; c->stats.trial_blocks += r.blocks;
         c->stats.trial_cyc_lookup += r.cyc_lookup; c->stats.trial_cyc_fallback += r.cyc_fallback;
         c->stats.trial_symbols += r.symbols;
+        uint64_t* gk = g_kind[k][tr[k][q].clevel];
+        gk[0]++; gk[1] += r.cyc_total; gk[2] += r.cyc_tree; gk[3] += r.cyc_emit; gk[4] += r.cyc_lookup;
+        gk[5] += r.cyc_fallback; gk[6] += r.parsed; gk[7] += r.symbols;
         // trial input read + compare read (bytes emitted and compared against the original)
         c->stats.k_trial_alg_bytes += c->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
       }
@@ -1088,6 +1094,16 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
   if (timing_on())
     std::fprintf(stderr, "atz: sweep host: chains %.1f ms (incl. kernels), trials %.1f ms (incl. kernels), apply %.1f ms, total %.1f ms\n",
                  g_t_chains, g_t_trials, g_t_apply, ms_since(t0));
+  if (timing_on())
+    for (int k = 0; k < 3; k++)
+      for (int l = 0; l < 10; l++) {
+        const uint64_t* gk = g_kind[k][l];
+        if (!gk[0]) continue;
+        std::fprintf(stderr, "atz: kind %d level %d: trials %llu cyc %.3fT (tree %.3fT emit %.3fT lookup %.3fT fb %.3fT) "
+                     "parsed %.1f MB syms %.1f M cyc/byte %.0f\n", k, l, (unsigned long long)gk[0], gk[1] / 1e12,
+                     gk[2] / 1e12, gk[3] / 1e12, gk[4] / 1e12, gk[5] / 1e12, gk[6] / 1e6, gk[7] / 1e6,
+                     gk[6] ? (double)gk[1] / gk[6] : 0.0);
+      }
   for (size_t s = 0; s < n; s++) {
     StreamState& st = ss[s];
     const uint64_t C = c->recs[s].comp_len;

@@ -538,6 +538,12 @@ struct TrialSharedFast {
   uint32_t holes[HOLE_SLOTS];   // position + 1 of the latest non-inserted position with hash & (SLOTS-1)
 };
 
+static constexpr uint32_t RING_SLOW = 512;   // >= 127 + 2 * 258 + 64: a walk never leaves the ring
+struct TrialSharedSlow {
+  TrialShared t;
+  uint64_t ring[RING_SLOW];   // match-table entries (.x low, .y high) of the positions around the window
+};
+
 struct SweepArgs {
   const uint8_t* file;          // original compressed bytes
   const uint8_t* infl;          // inflated bytes
@@ -1155,21 +1161,14 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   for (int i = lane; i < NDC; i += 64) s.dfreq[i] = 0;
   if (lane == 0) s.lfreq[256] = 1;
   uint32_t hazard = 0;
-  // Block statistics live in VGPRs across lanes (lfreq[c] in lane c & 63, register c >> 6) and
-  // symbols are staged one per lane, 64 per coalesced store: the scalar parse issues no LDS
-  // read-modify-write and no per-symbol HBM store.
-  uint32_t lf0 = 0, lf1 = 0, lf2 = 0, lf3 = 0, lf4 = lane == 0 ? 1u : 0u;   // lfreq[256] = 1 (END_BLOCK)
+  // Block statistics live in VGPRs across lanes and symbols are staged one per lane, 64 per
+  // coalesced store: the scalar parse issues no LDS read-modify-write and no per-symbol HBM store.
+  // Literal counts are packed two per register (a block holds < 32768 symbols): lfa = lfreq[l] |
+  // lfreq[64+l] << 16, lfb = lfreq[128+l] | lfreq[192+l] << 16 in lane l; length codes 256..285 in
+  // lf4 (lane code-256), distance codes in dfr.  (Selecting among registers by a computed index
+  // would be lowered to a scratch array with a memory round trip per literal.)
+  uint32_t lfa = 0, lfb = 0, lf4 = lane == 0 ? 1u : 0u;   // lfreq[256] = 1 (END_BLOCK)
   uint32_t dfr = 0, symreg = 0;
-  auto count_l = [&](uint32_t code) {
-    const uint32_t me = (uint32_t)lane == (code & 63u) ? 1u : 0u;
-    switch (code >> 6) {
-      case 0: lf0 += me; break;
-      case 1: lf1 += me; break;
-      case 2: lf2 += me; break;
-      case 3: lf3 += me; break;
-      default: lf4 += me; break;
-    }
-  };
   auto stage = [&](uint32_t v) {
     const uint32_t slot = z.last_lit & 63u;
     if ((uint32_t)lane == slot) symreg = v;
@@ -1178,23 +1177,29 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   };
   auto tally_lit = [&](uint32_t c) -> bool {
     stage(c);
-    count_l(c);
+    const uint32_t inc = (uint32_t)lane == (c & 63u) ? (1u << ((c >> 2) & 16u)) : 0u;
+    const bool hi = (c & 128u) != 0;
+    lfa += hi ? 0u : inc;
+    lfb += hi ? inc : 0u;
     return z.last_lit == z.lbs - 1;
   };
   auto tally_dist = [&](uint32_t dist, uint32_t len) -> bool {
     stage((dist << 8) | len);
-    count_l(len_code(len) + 257u);
+    lf4 += (uint32_t)lane == len_code(len) + 1u ? 1u : 0u;   // lfreq[257 + len_code]
     dfr += (uint32_t)lane == dist_code(dist - 1) ? 1u : 0u;
     return z.last_lit == z.lbs - 1;
   };
   auto FLUSH = [&](int last) {
-    const uint32_t part = z.last_lit & 63u;
-    if (part && (uint32_t)lane < part) syms[(z.last_lit & ~63u) + lane] = symreg;
-    s.lfreq[lane] = lf0; s.lfreq[64 + lane] = lf1; s.lfreq[128 + lane] = lf2; s.lfreq[192 + lane] = lf3;
-    if (lane < NLC - 256) s.lfreq[256 + lane] = lf4;
-    if (lane < NDC) s.dfreq[lane] = dfr;
+    if constexpr (KIND != 2) {   // the slow kind tallies straight into LDS and HBM
+      const uint32_t part = z.last_lit & 63u;
+      if (part && (uint32_t)lane < part) syms[(z.last_lit & ~63u) + lane] = symreg;
+      s.lfreq[lane] = lfa & 0xffffu; s.lfreq[64 + lane] = lfa >> 16;
+      s.lfreq[128 + lane] = lfb & 0xffffu; s.lfreq[192 + lane] = lfb >> 16;
+      if (lane < NLC - 256) s.lfreq[256 + lane] = lf4;
+      if (lane < NDC) s.dfreq[lane] = dfr;
+    }
     hazard |= uni(flush_block(s, b, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, lane));
-    lf0 = lf1 = lf2 = lf3 = 0; lf4 = lane == 0 ? 1u : 0u; dfr = 0;
+    lfa = lfb = 0; lf4 = lane == 0 ? 1u : 0u; dfr = 0;
     z.last_lit = 0;
     z.block_start = z.p;
   };
@@ -1396,53 +1401,177 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       }
     }
   } else {
-    // deflate_slow (Z/deflate.c:1730-1853) reading longest_match's results from the match table
-    uint32_t prev_byte = 0;   // input byte at strstart - 1 (the lazily held literal)
-    for (;;) {
-      if (z.lookahead < LOOKMIN) { fill(z); if (z.lookahead == 0) break; }
-      if (z.p >= tr.x_lim) { state = TR_NEED_R; break; }
-      const uint64_t cl0 = STEP_CLOCK();
-      const uint2 e = pw.get(z.p, lane);
-      const bool hv = z.lookahead >= 3 && (e.y & 1u) && !head_is_S();
-      z.prev_length = z.match_length; z.prev_match = z.match_start;
-      z.match_length = 2;
-      if (hv && z.prev_length < z.lazy) {
-        const uint32_t ev = z.prev_length >= z.good ? e.y : e.x;
-        const uint32_t len = ev >> 23;
-        if (len > z.prev_length) { z.match_length = len; z.match_start = z.p - ((ev >> 8) & 0x7fffu); }
-        else z.match_length = z.prev_length <= z.lookahead ? z.prev_length : (uint32_t)z.lookahead;
-        if (z.match_length == 3 && z.p - z.match_start > 4096) z.match_length = 2;
+    // deflate_slow (Z/deflate.c:1730-1853), lane-parallel.
+    // After an emitted match (and at the start) deflate_slow's state is canonical: prev_length 2,
+    // no pending literal; after a literal with no match pending it is prev_length 2 with a pending
+    // literal.  So the iterations from a position x up to the next canonical state -- "the walk
+    // from x": either no match at x (next state at x + 1), or a lazy chain of c improving matches
+    // that emits literals x .. m-1 and then the match at m = x + c (next state at m + length) --
+    // depend on x alone.  A window computes the walks from its 64 positions in lanes, the scalar
+    // unit follows the parse path through them (one hop per match or literal run), and the path's
+    // symbols are tallied lane-parallel in position order, which is deflate_slow's tally order.
+    // Window slides are a function of the iteration position (fill_window runs at the top of the
+    // iteration when lookahead < MIN_LOOKAHEAD), so each lane evaluates them itself.
+    LDS uint64_t* ring = (LDS uint64_t*)shm.ring;    // match-table entries, position & (RING_SLOW - 1)
+    const GLOBAL uint64_t* Rt = (const GLOBAL uint64_t*)(A.R + tr.r_off);
+    const uint32_t n = z.n, wsz = z.wsize, maxd = z.maxdist, xlim = (uint32_t)tr.x_lim;
+    auto S_iter = [&](uint32_t S0, uint32_t q) -> uint32_t {   // S at an iteration at q >= one with S0
+      uint32_t Sx = S0;
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const bool exh = n <= Sx + 2u * wsz;
+        const bool slide = exh ? (q + LOOKMIN > n && q >= Sx + wsz + maxd) : (q > Sx + wsz + maxd);
+        if (slide) Sx += wsz;
       }
-      cyc_lookup += STEP_CLOCK() - cl0;
-      if (z.prev_length >= 3 && z.match_length <= z.prev_length) {
-        bool bflush = tally_dist((uint32_t)(z.p - 1 - z.prev_match), z.prev_length - 3);
-        z.lookahead -= z.prev_length - 1;
-        z.p += z.prev_length - 1;
-        z.match_available = 0;
-        z.match_length = 2;
-        if (bflush) {
+      return Sx;
+    };
+    // ring: chunks of 64 entries below `hi` are resident; the chunk at `hi` is in flight in pf
+    uint32_t hi = 0;
+    uint64_t pf = n ? Rt[lane] : 0ull;
+    uint32_t q = 0, ma = 0, Sb = 0, prevb = 0;   // canonical position, pending literal, S there, byte q-1
+    bool need = false;
+    while (q < n) {
+      const uint32_t wb = q, bal = wb & ~63u;
+      while (hi < bal + RING_SLOW) {
+        ring[(hi + lane) & (RING_SLOW - 1)] = pf;
+        hi += 64;
+        if (hi < n) pf = Rt[hi + lane];
+      }
+      Sb = S_iter(Sb, wb);
+      // ---- the walk from x = wb + lane: wt 0 none (x >= n), 1 no match, 2 match, 3 needs R >= x_lim
+      const uint32_t x = wb + lane;
+      uint32_t wt = 0, nxt = 0, c = 0, L = 0, D = 0;
+      if (x < n) {
+        uint32_t qq = x, PL = 2, PD = 0;
+        for (;;) {
+          if (qq >= xlim) { wt = 3; break; }
+          const uint64_t e64 = ring[qq & (RING_SLOW - 1)];
+          const uint32_t ex = (uint32_t)e64, ey = (uint32_t)(e64 >> 32);
+          bool hv = qq + 3u <= n && (ey & 1u);
+          if (hv) {   // hash_head == S is NIL after a slide (only right after one)
+            const uint32_t Sq = S_iter(Sb, qq);
+            if (Sq != 0 && qq - Sq <= maxd) {
+              const uint32_t si = sidx[qq];
+              hv = (bpos[si] & BUCKET_FIRST) || (bpos[si - 1] & ~BUCKET_FIRST) != Sq;
+            }
+          }
+          if (PL == 2) {   // first iteration of the walk (qq == x)
+            const uint32_t len = ex >> 23, dist = (ex >> 8) & 0x7fffu;
+            uint32_t ML = hv && len > 2 ? len : 2u;
+            if (ML == 3 && dist > 4096) ML = 2;   // TOO_FAR
+            if (ML == 2) { wt = 1; nxt = x + 1; break; }
+            PL = ML; PD = dist; qq++;
+            continue;
+          }
+          if (PL < z.lazy && hv) {
+            const uint32_t ev = PL >= z.good ? ey : ex;
+            const uint32_t len = ev >> 23;
+            if (len > PL) { PL = len; PD = (ev >> 8) & 0x7fffu; c++; qq++; continue; }
+          }
+          wt = 2; L = PL; D = PD; nxt = qq - 1 + PL;
+          break;
+        }
+      }
+      // ---- follow the parse path through the window
+      const uint64_t Am = __ballot(wt == 1), Nm = __ballot(wt == 3);
+      uint64_t P = 0, MAm = 0;
+      uint32_t qn = wb, man = ma;
+      while (qn < wb + 64 && qn < n) {
+        const uint32_t i = qn - wb;
+        const uint64_t bit = 1ull << i;
+        if (Nm & bit) { need = true; break; }
+        P |= bit;
+        if (man) MAm |= bit;
+        if (Am & bit) {   // a run of positions without a match: one literal each
+          const uint64_t rest = ~(Am >> i);
+          const uint32_t k = rest ? (uint32_t)__builtin_ctzll(rest) : 64u - i;
+          const uint64_t rm = (k >= 64 ? ~0ull : ((1ull << k) - 1ull)) << i;
+          P |= rm;
+          MAm |= rm & ~bit;
+          qn += k;
+          man = 1;
+        } else {
+          qn = (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)i);
+          man = 0;
+        }
+      }
+      // ---- tally the path's symbols: node x emits [literal x-1 if pending], literals x..m-1, match
+      const bool onp = (P >> lane) & 1ull;
+      const uint32_t mab = (uint32_t)((MAm >> lane) & 1ull);
+      const uint32_t cnt = onp ? mab + (wt == 2 ? c + 1u : 0u) : 0u;
+      uint32_t incl = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += t;
+      }
+      const uint32_t o = incl - cnt;
+      const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      z.nsym += T;
+      uint32_t base = 0;
+      while (base < T) {
+        const uint32_t room = z.lbs - 1u - z.last_lit;
+        const uint32_t seg_end = T - base < room ? T : base + room;
+        const uint32_t klo = o > base ? 0u : base - o;
+        const uint32_t khi = o + cnt < seg_end ? cnt : (seg_end > o ? seg_end - o : 0u);
+        for (uint32_t k = klo; k < khi; k++) {
+          const uint32_t j = k - mab;   // k == 0 with mab: literal x-1
+          uint32_t v;
+          if (mab && k == 0) v = lane == 0 ? prevb : (uint32_t)ring[(x - 1) & (RING_SLOW - 1)] & 0xffu;
+          else if (j < c) v = (uint32_t)ring[(x + j) & (RING_SLOW - 1)] & 0xffu;
+          else v = 0x80000000u | (D << 8) | (L - 3u);
+          if (v & 0x80000000u) {
+            v &= 0x7fffffffu;
+            __hip_atomic_fetch_add(&s.lfreq[257u + len_code(L - 3u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.dfreq[dist_code(D - 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            __hip_atomic_fetch_add(&s.lfreq[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          syms[z.last_lit + (o + k - base)] = v;
+        }
+        z.last_lit += seg_end - base;
+        if (z.last_lit == z.lbs - 1u) {
+          // flush after symbol seg_end - 1: strstart = its iteration + 1 for a literal (the
+          // literal of y is tallied at iteration y + 1), match end for a match (tallied at m + 1)
+          const uint32_t g = seg_end - 1u;
+          const bool own = cnt && o <= g && g < o + cnt;
+          uint32_t fp = 0, fit = 0;
+          if (own) {
+            const uint32_t k = g - o, j = k - mab;
+            if (mab && k == 0) { fp = x; fit = x; }
+            else if (j < c) { fp = x + j + 1u; fit = fp; }
+            else { fp = x + c + L; fit = x + c + 1u; }
+          }
+          const uint64_t om = __ballot(own);
+          const int ol = (int)__builtin_ctzll(om);
+          z.p = (uint32_t)__builtin_amdgcn_readlane((int)fp, ol);
+          z.S = S_iter(Sb, (uint32_t)__builtin_amdgcn_readlane((int)fit, ol));
           FLUSH(0);
           state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
           if (state != ~0u) break;
         }
-      } else if (z.match_available) {
-        bool bflush = tally_lit(prev_byte);
-        prev_byte = e.x & 0xffu;
-        if (bflush) {
-          FLUSH(0);
-          state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
-          if (state != ~0u) break;
-        }
-        z.p++;
-        z.lookahead--;
-      } else {
-        prev_byte = e.x & 0xffu;
-        z.match_available = 1;
-        z.p++;
-        z.lookahead--;
+        base = seg_end;
       }
+      if (state != ~0u) break;
+      if (need) { state = TR_NEED_R; z.p = qn; break; }
+      prevb = qn > 0 ? (uint32_t)ring[(qn - 1u) & (RING_SLOW - 1)] & 0xffu : 0u;   // read when man: qn - 1 < wb + 64
+      q = qn;
+      ma = man;
     }
-    if (state == ~0u && z.match_available) { tally_lit(prev_byte); z.match_available = 0; }
+    if (state == ~0u) {
+      // end of input: the pending literal goes into the final block without a flush check
+      if (ma) {
+        const uint32_t v = prevb;
+        if (lane == 0) {
+          syms[z.last_lit] = v;
+          __hip_atomic_fetch_add(&s.lfreq[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        z.last_lit++;
+        z.nsym++;
+      }
+      z.p = n;
+      z.S = S_iter(Sb, n);
+    }
   }
   if (state == ~0u) {
     FLUSH(1);
@@ -1492,7 +1621,7 @@ __global__ __launch_bounds__(64) void k_trial_fast(SweepArgs A) {
   trial_body<1>(A, shm, threadIdx.x);
 }
 __global__ __launch_bounds__(64) void k_trial_slow(SweepArgs A) {
-  __shared__ struct { TrialShared t; } shm;
+  __shared__ TrialSharedSlow shm;
   trial_body<2>(A, shm, threadIdx.x);
 }
 
