@@ -534,6 +534,7 @@ struct TrialShared {
 
 struct TrialSharedFast {
   TrialShared t;
+  uint64_t ring[512];   // match-table entries around the parse window (RING_SLOW)
   uint32_t ins[BITMAP_BITS / 32];   // insertion ring (InsRing)
   uint32_t holes[HOLE_SLOTS];   // position + 1 of the latest non-inserted position with hash & (SLOTS-1)
 };
@@ -947,26 +948,6 @@ struct Lz {
 // Double-buffered lane-resident window over the trial's match table: lane l holds the entry of
 // position rb + l and the entry of rb + 64 + l is in flight, so the wave-uniform parse reads its
 // per-position data with v_readlane and the next HBM round trip overlaps ~64 positions of work.
-struct PosWin {
-  const uint2* R;
-  uint32_t rb;
-  uint32_t cx, cy, nx, ny;
-  __device__ __forceinline__ void init(const uint2* r) { R = r; rb = 1u << 31; cx = cy = nx = ny = 0; }
-  __device__ __forceinline__ uint2 get(uint32_t p, int lane) {
-    if (p - rb >= 64) {
-      if (p - rb < 128) { cx = nx; cy = ny; rb += 64; }
-      else { rb = p; const uint2 e = R[rb + lane]; cx = e.x; cy = e.y; }
-      const uint2 f = R[rb + 64 + lane];
-      nx = f.x; ny = f.y;
-    }
-    uint2 e;
-    e.x = (uint32_t)__builtin_amdgcn_readlane((int)cx, (int)(p - rb));
-    e.y = (uint32_t)__builtin_amdgcn_readlane((int)cy, (int)(p - rb));
-    return e;
-  }
-};
-
-
 // fill_window bookkeeping (Z/deflate.c:1390-1532) on absolute positions
 __device__ __forceinline__ void fill(Lz& z) {
   do {
@@ -996,26 +977,6 @@ __device__ inline uint32_t common_len(const uint8_t* in, uint64_t a, uint64_t b,
   }
   return cap;
 }
-
-// deflate_fast insertion state: positions >= w0 live in a uniform 64-bit mask, older ones in a
-// 65536-bit ring in LDS written one whole word per 32 positions.
-struct InsRing {
-  LDS uint32_t* ring;
-  uint32_t w0;     // multiple of 32
-  uint64_t mask;   // bit k: position w0 + k inserted
-  __device__ __forceinline__ void set(uint32_t q) { mask |= 1ull << (q - w0); }
-  __device__ __forceinline__ void advance(uint32_t p) {   // keep p < w0 + 32
-    while (p >= w0 + 32) {
-      ring[(w0 >> 5) & (BITMAP_BITS / 32 - 1)] = (uint32_t)mask;
-      mask >>= 32;
-      w0 += 32;
-    }
-  }
-  __device__ __forceinline__ bool get(uint32_t q) const {   // per lane (q may differ between lanes)
-    if (q >= w0) return (mask >> (q - w0)) & 1;
-    return (ring[(q >> 5) & (BITMAP_BITS / 32 - 1)] >> (q & 31)) & 1;
-  }
-};
 
 // _tr_flush_block (Z/trees.c:907-1004) + FLUSH_BLOCK_ONLY bookkeeping
 // The parse state is passed by value so that it never leaves registers (a reference to it here
@@ -1137,10 +1098,6 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   const uint32_t npad = (sd.infl_len + 63) & ~63ull;
   const uint32_t* sidx = KIND == 0 ? nullptr : A.chains + tr.chain_off;
   const uint32_t* bpos = KIND == 0 ? nullptr : sidx + npad;
-  InsRing insr;   // fast levels: insertion state
-  if constexpr (KIND == 1) insr.ring = (LDS uint32_t*)shm.ins;
-  else insr.ring = nullptr;
-  insr.w0 = 0; insr.mask = 0;
   const bool full_needed = tr.mode & 1;
   Lz z;
   z.level = tr.clevel; z.kind = KIND;
@@ -1161,52 +1118,14 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   for (int i = lane; i < NDC; i += 64) s.dfreq[i] = 0;
   if (lane == 0) s.lfreq[256] = 1;
   uint32_t hazard = 0;
-  // Block statistics live in VGPRs across lanes and symbols are staged one per lane, 64 per
-  // coalesced store: the scalar parse issues no LDS read-modify-write and no per-symbol HBM store.
-  // Literal counts are packed two per register (a block holds < 32768 symbols): lfa = lfreq[l] |
-  // lfreq[64+l] << 16, lfb = lfreq[128+l] | lfreq[192+l] << 16 in lane l; length codes 256..285 in
-  // lf4 (lane code-256), distance codes in dfr.  (Selecting among registers by a computed index
-  // would be lowered to a scratch array with a memory round trip per literal.)
-  uint32_t lfa = 0, lfb = 0, lf4 = lane == 0 ? 1u : 0u;   // lfreq[256] = 1 (END_BLOCK)
-  uint32_t dfr = 0, symreg = 0;
-  auto stage = [&](uint32_t v) {
-    const uint32_t slot = z.last_lit & 63u;
-    if ((uint32_t)lane == slot) symreg = v;
-    if (slot == 63u) syms[z.last_lit - 63u + lane] = symreg;
-    z.last_lit++; z.nsym++;
-  };
-  auto tally_lit = [&](uint32_t c) -> bool {
-    stage(c);
-    const uint32_t inc = (uint32_t)lane == (c & 63u) ? (1u << ((c >> 2) & 16u)) : 0u;
-    const bool hi = (c & 128u) != 0;
-    lfa += hi ? 0u : inc;
-    lfb += hi ? inc : 0u;
-    return z.last_lit == z.lbs - 1;
-  };
-  auto tally_dist = [&](uint32_t dist, uint32_t len) -> bool {
-    stage((dist << 8) | len);
-    lf4 += (uint32_t)lane == len_code(len) + 1u ? 1u : 0u;   // lfreq[257 + len_code]
-    dfr += (uint32_t)lane == dist_code(dist - 1) ? 1u : 0u;
-    return z.last_lit == z.lbs - 1;
-  };
+  // Symbols and block statistics are tallied straight into HBM (syms) and LDS (lfreq / dfreq).
   auto FLUSH = [&](int last) {
-    if constexpr (KIND != 2) {   // the slow kind tallies straight into LDS and HBM
-      const uint32_t part = z.last_lit & 63u;
-      if (part && (uint32_t)lane < part) syms[(z.last_lit & ~63u) + lane] = symreg;
-      s.lfreq[lane] = lfa & 0xffffu; s.lfreq[64 + lane] = lfa >> 16;
-      s.lfreq[128 + lane] = lfb & 0xffffu; s.lfreq[192 + lane] = lfb >> 16;
-      if (lane < NLC - 256) s.lfreq[256 + lane] = lf4;
-      if (lane < NDC) s.dfreq[lane] = dfr;
-    }
     hazard |= uni(flush_block(s, b, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, lane));
-    lfa = lfb = 0; lf4 = lane == 0 ? 1u : 0u; dfr = 0;
     z.last_lit = 0;
     z.block_start = z.p;
   };
   uint32_t state = ~0u;
   uint64_t fallbacks = 0, cyc_lookup = 0, cyc_fb = 0;
-  PosWin pw;
-  pw.init(A.R + tr.r_off);
   // zlib header (Z/deflate.c:738-759)
   {
     uint32_t header = (8u + ((uint32_t)(tr.window - 8) << 4)) << 8;
@@ -1215,14 +1134,27 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     header += 31 - (header % 31);
     put_bits(b, s.stage, ((header >> 8) & 0xff) | ((header & 0xff) << 8), 16, lane);
   }
-  // hash_head of zlib after a window slide: NIL when it is exactly the slide offset S.  Only
-  // possible while p - S <= MAX_DIST (right at a slide); then the chain link is read directly.
-  auto head_is_S = [&]() -> bool {
-    if (z.S == 0 || z.p - z.S > z.maxdist) return false;
-    const uint32_t si = uni(sidx[z.p]);
-    if (uni(bpos[si]) & BUCKET_FIRST) return false;
-    return (uni(bpos[si - 1]) & ~BUCKET_FIRST) == z.S;
+  // fast and slow kinds: match-table entries of the positions around the parse window in an LDS
+  // ring; window slides (fill_window at the top of an iteration when lookahead < MIN_LOOKAHEAD)
+  // are a function of the iteration position, so any lane can evaluate them.
+  LDS uint64_t* ring = nullptr;
+  if constexpr (KIND != 0) ring = (LDS uint64_t*)shm.ring;   // position & (RING_SLOW - 1); .x low, .y high
+  const GLOBAL uint64_t* Rt = (const GLOBAL uint64_t*)(A.R + tr.r_off);
+  const uint32_t n = z.n, wsz = z.wsize, maxd = z.maxdist, xlim = (uint32_t)tr.x_lim;
+  auto S_iter = [&](uint32_t S0, uint32_t q) -> uint32_t {   // S at an iteration at q >= one with S0
+    uint32_t Sx = S0;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const bool exh = n <= Sx + 2u * wsz;
+      const bool slide = exh ? (q + LOOKMIN > n && q >= Sx + wsz + maxd) : (q > Sx + wsz + maxd);
+      if (slide) Sx += wsz;
+    }
+    return Sx;
   };
+  // ring: chunks of 64 entries below `hi` are resident; the chunk at `hi` is in flight in pf
+  uint32_t hi = 0;
+  uint64_t pf = 0;
+  if (KIND != 0 && n) pf = Rt[lane];
   if constexpr (KIND == 0) {
     // deflate_stored (Z/deflate.c:1564-1619)
     uint64_t max_block = 0xffff;
@@ -1246,159 +1178,291 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       }
     }
   } else if constexpr (KIND == 1) {
-    // deflate_fast (Z/deflate.c:1628-1722).  The match table holds each position's walk over ALL
-    // same-hash positions; it equals deflate_fast's walk over the INSERTED ones unless a position
-    // this parse skipped (interior of a match longer than max_insert_length) lies in the walked
-    // range [p - reach, p) with the same hash -- detected through holes[] (per hash slot, the
-    // latest skipped position; slot collisions only cause extra exact walks).
-    uint32_t* holes = shm.holes;
+    // deflate_fast (Z/deflate.c:1628-1722), lane-parallel.  Every deflate_fast iteration starts in
+    // the same state, so a window takes the match table's step at each of its 64 positions in
+    // lanes, the scalar unit follows the parse path through them, and the path's insertion state
+    // and symbols are written lane-parallel.  A table entry is the walk over ALL same-hash
+    // positions; deflate_fast walks the INSERTED ones (interiors of matches longer than
+    // max_insert_length are skipped: "holes"), so every path node is checked: the entry is exact
+    // unless a hole with its hash slot lies in the walked range [lowest visited node, p) AND it
+    // can matter -- skipped nodes only shrink the visited set, so a walk that ended by nice_match
+    // or by the end of the chain keeps its winner W if W itself was inserted (and with no winner
+    // the step emits a literal either way); only a walk that spent its budget with nodes left can
+    // see new nodes (bit 12).  The first node that fails the check is walked exactly over the
+    // inserted positions and the window ends there.  holes[] keeps per slot the latest hole; the
+    // window's own holes are entered before the check, so a hole behind the node only makes the
+    // check conservative (slot collisions likewise).
+    LDS uint32_t* holes = (LDS uint32_t*)shm.holes;
+    LDS uint32_t* ins = (LDS uint32_t*)shm.ins;   // insertion bits, position mod BITMAP_BITS
     for (int i = lane; i < (int)HOLE_SLOTS; i += 64) holes[i] = 0;
-    const uint32_t hbits = tr.memlevel + 7u, hmask = (1u << hbits) - 1u, hshift = (hbits + 2u) / 3u;
-    for (;;) {
-      if (z.lookahead < LOOKMIN) { fill(z); if (z.lookahead == 0) break; }
-      if (z.p >= tr.x_lim) { state = TR_NEED_R; break; }
-      insr.advance(z.p);
-      const uint64_t cl0 = STEP_CLOCK();
-      const uint2 e = pw.get(z.p, lane);
-      if (z.lookahead >= 3) {
-        insr.set(z.p);
-        const uint32_t hl = uni(holes[(e.y >> 1) & (HOLE_SLOTS - 1)]);
-        // The table entry is deflate_fast's exact result unless a skipped position with this hash
-        // lies in the walked range AND it can matter: skipped nodes only shrink the visited set,
-        // so a walk that ended by nice_match or by the end of the chain keeps its winner W if W
-        // itself was inserted (and with no winner the step emits a literal either way); only a
-        // walk that spent its budget with nodes left can see new nodes (bit 12).
-        bool exact = hl == 0 || hl - 1 < z.p - (e.y >> 16);
-        if (!exact && !((e.y >> 12) & 1u)) {
-          if ((e.x >> 23) <= 2) exact = true;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    auto ins_get = [&](uint32_t q) -> bool { return (ins[(q >> 5) & (BITMAP_BITS / 32 - 1)] >> (q & 31)) & 1u; };
+    // insertion bits and holes of the positions [lo, hi) covered by path nodes; cover(p) gives the
+    // node y <= p covering p and its match length (0: literal).  cover runs with all lanes active
+    // (it may shuffle: a lane outside EXEC would read as 0).
+    auto span_set = [&](uint32_t lo, uint32_t hi2, auto cover) {
+      for (uint32_t c0 = lo & ~63u; c0 < hi2; c0 += 64) {
+        const uint32_t p = c0 + (uint32_t)lane;
+        const bool insp = p >= lo && p < hi2;
+        bool insd = false, hole = false;
+        uint32_t y, Ly;
+        cover(p, y, Ly);
+        if (insp) {
+          if (p == y) insd = p + 3u <= n;
+          else if (Ly <= z.lazy && y + Ly + 3u <= n) insd = true;
+          else hole = p + 3u <= n;
+        }
+        const uint64_t bits = __ballot(insd), sm = __ballot(insp);
+        if (lane < 2) {
+          const uint32_t sh = 32u * (uint32_t)lane;
+          const uint32_t m = (uint32_t)(sm >> sh), bv = (uint32_t)(bits >> sh);
+          if (m) {
+            LDS uint32_t& w = ins[((c0 + sh) >> 5) & (BITMAP_BITS / 32 - 1)];
+            w = (w & ~m) | (bv & m);
+          }
+        }
+        if (hole) {
+          const uint32_t slot = ((uint32_t)(ring[p & (RING_SLOW - 1)] >> 32) >> 1) & (HOLE_SLOTS - 1);
+          __hip_atomic_fetch_max(&holes[slot], p + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    };
+    // one symbol, tallied by the scalar unit; returns true when the block is full
+    auto tally1 = [&](uint32_t v) -> bool {
+      if (lane == 0) {
+        syms[z.last_lit] = v;
+        if (v >> 8) {
+          __hip_atomic_fetch_add(&s.lfreq[257u + len_code(v & 0xffu)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&s.dfreq[dist_code((v >> 8) - 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          __hip_atomic_fetch_add(&s.lfreq[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      z.last_lit++;
+      z.nsym++;
+      return z.last_lit == z.lbs - 1u;
+    };
+    uint32_t q = 0, Sb = 0;
+    bool need = false;
+    while (q < n) {
+      const uint32_t wb = q, bal = wb & ~63u;
+      while (hi < bal + RING_SLOW) {
+        ring[(hi + lane) & (RING_SLOW - 1)] = pf;
+        hi += 64;
+        if (hi < n) pf = Rt[hi + lane];
+      }
+      Sb = S_iter(Sb, wb);
+      // ---- the table's step at x = wb + lane: wt 0 none (x >= n), 1 literal, 2 match, 3 needs R >= x_lim
+      const uint32_t x = wb + lane;
+      uint32_t wt = 0, L = 0, D = 0, ex = 0, ey = 0, Sx = Sb;
+      if (x < n) {
+        if (x >= xlim) wt = 3;
+        else {
+          const uint64_t e64 = ring[x & (RING_SLOW - 1)];
+          ex = (uint32_t)e64; ey = (uint32_t)(e64 >> 32);
+          Sx = S_iter(Sb, x);
+          bool hv = x + 3u <= n && (ey & 1u);
+          if (hv && Sx != 0 && x - Sx <= maxd) {   // hash_head == S is NIL after a slide
+            const uint32_t si = sidx[x];
+            hv = (bpos[si] & BUCKET_FIRST) || (bpos[si - 1] & ~BUCKET_FIRST) != Sx;
+          }
+          const uint32_t len = ex >> 23;
+          if (hv && len > 2) { wt = 2; L = len; D = (ex >> 8) & 0x7fffu; }
+          else wt = 1;
+        }
+      }
+      // ---- follow the parse path through the window
+      const uint64_t Am = __ballot(wt == 1), Nm = __ballot(wt == 3);
+      uint64_t P = 0;
+      uint32_t qn = wb, last = wb;
+      while (qn < wb + 64 && qn < n) {
+        const uint32_t i = qn - wb;
+        const uint64_t bit = 1ull << i;
+        if (Nm & bit) { need = true; break; }
+        P |= bit;
+        last = qn;
+        if (Am & bit) {   // a run of literals
+          const uint64_t rest = ~(Am >> i);
+          const uint32_t k = rest ? (uint32_t)__builtin_ctzll(rest) : 64u - i;
+          P |= (k >= 64 ? ~0ull : ((1ull << k) - 1ull)) << i;
+          qn += k;
+          last = qn - 1;
+        } else {
+          qn += (uint32_t)__builtin_amdgcn_readlane((int)L, (int)i);
+        }
+      }
+      // ---- insertion state of the path, then the check of its nodes
+      if (qn > wb)
+        span_set(wb, qn, [&](uint32_t p, uint32_t& y, uint32_t& Ly) {
+          const uint32_t i = p - wb;   // huge for p < wb (such lanes are outside the span)
+          uint32_t yl = last - wb;
+          if (i < 64) yl = 63u - (uint32_t)__builtin_clzll(P & (~0ull >> (63 - i)));
+          y = wb + yl;
+          Ly = (uint32_t)__shfl((int)L, (int)yl, 64);
+        });
+      const bool onp = (P >> lane) & 1ull;
+      bool bad = false;
+      if (onp && x + 3u <= n) {
+        const uint32_t hl = holes[(ey >> 1) & (HOLE_SLOTS - 1)];
+        bool exact = hl == 0 || hl - 1u < x - (ey >> 16);
+        if (!exact && !((ey >> 12) & 1u)) {
+          if ((ex >> 23) <= 2) exact = true;
           else {
-            const uint32_t wpos = z.p - ((e.x >> 8) & 0x7fffu);
-            exact = wpos > z.S && uni((uint32_t)insr.get(wpos));
+            const uint32_t wpos = x - ((ex >> 8) & 0x7fffu);
+            exact = wpos > Sx && ins_get(wpos);
           }
         }
-        if (exact) {
-          if ((e.y & 1u) && !head_is_S()) {
-            const uint32_t len = e.x >> 23;
-            if (len > 2) { z.match_length = len; z.match_start = z.p - ((e.x >> 8) & 0x7fffu); }
-            else z.match_length = 2;
-          }
-        } else {
-          fallbacks++;
-          const uint64_t cf0 = STEP_CLOCK();
-          // Exact deflate_fast longest_match over the INSERTED same-hash positions
-          // (Z/deflate.c:1148-1289): 64 bucket entries per step, lanes test insertion and compare
-          // bytes in parallel; the walk order is the lane order.
-          const uint32_t si = uni(sidx[z.p]);
-          bool done = (uni(bpos[si]) & BUCKET_FIRST) != 0;   // first of its bucket: no chain
-          bool head_done = false, hv = false, won = false;
-          uint32_t examined = 0, best = 2, win = 0;
-          const uint32_t limit = z.p > z.maxdist ? z.p - z.maxdist : 0u;   // later nodes only while > limit
-          const uint32_t cap = z.n - z.p < 258u ? z.n - z.p : 258u;
-          const uint32_t nicec = z.nice < z.lookahead ? z.nice : z.lookahead;   // <= cap
-          const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-          int32_t top = (int32_t)si - 1;
-          while (!done) {
-            const int32_t k = top - lane;
-            const uint32_t e = k >= 0 ? bpos[k] : BUCKET_FIRST;
-            const uint64_t fm = __ballot((e & BUCKET_FIRST) != 0);
-            const int flane = fm ? __ffsll((unsigned long long)fm) - 1 : 64;   // bucket's first entry: last node
-            const uint32_t q = e & ~BUCKET_FIRST;
-            const bool ins = lane <= flane && k >= 0 && insr.get(q);
-            const uint64_t im = __ballot(ins);
-            int head_lane = -1, from = 0;
-            if (!head_done) {
-              if (!im) {   // no inserted node in this chunk yet
-                if (flane < 64) break;
-                top -= 64;
-                continue;
-              }
-              head_lane = __ffsll((unsigned long long)im) - 1;
-              const uint32_t hh = (uint32_t)__builtin_amdgcn_readlane((int)q, head_lane);
-              head_done = true;
-              hv = hh > z.S && z.p - hh <= z.maxdist;   // zlib calls longest_match only then
-              if (!hv) break;
-              from = head_lane;
+        bad = !exact;
+      }
+      const uint64_t badm = __ballot(bad);
+      const uint64_t Pc = badm ? P & ((1ull << __builtin_ctzll(badm)) - 1ull) : P;
+      // ---- tally the committed nodes' symbols lane-parallel, in position order
+      {
+        const bool mine = (Pc >> lane) & 1ull;
+        const uint32_t o = (uint32_t)__popcll(Pc & lt);
+        const uint32_t T = (uint32_t)__popcll(Pc);
+        z.nsym += T;
+        uint32_t base = 0;
+        while (base < T) {
+          const uint32_t room = z.lbs - 1u - z.last_lit;
+          const uint32_t seg_end = T - base < room ? T : base + room;
+          if (mine && o >= base && o < seg_end) {
+            uint32_t v;
+            if (wt == 2) {
+              v = (D << 8) | (L - 3u);
+              __hip_atomic_fetch_add(&s.lfreq[257u + len_code(L - 3u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_fetch_add(&s.dfreq[dist_code(D - 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+              v = ex & 0xffu;
+              __hip_atomic_fetch_add(&s.lfreq[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            // the walk stops at the first inserted node <= limit (the head is always examined)
-            const uint64_t sm = __ballot(ins && lane >= from && lane != head_lane && q <= limit);
-            const int slane = sm ? __ffsll((unsigned long long)sm) - 1 : 64;
-            bool cand = ins && lane >= from && lane < slane;
-            const uint32_t room = z.chain - examined;
-            cand = cand && (uint32_t)__popcll(__ballot(cand) & lt) < room;
-            const uint64_t cm = __ballot(cand);
-            examined += (uint32_t)__popcll(cm);
-            // match lengths capped at nice (8 bytes per round trip); the first candidate reaching
-            // nice ends the walk, so capped lengths decide the winner
-            uint32_t len = 0;
-            bool go = cand;
-            while (__ballot(go)) {
-              if (go) {
-                uint32_t m = 0;
+            syms[z.last_lit + (o - base)] = v;
+          }
+          z.last_lit += seg_end - base;
+          if (z.last_lit == z.lbs - 1u) {   // flush after the node tallied last: strstart past its step
+            const uint64_t om = __ballot(mine && o == seg_end - 1u);
+            const int ol = (int)__builtin_ctzll(om);
+            const uint32_t fx = (uint32_t)__builtin_amdgcn_readlane((int)x, ol);
+            const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)L, ol);
+            z.p = fx + (fl ? fl : 1u);
+            z.S = S_iter(Sb, fx);
+            FLUSH(0);
+            state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+            if (state != ~0u) break;
+          }
+          base = seg_end;
+        }
+      }
+      if (state != ~0u) break;
+      if (!badm) {
+        if (need) { state = TR_NEED_R; z.p = qn; break; }
+        q = qn;
+        continue;
+      }
+      // ---- the first node that may differ: deflate_fast's longest_match over the INSERTED
+      // same-hash positions (Z/deflate.c:1148-1289): 64 bucket entries per step, lanes test
+      // insertion and compare bytes in parallel; the walk order is the lane order.
+      fallbacks++;
+      const uint64_t cf0 = STEP_CLOCK();
+      const uint32_t f = wb + (uint32_t)__builtin_ctzll(badm);
+      const uint32_t Sf = S_iter(Sb, f);
+      const uint32_t la = n - f < LOOKMIN ? n - f : LOOKMIN;   // lookahead (>= 258 stands for more)
+      uint32_t ml = 0, ms = 0;
+      {
+        const uint32_t si = uni(sidx[f]);
+        bool done = (uni(bpos[si]) & BUCKET_FIRST) != 0;   // first of its bucket: no chain
+        bool head_done = false, hv = false, won = false;
+        uint32_t examined = 0, best = 2, win = 0;
+        const uint32_t limit = f > maxd ? f - maxd : 0u;   // later nodes only while > limit
+        const uint32_t cap = n - f < 258u ? n - f : 258u;
+        const uint32_t nicec = z.nice < la ? z.nice : la;   // <= cap
+        int32_t top = (int32_t)si - 1;
+        while (!done) {
+          const int32_t k = top - lane;
+          const uint32_t e = k >= 0 ? bpos[k] : BUCKET_FIRST;
+          const uint64_t fm = __ballot((e & BUCKET_FIRST) != 0);
+          const int flane = fm ? __ffsll((unsigned long long)fm) - 1 : 64;   // bucket's first entry: last node
+          const uint32_t qc = e & ~BUCKET_FIRST;
+          const bool insd = lane <= flane && k >= 0 && ins_get(qc);
+          const uint64_t im = __ballot(insd);
+          int head_lane = -1, from = 0;
+          if (!head_done) {
+            if (!im) {   // no inserted node in this chunk yet
+              if (flane < 64) break;
+              top -= 64;
+              continue;
+            }
+            head_lane = __ffsll((unsigned long long)im) - 1;
+            const uint32_t hh = (uint32_t)__builtin_amdgcn_readlane((int)qc, head_lane);
+            head_done = true;
+            hv = hh > Sf && f - hh <= maxd;   // zlib calls longest_match only then
+            if (!hv) break;
+            from = head_lane;
+          }
+          // the walk stops at the first inserted node <= limit (the head is always examined)
+          const uint64_t sm = __ballot(insd && lane >= from && lane != head_lane && qc <= limit);
+          const int slane = sm ? __ffsll((unsigned long long)sm) - 1 : 64;
+          bool cand = insd && lane >= from && lane < slane;
+          const uint32_t room = z.chain - examined;
+          cand = cand && (uint32_t)__popcll(__ballot(cand) & lt) < room;
+          const uint64_t cm = __ballot(cand);
+          examined += (uint32_t)__popcll(cm);
+          // match lengths capped at nice (8 bytes per round trip); the first candidate reaching
+          // nice ends the walk, so capped lengths decide the winner
+          uint32_t len = 0;
+          bool go = cand;
+          while (__ballot(go)) {
+            if (go) {
+              uint32_t m = 0;
 #pragma unroll
-                for (int j = 0; j < 8; j++) m |= (in[q + len + j] == in[z.p + len + j] ? 1u : 0u) << j;
-                const uint32_t run = (uint32_t)__builtin_ctz(~m);   // matching prefix of the 8
-                const uint32_t left = nicec - len;
-                len += run < left ? run : left;
-                go = run == 8 && len < nicec;
-              }
+              for (int j = 0; j < 8; j++) m |= (in[qc + len + j] == in[f + len + j] ? 1u : 0u) << j;
+              const uint32_t run = (uint32_t)__builtin_ctz(~m);   // matching prefix of the 8
+              const uint32_t left = nicec - len;
+              len += run < left ? run : left;
+              go = run == 8 && len < nicec;
             }
-            const uint64_t nm = __ballot(cand && len >= nicec);
-            if (nm) {
-              const int wl = __ffsll((unsigned long long)nm) - 1;
-              win = (uint32_t)__builtin_amdgcn_readlane((int)q, wl);
-              best = uni(common_len(in, win, z.p, nicec, cap, lane));   // full length of the winner
-              won = true;
-              break;
-            }
-            uint32_t mx = cand ? len : 0u;
-            for (int d = 32; d >= 1; d >>= 1) { const uint32_t o = __shfl_xor(mx, d, 64); mx = mx > o ? mx : o; }
-            mx = uni(mx);
-            if (mx > best) {
-              const uint64_t xm = __ballot(cand && len == mx);
-              win = (uint32_t)__builtin_amdgcn_readlane((int)q, __ffsll((unsigned long long)xm) - 1);
-              best = mx;
-              won = true;
-            }
-            done = examined >= z.chain || slane < 64 || flane < 64;
-            top -= 64;
           }
-          if (hv) {
-            z.match_length = best <= z.lookahead ? best : z.lookahead;
-            if (won) z.match_start = win;
+          const uint64_t nm = __ballot(cand && len >= nicec);
+          if (nm) {
+            const int wl = __ffsll((unsigned long long)nm) - 1;
+            win = (uint32_t)__builtin_amdgcn_readlane((int)qc, wl);
+            best = uni(common_len(in, win, f, nicec, cap, lane));   // full length of the winner
+            won = true;
+            break;
           }
-          cyc_fb += STEP_CLOCK() - cf0;
+          uint32_t mx = cand ? len : 0u;
+          for (int d = 32; d >= 1; d >>= 1) { const uint32_t o2 = __shfl_xor(mx, d, 64); mx = mx > o2 ? mx : o2; }
+          mx = uni(mx);
+          if (mx > best) {
+            const uint64_t xm = __ballot(cand && len == mx);
+            win = (uint32_t)__builtin_amdgcn_readlane((int)qc, __ffsll((unsigned long long)xm) - 1);
+            best = mx;
+            won = true;
+          }
+          done = examined >= z.chain || slane < 64 || flane < 64;
+          top -= 64;
+        }
+        if (hv && won) {
+          ml = best <= la ? best : la;
+          ms = win;
         }
       }
-      cyc_lookup += STEP_CLOCK() - cl0;
-      bool bflush;
-      if (z.match_length >= 3) {
-        const uint32_t ml = z.match_length;
-        bflush = tally_dist((uint32_t)(z.p - z.match_start), ml - 3);
-        z.lookahead -= ml;
-        if (ml <= z.lazy && z.lookahead >= 3) {
-          for (uint32_t k = 1; k < ml; k++) insr.set(z.p + k);
-        } else {
-          // p+1 .. p+ml-1 are not inserted: record them per hash slot
-          for (uint32_t k0 = 1; k0 < ml; k0 += 64) {
-            const uint32_t q = z.p + k0 + lane;
-            if (k0 + lane < ml && q + 3 <= z.n) {
-              const uint32_t hq = (((uint32_t)in[q] << (2 * hshift)) ^ ((uint32_t)in[q + 1] << hshift) ^ in[q + 2]) & hmask;
-              atomicMax(&holes[hq & (HOLE_SLOTS - 1)], (uint32_t)(q + 1));
-            }
-          }
-        }
-        z.p += ml;
-        z.match_length = 0;
-      } else {
-        bflush = tally_lit(e.x & 0xffu);
-        z.lookahead--;
-        z.p++;
-      }
-      if (bflush) {
+      cyc_fb += STEP_CLOCK() - cf0;
+      const uint32_t step = ml >= 3 ? ml : 1u;
+      span_set(f, f + step, [&](uint32_t p, uint32_t& y, uint32_t& Ly) { y = f; Ly = ml >= 3 ? ml : 0u; });
+      const bool full = tally1(ml >= 3 ? (((f - ms) << 8) | (ml - 3u)) : (uint32_t)in[f]);
+      if (full) {
+        z.p = f + step;
+        z.S = Sf;
         FLUSH(0);
         state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
         if (state != ~0u) break;
       }
+      q = f + step;
+    }
+    if (state == ~0u) {
+      z.p = n;
+      z.S = S_iter(Sb, n);
     }
   } else {
     // deflate_slow (Z/deflate.c:1730-1853), lane-parallel.
@@ -1412,22 +1476,6 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     // symbols are tallied lane-parallel in position order, which is deflate_slow's tally order.
     // Window slides are a function of the iteration position (fill_window runs at the top of the
     // iteration when lookahead < MIN_LOOKAHEAD), so each lane evaluates them itself.
-    LDS uint64_t* ring = (LDS uint64_t*)shm.ring;    // match-table entries, position & (RING_SLOW - 1)
-    const GLOBAL uint64_t* Rt = (const GLOBAL uint64_t*)(A.R + tr.r_off);
-    const uint32_t n = z.n, wsz = z.wsize, maxd = z.maxdist, xlim = (uint32_t)tr.x_lim;
-    auto S_iter = [&](uint32_t S0, uint32_t q) -> uint32_t {   // S at an iteration at q >= one with S0
-      uint32_t Sx = S0;
-#pragma unroll
-      for (int i = 0; i < 2; i++) {
-        const bool exh = n <= Sx + 2u * wsz;
-        const bool slide = exh ? (q + LOOKMIN > n && q >= Sx + wsz + maxd) : (q > Sx + wsz + maxd);
-        if (slide) Sx += wsz;
-      }
-      return Sx;
-    };
-    // ring: chunks of 64 entries below `hi` are resident; the chunk at `hi` is in flight in pf
-    uint32_t hi = 0;
-    uint64_t pf = n ? Rt[lane] : 0ull;
     uint32_t q = 0, ma = 0, Sb = 0, prevb = 0;   // canonical position, pending literal, S there, byte q-1
     bool need = false;
     while (q < n) {
