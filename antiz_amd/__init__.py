@@ -42,7 +42,7 @@ class Stats(C.Structure):
                [("k_match_ms", C.c_double)] + \
                [(k, u64) for k in ("k_match_launches", "k_match_positions", "n_trials_rerun", "n_fast_fallbacks",
                                    "trial_cyc_total", "trial_cyc_tree", "trial_cyc_emit", "trial_blocks",
-                                   "trial_cyc_lookup", "trial_cyc_fallback", "trial_symbols",
+                                   "trial_cyc_heap", "trial_cyc_fallback", "trial_symbols",
                                    "n_trials_speculative", "n_reinflated")]
 
     def as_dict(self):

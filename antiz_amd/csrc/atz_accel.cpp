@@ -784,7 +784,13 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
 // Match-table prefix for a trial that may stop early: enough positions for the blocks that decide
 // the shortcut (~3 positions per symbol, lit_bufsize symbols per block); the rest on demand.
 static uint64_t match_prefix(uint64_t n, int memlevel) {
-  uint64_t x = std::max<uint64_t>(8192, 6ull << (memlevel + 6));
+  static uint64_t pmin = 1024, pmul4 = 8;   // 2 * lit_bufsize positions (measured on C4: 1.5x-6x)
+  static bool init = false;
+  if (!init) {   // ATZ_XLIM=min,mul*4 (tuning)
+    init = true;
+    if (const char* e = std::getenv("ATZ_XLIM")) std::sscanf(e, "%llu,%llu", (unsigned long long*)&pmin, (unsigned long long*)&pmul4);
+  }
+  uint64_t x = std::max<uint64_t>(pmin, (pmul4 << (memlevel + 6)) >> 2);
   return std::min(n, x);
 }
 
@@ -903,7 +909,7 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
 
 static double g_t_list = 0, g_t_chains = 0, g_t_trials = 0, g_t_apply = 0;
 // per trial kind (stored/fast/slow) x level: count, cycles total/tree/emit/lookup/fallback, parsed bytes, symbols
-static uint64_t g_kind[3][10][8];
+static uint64_t g_kind[3][10][14];
 static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
   auto t0 = std::chrono::steady_clock::now();
   g_t_list = g_t_chains = g_t_trials = g_t_apply = 0;
@@ -981,11 +987,12 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
         c->stats.n_fast_fallbacks += r.fallbacks;
         c->stats.trial_cyc_total += r.cyc_total; c->stats.trial_cyc_tree += r.cyc_tree;
         c->stats.trial_cyc_emit += r.cyc_emit; c->stats.trial_blocks += r.blocks;
-        c->stats.trial_cyc_lookup += r.cyc_lookup; c->stats.trial_cyc_fallback += r.cyc_fallback;
+        c->stats.trial_cyc_heap += r.cyc_heap; c->stats.trial_cyc_fallback += r.cyc_fallback;
         c->stats.trial_symbols += r.symbols;
         uint64_t* gk = g_kind[k][tr[k][q].clevel];
-        gk[0]++; gk[1] += r.cyc_total; gk[2] += r.cyc_tree; gk[3] += r.cyc_emit; gk[4] += r.cyc_lookup;
-        gk[5] += r.cyc_fallback; gk[6] += r.parsed; gk[7] += r.symbols;
+        gk[0]++; gk[1] += r.cyc_total; gk[2] += r.cyc_tree; gk[3] += r.cyc_emit; gk[4] += r.cyc_heap;
+        gk[5] += r.cyc_fallback; gk[6] += r.parsed; gk[7] += r.symbols; gk[8] += r.cyc_scan; gk[9] += r.cyc_send;
+        for (int i = 0; i < 4; i++) gk[10 + i] += r.cyc_sec[i];
         // trial input read + compare read (bytes emitted and compared against the original)
         c->stats.k_trial_alg_bytes += c->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
       }
@@ -1099,10 +1106,12 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
       for (int l = 0; l < 10; l++) {
         const uint64_t* gk = g_kind[k][l];
         if (!gk[0]) continue;
-        std::fprintf(stderr, "atz: kind %d level %d: trials %llu cyc %.3fT (tree %.3fT emit %.3fT lookup %.3fT fb %.3fT) "
+        std::fprintf(stderr, "atz: kind %d level %d: trials %llu cyc %.3fT (tree %.3fT [heap %.3fT scan %.3fT] emit %.3fT [send %.3fT] fb %.3fT) "
                      "parsed %.1f MB syms %.1f M cyc/byte %.0f\n", k, l, (unsigned long long)gk[0], gk[1] / 1e12,
-                     gk[2] / 1e12, gk[3] / 1e12, gk[4] / 1e12, gk[5] / 1e12, gk[6] / 1e6, gk[7] / 1e6,
+                     gk[2] / 1e12, gk[4] / 1e12, gk[8] / 1e12, gk[3] / 1e12, gk[9] / 1e12, gk[5] / 1e12, gk[6] / 1e6, gk[7] / 1e6,
                      gk[6] ? (double)gk[1] / gk[6] : 0.0);
+        std::fprintf(stderr, "atz:     window phases: refill %.3fT steps %.3fT path %.3fT tally+flush %.3fT\n",
+                     gk[10] / 1e12, gk[11] / 1e12, gk[12] / 1e12, gk[13] / 1e12);
       }
   for (size_t s = 0; s < n; s++) {
     StreamState& st = ss[s];

@@ -73,7 +73,9 @@ struct TrialRes {
   uint64_t fallbacks;   // fast levels: steps that walked the chain because a skipped position was on it
   uint64_t cyc_total, cyc_tree, cyc_emit, blocks;   // diagnostics: shader clocks in the trial / tree
                                                     // construction / block emission, blocks flushed
-  uint64_t cyc_lookup, cyc_fallback;                // match lookup in the parse / fast-level chain walks
+  uint64_t cyc_heap, cyc_fallback;                  // tree heap steps (ATZ_STEP_CLOCKS) / fast-level exact walks
+  uint64_t cyc_scan, cyc_send;                      // scan_tree / send_tree (ATZ_STEP_CLOCKS)
+  uint64_t cyc_sec[4];                              // parse window phases: refill / steps / path / tally (ATZ_STEP_CLOCKS)
 };
 enum : uint32_t {
   TR_FULL = 0,        // full output produced and compared: ident valid

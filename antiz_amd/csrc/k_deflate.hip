@@ -518,8 +518,10 @@ struct BitOut {
   uint64_t eq_sc;    // equal bytes at positions < min(pos, shortcut)
   int overflow;
   uint64_t cyc_tree, cyc_emit, blocks;   // diagnostics (shader clock)
+  uint64_t cyc_heap, cyc_scan, cyc_send;   // diagnostics (ATZ_STEP_CLOCKS)
 };
 
+static constexpr uint32_t STAGE_WORDS = 196;   // 64 * SYM_PER_LANE * 48 / 32 + 2 (+ pad)
 struct TrialShared {
   BitOut b;              // output / compare state of the trial (in LDS: the flush helpers take it by LDS reference)
   uint32_t lfreq[NLC];
@@ -529,7 +531,7 @@ struct TrialShared {
   uint16_t bcode[NBLC]; uint8_t blen[NBLC + 2];
   uint32_t bfreq[NBLC];
   TreeWork w;
-  uint32_t stage[112];   // bit-packing staging words (64 symbols x <=48 bits + carry)
+  uint32_t stage[STAGE_WORDS];   // bit-packing staging words (128 symbols x <= 48 bits + carry)
 };
 
 struct TrialSharedFast {
@@ -568,24 +570,31 @@ __device__ inline uint64_t wsum64(uint64_t v) {
   return v;
 }
 
-// write `nb` bytes (lane k supplies byte k via getter semantics: bytes[] in LDS words) -- used by
-// both scalar and lane-parallel emitters.  Compares against the original on the fly.
+// write the `nb` bytes of the staging words (byte k = byte k & 3 of stage[k >> 2]) and compare them
+// with the original on the fly.  Lane w takes word w: its 4 output bytes and 4 original bytes are
+// independent accesses, all in flight together.
 __device__ inline void emit_bytes_from_stage(LDS BitOut& b, const LDS uint32_t* stage, uint32_t nb, int lane) {
-  uint64_t eqa = 0, eqs = 0;
-  for (uint32_t k = lane; k < nb; k += 64) {
-    uint8_t x = (uint8_t)(stage[k >> 2] >> (8 * (k & 3)));
-    uint64_t at = b.pos + k;
-    if (at < b.cap) b.out[at] = x;
-    if (at < b.clen) {
-      bool e = b.orig[at] == x;
-      eqa += e;
-      if (at < b.shortcut) eqs += e;
+  uint32_t eqa = 0, eqs = 0;
+  const uint64_t pos = b.pos, cap = b.cap, clen = b.clen, sc = b.shortcut;
+  for (uint32_t w = (uint32_t)lane; 4 * w < nb; w += 64) {
+    const uint32_t word = stage[w];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint32_t k = 4 * w + j;
+      const uint8_t x = (uint8_t)(word >> (8 * j));
+      const uint64_t at = pos + k;
+      if (k < nb && at < cap) b.out[at] = x;
+      if (k < nb && at < clen) {
+        const uint32_t e = b.orig[at] == x ? 1u : 0u;
+        eqa += e;
+        if (at < sc) eqs += e;
+      }
     }
   }
   b.eq_all += wsum64(eqa);
   b.eq_sc += wsum64(eqs);
-  if (b.pos + nb > b.cap) b.overflow = 1;
-  b.pos += nb;
+  if (pos + nb > cap) b.overflow = 1;
+  b.pos = pos + nb;
 }
 
 // scalar emission (block headers, tree descriptions): bits accumulate in bb; whole bytes go out in
@@ -623,21 +632,36 @@ __device__ inline void windup(LDS BitOut& b, LDS uint32_t* stage, int lane) {  /
 // is one compare of key >> 10 and a sift-down level is one ds_read2 of the sibling pair.
 __device__ __forceinline__ uint32_t tkey(uint32_t f, uint32_t d, uint32_t n) { return (f << 15) | (d << 10) | n; }
 
-// pqdownheap (Z/trees.c:453-476)
-__device__ __forceinline__ void pq_down(LDS uint32_t* heap, int heap_len, int k) {
+// pqdownheap (Z/trees.c:453-476).  One lane-parallel LDS read gathers the 62 descendants of k
+// within 5 levels (lanes [2^t - 2, 2^(t+1) - 2) hold level t); the sift path through them is
+// chosen with v_readlane, so a sift-down costs one LDS round trip per 5 levels, not one per level.
+__device__ __forceinline__ void pq_down(LDS uint32_t* heap, int heap_len, int k, int lane) {
   const uint32_t v = uni(heap[k]);
   const uint32_t vk = v >> 10;
-  int j = k << 1;
-  while (j <= heap_len) {
-    uint32_t hj = uni(heap[j]);
-    if (j < heap_len) {
-      const uint32_t hj1 = uni(heap[j + 1]);
-      if ((hj1 >> 10) <= (hj >> 10)) { j++; hj = hj1; }
+  const int t_l = 31 - __builtin_clz((uint32_t)lane + 2u);   // level of this lane (6 for lanes 62, 63)
+  const int off_l = lane + 2 - (1 << t_l);
+  for (;;) {
+    if (2 * k > heap_len) break;
+    const int idx = (k << t_l) + off_l;
+    const uint32_t g = (t_l <= 5 && idx <= heap_len) ? heap[idx] : 0xffffffffu;
+    int p = k;
+    bool stop = false;
+#pragma unroll
+    for (int t = 1; t <= 5; t++) {
+      int j = p << 1;
+      if (j > heap_len) { stop = true; break; }
+      const int lj = (1 << t) - 2 + (j - (k << t));
+      uint32_t hj = (uint32_t)__builtin_amdgcn_readlane((int)g, lj);
+      if (j < heap_len) {
+        const uint32_t hj1 = (uint32_t)__builtin_amdgcn_readlane((int)g, lj + 1);
+        if ((hj1 >> 10) <= (hj >> 10)) { j++; hj = hj1; }
+      }
+      if (vk <= (hj >> 10)) { stop = true; break; }
+      heap[p] = hj;
+      p = j;
     }
-    if (vk <= (hj >> 10)) break;
-    heap[k] = hj;
-    k = j;
-    j <<= 1;
+    k = p;
+    if (stop) break;
   }
   heap[k] = v;
 }
@@ -646,7 +670,7 @@ __device__ __forceinline__ void pq_down(LDS uint32_t* heap, int heap_len, int k)
 // in w.len, bl_count in w.bl_count; opt_len / static_len accumulate as in zlib.  Returns max_code.
 __device__ __noinline__ int build_tree(LDS TreeWork& w, int elems, int max_length, const CONSTANT uint8_t* xbits,
                                        int xbase, const CONSTANT uint8_t* stlen, uint64_t& opt_len,
-                                       uint64_t& static_len, int lane) {
+                                       uint64_t& static_len, LDS uint64_t& cyc_heap, int lane) {
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   LDS uint32_t* const heap = w.heap;
   // leaves enter heap[1..] in increasing symbol order (Z/trees.c:631-638)
@@ -668,7 +692,8 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, int elems, int max_lengt
     opt_len--;
     if (stlen) static_len -= stlen[node];
   }
-  for (int n = heap_len / 2; n >= 1; n--) pq_down(heap, heap_len, n);
+  const uint64_t ch0 = STEP_CLOCK();
+  for (int n = heap_len / 2; n >= 1; n--) pq_down(heap, heap_len, n, lane);
   // combine the two least frequent nodes until one is left (Z/trees.c:663-690)
   int heap_max = HEAPN;
   uint32_t node = (uint32_t)elems;
@@ -676,7 +701,7 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, int elems, int max_lengt
     const uint32_t kn = uni(heap[1]);
     heap[1] = uni(heap[heap_len]);
     heap_len--;
-    pq_down(heap, heap_len, 1);
+    pq_down(heap, heap_len, 1, lane);
     const uint32_t km = uni(heap[1]);
     const uint32_t dn = (kn >> 10) & 31u, dm = (km >> 10) & 31u;
     if (lane == 0) {
@@ -689,9 +714,10 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, int elems, int max_lengt
     }
     heap[1] = tkey((kn >> 15) + (km >> 15), (dn >= dm ? dn : dm) + 1u, node);
     node++;
-    pq_down(heap, heap_len, 1);
+    pq_down(heap, heap_len, 1, lane);
   } while (heap_len >= 2);
   const uint32_t root = uni(heap[1]) & 1023u;
+  if (lane == 0) cyc_heap += STEP_CLOCK() - ch0;
   --heap_max;
   if (lane == 0) heap[heap_max] = root;
   // gen_bitlen: every node's depth by pointer jumping over dad[] (lane-parallel, depth <= 31 so
@@ -867,61 +893,77 @@ __device__ __forceinline__ uint32_t dcode_extra(uint32_t d) { return d < 2 ? 0u 
 __device__ __forceinline__ uint32_t dcode_base(uint32_t d) { return d < 2 ? d : ((2 + (d & 1)) << dcode_extra(d)); }  // base_dist[d]
 
 
-// Lane-parallel compress_block (Z/trees.c:1060-1105): 64 symbols per step.
+// Lane-parallel compress_block (Z/trees.c:1060-1105): 128 symbols per step, two per lane (one
+// 8-byte load), bit offsets by a wave prefix sum, words assembled with LDS atomics.
+static constexpr uint32_t SYM_PER_LANE = 2;
+template <typename C16, typename C8>
+__device__ __forceinline__ void sym_bits(uint32_t sy, bool valid, bool end, C16 lc, C8 ll, C16 dc, C8 dl,
+                                         uint64_t& v, uint32_t& nb) {
+  v = 0; nb = 0;
+  if (valid) {
+    uint32_t dist = sy >> 8;
+    const uint32_t c = sy & 0xff;
+    if (dist == 0) {
+      v = lc[c]; nb = ll[c];
+    } else {
+      const uint32_t code = len_code(c);
+      v = lc[code + 257]; nb = ll[code + 257];
+      const uint32_t xe = lcode_extra(code);
+      if (xe) { v |= (uint64_t)(c - lcode_base(code)) << nb; nb += xe; }
+      dist--;
+      const uint32_t dcd = dist_code(dist);
+      v |= (uint64_t)dc[dcd] << nb; nb += dl[dcd];
+      const uint32_t xd = dcode_extra(dcd);
+      if (xd) { v |= (uint64_t)(dist - dcode_base(dcd)) << nb; nb += xd; }
+    }
+  } else if (end) {
+    v = lc[256]; nb = ll[256];   // END_BLOCK
+  }
+}
+__device__ __forceinline__ void stage_or(LDS uint32_t* stage, uint32_t off, uint64_t v, uint32_t nb) {
+  if (!nb) return;
+  const uint32_t wi = off >> 5, sh = off & 31;
+  const uint64_t lo = v << sh;                       // bits 0..63 of the shifted value
+  const uint32_t hi = sh ? (uint32_t)(v >> (64 - sh)) : 0;
+  __atomic_fetch_or(&stage[wi], (uint32_t)lo, __ATOMIC_RELAXED);
+  if ((uint32_t)(lo >> 32)) __atomic_fetch_or(&stage[wi + 1], (uint32_t)(lo >> 32), __ATOMIC_RELAXED);
+  if (hi) __atomic_fetch_or(&stage[wi + 2], hi, __ATOMIC_RELAXED);
+}
 template <typename C16, typename C8>
 __device__ void compress_block(LDS BitOut& b, LDS TrialShared& s, const GLOBAL uint32_t* syms, uint32_t nsym,
                                C16 lc, C8 ll, C16 dc, C8 dl,
                                int lane) {
-  // the symbols were stored by lane 0 during the parse: order those HBM stores before the reads
+  // the symbols were stored by other lanes during the parse: order those HBM stores before the reads
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-  for (uint32_t base = 0; base <= nsym; base += 64) {
-    uint32_t k = base + lane;
-    uint64_t v = 0;
-    uint32_t nb = 0;
-    if (k < nsym) {
-      uint32_t sy = syms[k];
-      uint32_t dist = sy >> 8, c = sy & 0xff;
-      if (dist == 0) {
-        v = lc[c]; nb = ll[c];
-      } else {
-        uint32_t code = len_code(c);
-        v = lc[code + 257]; nb = ll[code + 257];
-        uint32_t xe = lcode_extra(code);
-        if (xe) { v |= (uint64_t)(c - lcode_base(code)) << nb; nb += xe; }
-        dist--;
-        uint32_t dcd = dist_code(dist);
-        v |= (uint64_t)dc[dcd] << nb; nb += dl[dcd];
-        uint32_t xd = dcode_extra(dcd);
-        if (xd) { v |= (uint64_t)(dist - dcode_base(dcd)) << nb; nb += xd; }
-      }
-    } else if (k == nsym) {
-      v = lc[256]; nb = ll[256];   // END_BLOCK
-    }
+  for (uint32_t base = 0; base <= nsym; base += 64 * SYM_PER_LANE) {
+    const uint32_t k0 = base + SYM_PER_LANE * (uint32_t)lane;
+    // symbol buffers are 256-byte aligned with >= 4 KiB slack after the last one: the pair load
+    // may read past nsym (those values are not used)
+    const uint64_t sp = *(const GLOBAL uint64_t*)(syms + k0);
+    uint64_t v0, v1;
+    uint32_t n0, n1;
+    sym_bits((uint32_t)sp, k0 < nsym, k0 == nsym, lc, ll, dc, dl, v0, n0);
+    sym_bits((uint32_t)(sp >> 32), k0 + 1 < nsym, k0 + 1 == nsym, lc, ll, dc, dl, v1, n1);
+    const uint32_t nb = n0 + n1;
     // exclusive prefix sum of bit lengths
     uint32_t incl = nb;
     for (int d = 1; d < 64; d <<= 1) {
-      uint32_t t = __shfl_up(incl, d, 64);
+      const uint32_t t = __shfl_up(incl, d, 64);
       if (lane >= d) incl += t;
     }
-    uint32_t total = __shfl(incl, 63, 64);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (total == 0) break;
     // stage words: word 0..1 seeded with the pending bits
-    for (int i = lane; i < 112; i += 64) s.stage[i] = 0;
+    for (int i = lane; i < (int)STAGE_WORDS; i += 64) s.stage[i] = 0;
     if (lane == 0) { s.stage[0] = (uint32_t)b.bb; s.stage[1] = (uint32_t)(b.bb >> 32); }
-    uint32_t off = b.bc + incl - nb;
-    if (nb) {
-      uint32_t wi = off >> 5, sh = off & 31;
-      uint64_t lo = v << sh;                       // bits 0..63 of the shifted value
-      uint32_t hi = sh ? (uint32_t)(v >> (64 - sh)) : 0;
-      __atomic_fetch_or(&s.stage[wi], (uint32_t)lo, __ATOMIC_RELAXED);
-      if ((uint32_t)(lo >> 32)) __atomic_fetch_or(&s.stage[wi + 1], (uint32_t)(lo >> 32), __ATOMIC_RELAXED);
-      if (hi) __atomic_fetch_or(&s.stage[wi + 2], hi, __ATOMIC_RELAXED);
-    }
-    uint32_t all = b.bc + total;
-    uint32_t full = all >> 3;
+    const uint32_t off = b.bc + incl - nb;
+    stage_or(s.stage, off, v0, n0);
+    stage_or(s.stage, off + n0, v1, n1);
+    const uint32_t all = b.bc + total;
+    const uint32_t full = all >> 3;
     emit_bytes_from_stage(b, s.stage, full, lane);
-    uint32_t rem = all & 7;
-    uint32_t lastw = s.stage[full >> 2];
+    const uint32_t rem = all & 7;
+    const uint32_t lastw = s.stage[full >> 2];
     b.bb = rem ? ((lastw >> (8 * (full & 3))) & 0xff) & ((1u << rem) - 1) : 0;
     b.bc = rem;
   }
@@ -995,20 +1037,22 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, 
     // literal/length tree
     for (int i = lane; i < NLC; i += 64) s.w.freq[i] = (uint16_t)s.lfreq[i];
     lmax = build_tree(s.w, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
-                      opt_len, static_len, lane);
+                      opt_len, static_len, b.cyc_heap, lane);
     gen_codes(s.w, lmax, s.lcode, s.llen, lane);
     for (int i = lmax + 1 + lane; i < NLC + 2; i += 64) s.llen[i] = 0;
     // distance tree
     for (int i = lane; i < NDC; i += 64) s.w.freq[i] = (uint16_t)s.dfreq[i];
     dmax = build_tree(s.w, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
-                      opt_len, static_len, lane);
+                      opt_len, static_len, b.cyc_heap, lane);
     gen_codes(s.w, dmax, s.dcode, s.dlen, lane);
     for (int i = dmax + 1 + lane; i < NDC + 2; i += 64) s.dlen[i] = 0;
     // bit length tree
     for (int i = lane; i < NBLC; i += 64) s.bfreq[i] = 0;
+    const uint64_t cs0 = STEP_CLOCK();
     if (lane == 0) { scan_tree(s.bfreq, s.llen, lmax); scan_tree(s.bfreq, s.dlen, dmax); }
+    b.cyc_scan += STEP_CLOCK() - cs0;
     for (int i = lane; i < NBLC; i += 64) s.w.freq[i] = (uint16_t)s.bfreq[i];
-    int bmax = build_tree(s.w, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, opt_len, static_len, lane);
+    int bmax = build_tree(s.w, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, opt_len, static_len, b.cyc_heap, lane);
     gen_codes(s.w, bmax, s.bcode, s.blen, lane);
     for (int i = bmax + 1 + lane; i < NBLC + 2; i += 64) s.blen[i] = 0;
     for (max_blindex = NBLC - 1; max_blindex >= 3; max_blindex--)
@@ -1054,8 +1098,10 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, 
     put_bits(b, s.stage, (uint32_t)(dcodes - 1), 5, lane);
     put_bits(b, s.stage, (uint32_t)(blcodes - 4), 4, lane);
     for (int r = 0; r < blcodes; r++) put_bits(b, s.stage, s.blen[bl_order((uint32_t)r)], 3, lane);
+    const uint64_t cs0 = STEP_CLOCK();
     send_tree(b, s, s.llen, lcodes - 1, lane);
     send_tree(b, s, s.dlen, dcodes - 1, lane);
+    b.cyc_send += STEP_CLOCK() - cs0;
     flush_bits_bytes(b, s.stage, lane);
     compress_block(b, s, syms, last_lit, (const LDS uint16_t*)s.lcode, (const LDS uint8_t*)s.llen,
                    (const LDS uint16_t*)s.dcode, (const LDS uint8_t*)s.dlen, lane);
@@ -1087,6 +1133,71 @@ __device__ inline uint32_t early_exit(const LDS BitOut& b, const SweepOpts& o, u
   return ~0u;
 }
 
+// The parse path through a window of 64 lanes (lane i = position wb + i).  Lane i's node kind:
+// Am bit = a step without a match (the path goes on at i + 1: runs of such lanes are one hop to the
+// run's end), Nm bit = the node needs match-table entries not built yet; otherwise `rel` holds the
+// next node's offset from wb (>= 64: beyond the window).  The scalar unit only chains readlanes
+// through the hop starts H; which lanes lie on the path is then derived in lanes.
+struct WinPath {
+  uint64_t H;       // hop starts (path nodes where a hop begins)
+  uint32_t end;     // offset of the position after the path (the next canonical position)
+  bool need;        // the path stops at a node that needs more match-table entries (at `end`)
+};
+__device__ __forceinline__ uint32_t run_end_rel(uint64_t Am, int lane) {   // first lane > lane not in Am
+  const uint64_t above = lane == 63 ? 0ull : (Am >> (lane + 1));
+  return (uint32_t)lane + 1u + (uint32_t)__builtin_ctzll(~above);
+}
+__device__ __forceinline__ WinPath follow_path(uint32_t rel, uint64_t Nm, uint32_t lim) {
+  WinPath w;
+  uint64_t H = 0;
+  uint32_t i = 0;
+  while (i < lim) {   // lim = min(64, n - wb); rel of a need lane is 0xffff
+    H |= 1ull << i;
+    i = (uint32_t)__builtin_amdgcn_readlane((int)rel, (int)i);
+  }
+  w.need = (H & Nm) != 0;
+  if (w.need) {   // the loop stopped right after entering the need node
+    i = 63u - (uint32_t)__builtin_clzll(H & Nm);
+    H &= ~Nm;
+  }
+  w.H = H;
+  w.end = i;
+  return w;
+}
+// lane's place on the path: on it, and whether a literal is pending when the path reaches it
+// (only meaningful for hop starts and run members; ma_in: pending literal at the window start)
+__device__ __forceinline__ void path_lane(const WinPath& w, uint64_t Am, uint32_t ma_in, int lane, bool& onp,
+                                          uint32_t& mab) {
+  const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);   // lanes <= lane
+  const uint64_t hb = w.H & le;
+  onp = false;
+  mab = 0;
+  if (hb) {
+    const int h = 63 - __builtin_clzll(hb);
+    if (h == lane) {
+      onp = true;
+      const uint64_t hs = w.H & (le >> 1);   // hop starts below
+      mab = hs ? (uint32_t)((Am >> (63 - __builtin_clzll(hs))) & 1ull) : ma_in;
+    } else if ((Am >> h) & 1ull) {   // member of the run starting at h: all lanes h..lane in Am
+      const uint64_t seg = le & ~((1ull << h) - 1ull);
+      onp = (~Am & seg) == 0;
+      mab = 1;
+    }
+  }
+}
+// exclusive prefix sum of small per-lane counts over the wave by ballot bit planes (no LDS)
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t cnt, uint64_t lt, uint32_t& total) {
+  uint32_t o = 0, T = 0;
+  for (uint32_t bit = 0; bit < 32; bit++) {
+    const uint64_t m = __ballot((cnt >> bit) & 1u);
+    o += (uint32_t)__popcll(m & lt) << bit;
+    T += (uint32_t)__popcll(m) << bit;
+    if (!__ballot(cnt >> (bit + 1))) break;
+  }
+  total = T;
+  return o;
+}
+
 template <int KIND, typename SH>
 __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   LDS TrialShared& s = *(LDS TrialShared*)&shm.t;
@@ -1113,6 +1224,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   b.eq_all = 0; b.eq_sc = 0; b.overflow = 0;
   uint32_t* const syms = A.syms + tr.sym_off;
   b.cyc_tree = b.cyc_emit = b.blocks = 0;
+  b.cyc_heap = b.cyc_scan = b.cyc_send = 0;
   const uint64_t cstart = clock64();
   for (int i = lane; i < NLC; i += 64) s.lfreq[i] = 0;
   for (int i = lane; i < NDC; i += 64) s.dfreq[i] = 0;
@@ -1125,7 +1237,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     z.block_start = z.p;
   };
   uint32_t state = ~0u;
-  uint64_t fallbacks = 0, cyc_lookup = 0, cyc_fb = 0;
+  uint64_t fallbacks = 0, cyc_fb = 0;
+  uint64_t csec[4] = {0, 0, 0, 0};   // diagnostics (ATZ_STEP_CLOCKS)
   // zlib header (Z/deflate.c:738-759)
   {
     uint32_t header = (8u + ((uint32_t)(tr.window - 8) << 4)) << 8;
@@ -1246,12 +1359,15 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     bool need = false;
     while (q < n) {
       const uint32_t wb = q, bal = wb & ~63u;
+      uint64_t t0 = STEP_CLOCK();
       while (hi < bal + RING_SLOW) {
         ring[(hi + lane) & (RING_SLOW - 1)] = pf;
         hi += 64;
         if (hi < n) pf = Rt[hi + lane];
       }
       Sb = S_iter(Sb, wb);
+      if (ATZ_STEP_CLOCKS) { (void)ring[wb & (RING_SLOW - 1)]; __builtin_amdgcn_s_waitcnt(0); }
+      uint64_t t1 = STEP_CLOCK(); csec[0] += t1 - t0; t0 = t1;
       // ---- the table's step at x = wb + lane: wt 0 none (x >= n), 1 literal, 2 match, 3 needs R >= x_lim
       const uint32_t x = wb + lane;
       uint32_t wt = 0, L = 0, D = 0, ex = 0, ey = 0, Sx = Sb;
@@ -1273,25 +1389,18 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       }
       // ---- follow the parse path through the window
       const uint64_t Am = __ballot(wt == 1), Nm = __ballot(wt == 3);
-      uint64_t P = 0;
-      uint32_t qn = wb, last = wb;
-      while (qn < wb + 64 && qn < n) {
-        const uint32_t i = qn - wb;
-        const uint64_t bit = 1ull << i;
-        if (Nm & bit) { need = true; break; }
-        P |= bit;
-        last = qn;
-        if (Am & bit) {   // a run of literals
-          const uint64_t rest = ~(Am >> i);
-          const uint32_t k = rest ? (uint32_t)__builtin_ctzll(rest) : 64u - i;
-          P |= (k >= 64 ? ~0ull : ((1ull << k) - 1ull)) << i;
-          qn += k;
-          last = qn - 1;
-        } else {
-          qn += (uint32_t)__builtin_amdgcn_readlane((int)L, (int)i);
-        }
-      }
+      t1 = STEP_CLOCK(); csec[1] += t1 - t0; t0 = t1;
+      const uint32_t rel = wt == 1 ? run_end_rel(Am, lane) : wt == 2 ? (uint32_t)lane + L : 0xffffu;
+      const WinPath wp = follow_path(rel, Nm, n - wb < 64 ? n - wb : 64u);
+      bool onp;
+      uint32_t mab_unused;
+      path_lane(wp, Am, 0, lane, onp, mab_unused);
+      const uint64_t P = __ballot(onp);
+      need = wp.need;
+      const uint32_t qn = wb + wp.end;
+      const uint32_t last = P ? wb + 63u - (uint32_t)__builtin_clzll(P) : wb;
       // ---- insertion state of the path, then the check of its nodes
+      t1 = STEP_CLOCK(); csec[2] += t1 - t0; t0 = t1;
       if (qn > wb)
         span_set(wb, qn, [&](uint32_t p, uint32_t& y, uint32_t& Ly) {
           const uint32_t i = p - wb;   // huge for p < wb (such lanes are outside the span)
@@ -1300,7 +1409,6 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           y = wb + yl;
           Ly = (uint32_t)__shfl((int)L, (int)yl, 64);
         });
-      const bool onp = (P >> lane) & 1ull;
       bool bad = false;
       if (onp && x + 3u <= n) {
         const uint32_t hl = holes[(ey >> 1) & (HOLE_SLOTS - 1)];
@@ -1353,6 +1461,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           base = seg_end;
         }
       }
+      t1 = STEP_CLOCK(); csec[3] += t1 - t0;
       if (state != ~0u) break;
       if (!badm) {
         if (need) { state = TR_NEED_R; z.p = qn; break; }
@@ -1480,12 +1589,15 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     bool need = false;
     while (q < n) {
       const uint32_t wb = q, bal = wb & ~63u;
+      uint64_t t0 = STEP_CLOCK();
       while (hi < bal + RING_SLOW) {
         ring[(hi + lane) & (RING_SLOW - 1)] = pf;
         hi += 64;
         if (hi < n) pf = Rt[hi + lane];
       }
       Sb = S_iter(Sb, wb);
+      if (ATZ_STEP_CLOCKS) { (void)ring[wb & (RING_SLOW - 1)]; __builtin_amdgcn_s_waitcnt(0); }
+      uint64_t t1 = STEP_CLOCK(); csec[0] += t1 - t0; t0 = t1;
       // ---- the walk from x = wb + lane: wt 0 none (x >= n), 1 no match, 2 match, 3 needs R >= x_lim
       const uint32_t x = wb + lane;
       uint32_t wt = 0, nxt = 0, c = 0, L = 0, D = 0;
@@ -1522,39 +1634,22 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       }
       // ---- follow the parse path through the window
       const uint64_t Am = __ballot(wt == 1), Nm = __ballot(wt == 3);
-      uint64_t P = 0, MAm = 0;
-      uint32_t qn = wb, man = ma;
-      while (qn < wb + 64 && qn < n) {
-        const uint32_t i = qn - wb;
-        const uint64_t bit = 1ull << i;
-        if (Nm & bit) { need = true; break; }
-        P |= bit;
-        if (man) MAm |= bit;
-        if (Am & bit) {   // a run of positions without a match: one literal each
-          const uint64_t rest = ~(Am >> i);
-          const uint32_t k = rest ? (uint32_t)__builtin_ctzll(rest) : 64u - i;
-          const uint64_t rm = (k >= 64 ? ~0ull : ((1ull << k) - 1ull)) << i;
-          P |= rm;
-          MAm |= rm & ~bit;
-          qn += k;
-          man = 1;
-        } else {
-          qn = (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)i);
-          man = 0;
-        }
-      }
+      t1 = STEP_CLOCK(); csec[1] += t1 - t0; t0 = t1;
+      const uint32_t rel = wt == 1 ? run_end_rel(Am, lane) : wt == 2 ? nxt - wb : 0xffffu;
+      const WinPath wp = follow_path(rel, Nm, n - wb < 64 ? n - wb : 64u);
+      bool onp;
+      uint32_t mab;
+      path_lane(wp, Am, ma, lane, onp, mab);
+      need = wp.need;
+      const uint32_t qn = wb + wp.end;
+      // pending literal at qn: after a run yes, after a match no
+      const uint32_t man = wp.H ? (uint32_t)((Am >> (63 - __builtin_clzll(wp.H))) & 1ull) : ma;
       // ---- tally the path's symbols: node x emits [literal x-1 if pending], literals x..m-1, match
-      const bool onp = (P >> lane) & 1ull;
-      const uint32_t mab = (uint32_t)((MAm >> lane) & 1ull);
+      t1 = STEP_CLOCK(); csec[2] += t1 - t0; t0 = t1;
       const uint32_t cnt = onp ? mab + (wt == 2 ? c + 1u : 0u) : 0u;
-      uint32_t incl = cnt;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += t;
-      }
-      const uint32_t o = incl - cnt;
-      const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      const uint64_t ltm = lane ? (~0ull >> (64 - lane)) : 0ull;
+      uint32_t T;
+      const uint32_t o = wave_excl_sum(cnt, ltm, T);
       z.nsym += T;
       uint32_t base = 0;
       while (base < T) {
@@ -1600,6 +1695,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         }
         base = seg_end;
       }
+      t1 = STEP_CLOCK(); csec[3] += t1 - t0;
       if (state != ~0u) break;
       if (need) { state = TR_NEED_R; z.p = qn; break; }
       prevb = qn > 0 ? (uint32_t)ring[(qn - 1u) & (RING_SLOW - 1)] & 0xffu : 0u;   // read when man: qn - 1 < wb + 64
@@ -1654,7 +1750,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     r.cyc_tree = b.cyc_tree;
     r.cyc_emit = b.cyc_emit;
     r.blocks = b.blocks;
-    r.cyc_lookup = cyc_lookup;
+    r.cyc_heap = b.cyc_heap;
+    r.cyc_scan = b.cyc_scan;
+    r.cyc_send = b.cyc_send;
+    for (int i = 0; i < 4; i++) r.cyc_sec[i] = csec[i];
     r.cyc_fallback = cyc_fb;
     A.res[t] = r;
   }

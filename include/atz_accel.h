@@ -70,7 +70,7 @@ typedef struct {
     uint64_t n_trials_rerun;                             /* trials run again after extending their match table */
     uint64_t n_fast_fallbacks;                           /* fast-level steps that walked a chain in the parse */
     uint64_t trial_cyc_total, trial_cyc_tree, trial_cyc_emit, trial_blocks;  /* shader clocks summed over trials */
-    uint64_t trial_cyc_lookup, trial_cyc_fallback, trial_symbols;
+    uint64_t trial_cyc_heap, trial_cyc_fallback, trial_symbols;   /* heap: ATZ_STEP_CLOCKS builds only */
     uint64_t n_trials_speculative;                       /* trials run ahead of a stream's stop and discarded */
     uint64_t n_reinflated;                               /* recorded streams inflated again (scan output not kept) */
 } atz_stats_t;
