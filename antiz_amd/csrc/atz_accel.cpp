@@ -317,6 +317,12 @@ struct Chunk {
 
 static constexpr uint64_t ARENA_SLOT = 65536;   // arena slot per scan candidate (longer outputs are re-inflated)
 
+static bool timing_on() {
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_TIMING"); v = e && *e == '1'; }
+  return v == 1;
+}
+
 static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, const std::vector<InfJob>& jobs,
                             std::vector<InfRes>& res, uint64_t arena_cap = 0) {
   res.resize(jobs.size());
@@ -340,6 +346,17 @@ static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, con
   kcollect(c);
   for (uint32_t k = 0; k < n; k++)   // bytes read + bytes written (when kept)
     c->stats.k_inflate_alg_bytes += res[k].consumed + (jobs[k].out_off == NO_OUT ? 0 : res[k].produced);
+  if (timing_on() && ATZ_INF_CLOCKS) {   // diagnostics build: clocks per job / per symbol
+    uint64_t cyc = 0, nl = 0, nm = 0, cmax = 0, outb = 0, cc = 0, cf = 0;
+    for (uint32_t k = 0; k < n; k++) {
+      cyc += res[k].cyc; nl += res[k].nlit; nm += res[k].nmatch; outb += res[k].produced;
+      cc += res[k].cyc_copy; cf += res[k].cyc_flush;
+      cmax = std::max<uint64_t>(cmax, res[k].cyc);
+    }
+    std::fprintf(stderr, "atz: k_inflate %u jobs: %.3f Gcyc, max %.2f Mcyc, lit %llu match %llu out %llu, "
+                 "%.1f cyc/symbol (copy %.3f Gcyc, flush %.3f Gcyc)\n", n, cyc / 1e9, cmax / 1e6, (unsigned long long)nl,
+                 (unsigned long long)nm, (unsigned long long)outb, (nl + nm) ? (double)cyc / (nl + nm) : 0.0, cc / 1e9, cf / 1e9);
+  }
   return 0;
 }
 
@@ -359,11 +376,6 @@ static void chunk_bytes(const uint8_t* f, const Chunk& ch, std::vector<uint8_t>&
   v.insert(v.end(), f + ch.co + 1, f + ch.co + ch.len);
 }
 
-static bool timing_on() {
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_TIMING"); v = e && *e == '1'; }
-  return v == 1;
-}
 // ATZ_TIMING=1: host phase timings on stderr
 #define TMARK(name)                                                                        \
   do {                                                                                     \

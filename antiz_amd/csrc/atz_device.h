@@ -26,6 +26,8 @@ struct InfRes {
   uint64_t consumed;  // zlib total_in at the stop
   uint64_t produced;  // zlib total_out at the stop
   uint64_t arena_off; // ARENA_OUT jobs: offset of the output slot (ARENA_NONE: none / incomplete)
+  uint64_t cyc, nlit, nmatch;  // diagnostics (ATZ_INF_CLOCKS builds): shader clocks, literals, matches
+  uint64_t cyc_copy, cyc_flush; //   clocks in match copies (incl. the stage write before) / ring flushes
 };
 
 // ---- deflate trial (k_trial) ---------------------------------------------------------------

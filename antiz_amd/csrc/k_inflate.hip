@@ -18,6 +18,9 @@ namespace atz {
 static constexpr uint32_t RING = 32768;        // history ring per wave (LDS)
 static constexpr uint32_t RMASK = RING - 1;
 static constexpr uint32_t FLUSH_AT = 16384;    // flush ring to HBM / Adler every 16 KiB
+#ifndef ATZ_INF_CLOCKS
+#define ATZ_INF_CLOCKS 0                       // 1: per-job clocks and symbol counts in InfRes
+#endif
 
 __device__ __constant__ uint16_t c_hdr_flg[6][4] = {
     {0x15, 0x53, 0x91, 0xcf}, {0x11, 0x4f, 0x8d, 0xcb}, {0x0d, 0x4b, 0x89, 0xc7},
@@ -85,8 +88,23 @@ __global__ __launch_bounds__(256) void k_find_headers(const uint8_t* __restrict_
 // ---------------------------------------------------------------------------------------------
 // k_inflate: one wavefront per job, everything inlined into the kernel so the decoder state stays
 // in (wave-uniform) SGPRs -- a by-reference state struct crossing a call would live in scratch.
+//
+// Per-symbol cost is what bounds this kernel (a serial bit-stream decode per stream), so the hot
+// loop is shaped for a short dependency chain and no memory wait per symbol:
+//  * input: a 256-byte window, one dword per lane, loaded when the previous one is used up; the
+//    refill reads one dword with readlane;
+//  * decode: canonical compare in lanes 1..15 + ballot/ff1 + two readlanes (index, 16-bit packed
+//    symbol table in 3 VGPRs);
+//  * literals go to a VGPR stage (one byte per lane, v_cndmask on lane == count) that reaches the LDS history
+//    ring with one ds_write_b8 per 64 literals or before a match copy;
+//  * while >= 64 input bits remain every field of the next symbol is available, so the fast loop
+//    drops zlib's per-field NEEDBITS checks; the last 8 bytes go through the careful path that
+//    reproduces 1.2.8's exact total_in at NEED / ERROR (oracle/ora_inflate.c).
 
 __device__ __forceinline__ uint32_t iuni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
 
 // RFC 1951 length / distance tables in closed form (an indexed __constant__ table compiles to a
 // global load per symbol).
@@ -110,23 +128,24 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   return v;
 }
 
-// Canonical Huffman code of one table: lane l (1..15) holds first-code/count/offset of length l;
-// the sorted symbols live in VGPRs (entry e in lane e & 63, register e >> 6) and are read with
-// v_readlane at a wave-uniform index -- no memory access per decoded symbol.
+// Canonical Huffman code of one table: lane l (1..15) holds first-code / count of length l and
+// ofm = offs - first (offs = index of its first symbol in the sorted list); the sorted symbols are
+// 16-bit packed in three VGPRs (entry e in dword e >> 1: lane (e >> 1) & 63, register e >> 7) and
+// read with v_readlane at a wave-uniform index -- no memory access per decoded symbol.
+// root: lane p (the next 6 stream bits, first bit in bit 0) holds (symbol << 4) | length for the
+// code of length <= 6 that p starts with, 0 if p starts a longer (or no) code.
 struct Huff {
-  uint32_t first, count, offs;
-  uint32_t s0, s1, s2, s3, s4;
+  uint32_t first, count, ofm;
+  uint32_t t0, t1, t2;
+  uint32_t root;
   int max;
   __device__ __forceinline__ uint32_t sym(uint32_t e) const {
-    uint32_t v;
-    switch (e >> 6) {
-      case 0: v = s0; break;
-      case 1: v = s1; break;
-      case 2: v = s2; break;
-      case 3: v = s3; break;
-      default: v = s4; break;
-    }
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(e & 63));
+    const uint32_t d = e >> 1;
+    uint32_t w;
+    if (d < 64) w = rl(t0, d);
+    else if (d < 128) w = rl(t1, d - 64);
+    else w = rl(t2, d - 128);
+    return (w >> ((e & 1) << 4)) & 0xffffu;
   }
 };
 
@@ -135,7 +154,7 @@ enum { R_OK = 0, R_ERR = -1, R_NEED = -2 };
 struct InfShared {
   uint8_t ring[RING];
   uint16_t lens[320];
-  uint16_t sort[320];
+  uint16_t sort[384];
 };
 
 __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_base, uint8_t* __restrict__ out_base,
@@ -147,45 +166,56 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
   const uint32_t j = blockIdx.x;
   if (j >= njobs) return;
   const InfJob job = jobs[j];
+  const uint64_t t_start = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t nlit = 0, nmatch = 0, cyc_copy = 0, cyc_flush = 0;
   uint8_t* const ring = sh.ring;
   uint16_t* const lens = sh.lens;
+  // per-lane shift of the canonical compare: lane l in 1..15 looks at the first l stream bits
+  const uint32_t lsh = (lane >= 1 && lane <= 15) ? (uint32_t)(15 - lane) : 31u;
+  // RFC 1951 base / extra bits per length symbol (lane = symbol - 257) and distance symbol
+  const uint32_t lentab = lane < 29 ? (len_base((uint32_t)lane) << 4) | len_extra((uint32_t)lane) : 0u;
+  const uint32_t disttab = lane < 30 ? (dist_base((uint32_t)lane) << 4) | dist_extra((uint32_t)lane) : 0u;
 
-  // ---- bit reader over the job's bytes: 256-byte windows staged in lane VGPRs, next one in flight
+  // ---- bit reader: 256-byte windows of the job's bytes, one dword per lane: `cur` is being read,
+  // `nxt` (the following 256 bytes) is in flight
   const uint8_t* p0 = in_base + job.in_off;
   const uintptr_t ap = reinterpret_cast<uintptr_t>(p0);
   const uint64_t skip = ap & 3;
   // global address space explicitly: a flat load would also count in lgkmcnt and make every LDS
-  // wait drain the input prefetch
+  // wait drain the input loads
   const __attribute__((address_space(1))) uint32_t* const abase =
       (const __attribute__((address_space(1))) uint32_t*)(ap - skip);
   const uint64_t skip_bits = 8 * skip;
   const uint64_t limit = 8 * (skip + job.in_len);   // bit limit (aligned coordinates)
-  uint64_t pos = 0, bb = 0, next_dw = 0, wbase = 1ull << 62;
-  uint32_t bc = 0, cw = 0, nw = 0;
-  // Bits past `limit` are never consumed (every consumption is preceded by has()), and a canonical
-  // code found within the available bits is the true code whatever follows (prefix-free), so
-  // the window is loaded unmasked -- the load stays asynchronous until its first readlane.  The
-  // input buffers carry >= 4 KiB of slack for the <= 512-byte over-read.
-  auto load_dw = [&](uint64_t dw) __attribute__((always_inline)) -> uint32_t { return abase[dw]; };
-  auto refill = [&]() __attribute__((always_inline)) {
-    while (bc <= 32) {
-      const uint64_t k = next_dw;
-      if (k - wbase >= 64) {
-        if (k - wbase < 128) { cw = nw; wbase += 64; }
-        else { wbase = k & ~63ull; cw = load_dw(wbase + lane); }
-        nw = load_dw(wbase + 64 + lane);
-      }
-      const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cw, (int)(k - wbase));
-      bb |= (uint64_t)w << bc;
-      bc += 32;
-      next_dw = k + 1;
+  uint64_t pos = 0, bb = 0, wcur = 0;   // wcur: dword index of the window in `cur`
+  uint32_t bc = 0, rk = 0;
+  uint32_t cur = 0;
+  // Bits past `limit` are never consumed (every consumption is preceded by a bounds check or by
+  // the fast loop's 64-bit margin), and a canonical code found within the available bits is the
+  // true code whatever follows (prefix-free), so windows are loaded unmasked.  The input buffers
+  // carry >= 4 KiB of slack for the <= 256-byte over-read.
+  // One dword into the bit buffer (bc <= 32 on entry).  The next 256-byte window is loaded when
+  // the current one is used up: one load latency per 256 input bytes (~2 % of the decode) and no
+  // in-flight load crossing the loop's register copies (a copy of an in-flight load waits for it).
+  auto refill1 = [&]() __attribute__((always_inline)) {
+    const uint32_t w = rl(cur, rk);
+    bb |= (uint64_t)w << bc;
+    bc += 32;
+    if (++rk == 64) {
+      wcur += 64;
+      cur = abase[wcur + lane];
+      rk = 0;
     }
   };
+  auto refill = [&]() __attribute__((always_inline)) { while (bc <= 32) refill1(); };
   auto seek = [&](uint64_t apos) __attribute__((always_inline)) {
+    const uint64_t dw = apos >> 5;
+    wcur = dw & ~63ull;
+    cur = abase[wcur + lane];
+    rk = (uint32_t)(dw & 63);
     bb = 0; bc = 0;
-    next_dw = apos >> 5;
     pos = apos & ~31ull;
-    refill();
+    refill1();
     const uint32_t d = (uint32_t)(apos & 31);
     bb >>= d; bc -= d; pos += d;
     refill();
@@ -202,12 +232,15 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
   uint64_t arena_off = ARENA_NONE;
   bool arena_tried = false;
   const uint64_t out_cap = job.out_cap;
-  uint64_t prod = 0, flushed = 0;
+  uint64_t prod = 0, flushed = 0;   // prod: bytes in the ring (the stage's nst literals follow)
   uint32_t ad_a = 1, ad_b = 0;
   int overflow = 0;
+  // literal stage: output byte prod + l in lane l (l < nst)
+  uint32_t stg = 0, nst = 0;
   auto flush = [&](bool final) __attribute__((always_inline)) {
     const uint64_t n = prod - flushed;
     if (!n) return;
+    const uint64_t tf0 = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
     if (to_arena && !arena_tried) {
       arena_tried = true;
       const uint64_t want = final ? ((prod + 255) & ~255ull) : out_cap;
@@ -217,6 +250,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
       if (o + want <= arena_cap && (final || prod <= out_cap)) { arena_off = o; out = arena + o; }
     }
     uint64_t S = 0, W = 0;
+#pragma unroll 4
     for (uint64_t k = lane; k < n; k += 64) {
       const uint32_t x = ring[(flushed + k) & RMASK];
       S += x;
@@ -234,6 +268,44 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
       if (to_arena) { arena_off = ARENA_NONE; out = nullptr; }
     }
     flushed = prod;
+    if (ATZ_INF_CLOCKS) cyc_flush += __builtin_amdgcn_s_memtime() - tf0;
+  };
+  auto stage_flush = [&]() __attribute__((always_inline)) {
+    if (nst) {
+      if ((uint32_t)lane < nst) ring[(prod + lane) & RMASK] = (uint8_t)stg;
+      prod += nst;
+      nst = 0;
+      if (prod - flushed >= FLUSH_AT) flush(false);
+    }
+  };
+  auto put_lit = [&](uint32_t s) __attribute__((always_inline)) {
+    stg = ((uint32_t)lane == nst) ? s : stg;
+    nst++;
+    if (ATZ_INF_CLOCKS) nlit++;
+    if (nst == 64) stage_flush();
+  };
+  // copy `len` bytes from `dist` back (dist <= prod); the stage must be empty
+  auto copy = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) {
+    if (ATZ_INF_CLOCKS) nmatch++;
+    if (dist >= len) {
+      for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        uint8_t v = 0;
+        if (i < len) v = ring[(prod - dist + i) & RMASK];
+        __builtin_amdgcn_wave_barrier();
+        if (i < len) ring[(prod + i) & RMASK] = v;
+      }
+    } else {   // overlapping: the source repeats with period `dist`
+      for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        uint8_t v = 0;
+        if (i < len) v = ring[(prod - dist + i % dist) & RMASK];
+        __builtin_amdgcn_wave_barrier();
+        if (i < len) ring[(prod + i) & RMASK] = v;
+      }
+    }
+    prod += len;
+    if (prod - flushed >= FLUSH_AT) flush(false);
   };
 
   // inflate_table acceptance (Z/inftrees.c:32-141); type 0 CODES, 1 LENS, 2 DISTS. Returns 0 / -1.
@@ -250,7 +322,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
     int max = 0, left = 1, bad = 0;
     uint32_t code = 0, offs = 0, my_first = 0, my_offs = 0;
     for (int l = 1; l <= 15; l++) {
-      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cnt, l);
+      const uint32_t c = rl(cnt, l);
       if (c) max = l;
       left <<= 1;
       left -= (int)c;
@@ -260,11 +332,12 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
       offs += c;
     }
     h.max = max;
-    if (max == 0) { h.count = 0; h.first = 0; h.offs = 0; return 0; }
+    h.root = 0;
+    if (max == 0) { h.count = 0; h.first = 0; h.ofm = 0; return 0; }
     if (bad) return -1;
     if (left > 0 && (type == 0 || max != 1)) return -1;
-    h.first = my_first; h.count = (lane >= 1 && lane <= 15) ? cnt : 0; h.offs = my_offs;
-    // ballot-ranked counting sort into LDS, then into the VGPR table
+    h.first = my_first; h.count = (lane >= 1 && lane <= 15) ? cnt : 0; h.ofm = my_offs - my_first;
+    // ballot-ranked counting sort into LDS, then into the packed VGPR table
     uint32_t run = my_offs;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (int g = 0; g < n; g += 64) {
@@ -273,20 +346,31 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
       for (int l = 1; l <= 15; l++) {
         const uint64_t m = __ballot(len == (uint32_t)l);
         if (!m) continue;
-        const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)run, l);
+        const uint32_t base = rl(run, l);
         if (len == (uint32_t)l) sh.sort[base + __popcll(m & lt)] = (uint16_t)i;
         if (lane == l) run += __popcll(m);
       }
     }
-    h.s0 = sh.sort[lane];
-    h.s1 = n > 64 ? sh.sort[64 + lane] : 0;
-    h.s2 = n > 128 ? sh.sort[128 + lane] : 0;
-    h.s3 = n > 192 ? sh.sort[192 + lane] : 0;
-    h.s4 = n > 256 && lane < 64 ? sh.sort[256 + lane] : 0;
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(sh.sort);
+    h.t0 = sw[lane];
+    h.t1 = n > 128 ? sw[64 + lane] : 0;
+    h.t2 = n > 256 ? sw[128 + lane] : 0;
+    // 6-bit root: lane p resolves the code of length <= 6 its stream bits start with
+    {
+      const uint32_t rp = __builtin_bitreverse32((uint32_t)lane) >> 26;
+      uint32_t e = 0;
+      const int lm = max < 6 ? max : 6;
+      for (int l = 1; l <= lm; l++) {
+        const uint32_t f = rl(h.first, l), k = rl(h.count, l), o = rl(h.ofm, l);
+        const uint32_t c = rp >> (6 - l);
+        if (e == 0 && (c - f) < k) e = ((uint32_t)sh.sort[o + c] << 4) | (uint32_t)l;
+      }
+      h.root = e;
+    }
     return 0;
   };
 
-  // Decode one symbol: >= 0 symbol, -1 invalid code, -2 need more input.  need = the bit position
+  // Careful decode: >= 0 symbol, -1 invalid code, -2 need more input.  need = the bit position
   // zlib would have required when it stops here.
   auto decode = [&](const Huff& h, bool cl_quirk, uint64_t& need) __attribute__((always_inline)) -> int {
     if (h.max == 0) {
@@ -296,9 +380,8 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
       return cl_quirk ? 0 : -1;
     }
     const uint32_t v = __builtin_bitreverse32((uint32_t)bb) >> 17;   // first stream bit at bit 14
-    const uint32_t c = v >> (15 - (lane & 15));
-    const bool hit = lane >= 1 && lane <= 15 && (c - h.first) < h.count;
-    const uint64_t m = __ballot(hit);
+    const uint32_t c = v >> lsh;
+    const uint64_t m = __ballot((c - h.first) < h.count);
     if (!m) {  // only incomplete codes have unused patterns: zlib's invalid entry has 1 bit
       need = pos + 1;
       if (!has(1)) return -2;
@@ -308,7 +391,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
     const uint32_t L = (uint32_t)__ffsll((unsigned long long)m) - 1;
     need = pos + L;
     if (!has(L)) return -2;
-    const uint32_t idx = (uint32_t)__builtin_amdgcn_readlane((int)(h.offs + (c - h.first)), (int)L);
+    const uint32_t idx = rl(c + h.ofm, L);
     drop(L);
     return (int)h.sym(idx);
   };
@@ -321,15 +404,72 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
   auto codes = [&](const Huff& lh, const Huff& dh) __attribute__((always_inline)) -> int {
     uint64_t need;
     for (;;) {
+      if (pos + 64 <= limit) {
+        // ---- fast loop: while >= 64 input bits remain at a symbol's start every field of it is
+        // buffered-or-refillable (<= 48 bits), so no NEEDBITS checks.  Bits consumed here are
+        // counted in `used` (32-bit) and folded into pos when the loop leaves.
+        const uint64_t pos0 = pos;
+        const uint64_t rr64 = limit - 64 - pos;
+        const uint32_t rem = rr64 > 0x7fffffffull ? 0x7fffffffu : (uint32_t)rr64;
+        uint32_t used = 0;
+        int rc = 1;   // 1: careful path next, R_OK / R_ERR: return
+        while (used <= rem) {
+          if (bc <= 32) refill1();
+          uint32_t e = rl(lh.root, (uint32_t)bb & 63);
+          if (e == 0) {   // code longer than 6 bits (or invalid): canonical compare
+            const uint32_t v = __builtin_bitreverse32((uint32_t)bb) >> 17;
+            const uint32_t c = v >> lsh;
+            const uint64_t m = __ballot((c - lh.first) < lh.count);
+            if (!m) { errneed = pos0 + used + 1; errcode = 10; used += 1; rc = R_ERR; break; }
+            const uint32_t L = (uint32_t)__ffsll((unsigned long long)m) - 1;
+            e = (lh.sym(rl(c + lh.ofm, L)) << 4) | L;
+          }
+          const uint32_t L = e & 15, sym = e >> 4;
+          bb >>= L; bc -= L; used += L;
+          if (sym < 256) { put_lit(sym); continue; }
+          if (sym == 256) { rc = R_OK; break; }
+          const uint32_t ls = sym - 257;
+          if (ls >= 29) { errneed = pos0 + used; errcode = 11; rc = R_ERR; break; }   // fixed codes 286/287
+          const uint32_t lt = rl(lentab, ls);
+          const uint32_t le = lt & 15;
+          const uint32_t len = (lt >> 4) + ((uint32_t)bb & ((1u << le) - 1));
+          bb >>= le; bc -= le; used += le;
+          if (bc <= 32) refill1();
+          if (dh.max == 0) { errneed = pos0 + used + 1; errcode = 12; used += 1; rc = R_ERR; break; }
+          uint32_t d = rl(dh.root, (uint32_t)bb & 63);
+          if (d == 0) {
+            const uint32_t v = __builtin_bitreverse32((uint32_t)bb) >> 17;
+            const uint32_t c = v >> lsh;
+            const uint64_t m = __ballot((c - dh.first) < dh.count);
+            if (!m) { errneed = pos0 + used + 1; errcode = 12; used += 1; rc = R_ERR; break; }
+            const uint32_t L2 = (uint32_t)__ffsll((unsigned long long)m) - 1;
+            d = (dh.sym(rl(c + dh.ofm, L2)) << 4) | L2;
+          }
+          const uint32_t L2 = d & 15, ds = d >> 4;
+          bb >>= L2; bc -= L2; used += L2;
+          if (ds >= 30) { errneed = pos0 + used; errcode = 13; rc = R_ERR; break; }   // fixed distance 30/31
+          const uint32_t dt = rl(disttab, ds);
+          const uint32_t de = dt & 15;
+          const uint32_t dist = (dt >> 4) + ((uint32_t)bb & ((1u << de) - 1));
+          bb >>= de; bc -= de; used += de;
+          const uint64_t tc0 = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
+          stage_flush();
+          if ((uint64_t)dist > prod) { errneed = pos0 + used; errcode = 14; rc = R_ERR; break; }   // too far back
+          copy(len, dist);
+          if (ATZ_INF_CLOCKS) cyc_copy += __builtin_amdgcn_s_memtime() - tc0;
+        }
+        pos = pos0 + used;
+        if (bc <= 32) refill();
+        if (rc == R_OK) return R_OK;
+        if (rc == R_ERR) return R_ERR;
+        continue;
+      }
+      // ---- careful path (the last 8 input bytes): zlib's NEEDBITS points exactly
+      if (bc <= 32) refill();
       int sym = decode(lh, false, need);
       if (sym == -2) return R_NEED;
       if (sym == -1) FAIL(10, need);
-      if (sym < 256) {
-        if (lane == 0) ring[prod & RMASK] = (uint8_t)sym;
-        prod++;
-        if (prod - flushed >= FLUSH_AT) flush(false);
-        continue;
-      }
+      if (sym < 256) { put_lit((uint32_t)sym); continue; }
       if (sym == 256) return R_OK;
       sym -= 257;
       if (sym >= 29) FAIL(11, need);                       // fixed codes 286/287
@@ -345,18 +485,9 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
       NEEDB(de);
       const uint32_t dist = dist_base((uint32_t)ds) + peek(de);
       drop(de);
+      stage_flush();
       if ((uint64_t)dist > prod) FAIL(14, pos);            // invalid distance too far back
-      // copy: read the whole source first (a period of `dist` repeats for overlapping copies)
-      for (uint32_t i0 = 0; i0 < len; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        const uint32_t src = dist >= len ? i : i % dist;
-        uint8_t v = 0;
-        if (i < len) v = ring[(prod - dist + src) & RMASK];
-        __builtin_amdgcn_wave_barrier();
-        if (i < len) ring[(prod + i) & RMASK] = v;
-      }
-      prod += len;
-      if (prod - flushed >= FLUSH_AT) flush(false);
+      copy(len, dist);
     }
   };
 
@@ -371,6 +502,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
     drop(16);
     if (flg & 0x20) { NEEDB(32); FAIL(4, pos + 32); }      // preset dictionary: not a stream end
     int last;
+    Huff lh, dh;
     do {
       NEEDB(3);
       last = (int)peek(1);
@@ -384,6 +516,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
         const uint32_t nlen = (peek(32) >> 16) & 0xffff;
         if (len != (~nlen & 0xffff)) FAIL(5, pos + 32);
         drop(32);
+        stage_flush();
         // copy `len` bytes straight from the input (byte aligned now)
         const uint64_t avail = (limit - pos) >> 3;
         const uint64_t take = len < avail ? len : avail;
@@ -404,12 +537,9 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
         if (take < len) return R_NEED;
       } else if (type == 1) {                               // FIXED
         for (int i = lane; i < 288; i += 64) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
-        Huff lh, dh;
         build(lh, lens, 288, 1);
         for (int i = lane; i < 32; i += 64) lens[i] = 5;
         build(dh, lens, 32, 2);
-        const int rr = codes(lh, dh);
-        if (rr != R_OK) return rr;
       } else if (type == 2) {                               // DYNAMIC (Z/inflate.c:908-1013)
         NEEDB(14);
         const uint32_t nlen = peek(5) + 257;
@@ -435,32 +565,33 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
           const int sym = decode(chh, true, need);
           if (sym == -2) return R_NEED;
           if (sym < 16) { if (lane == 0) lens[have] = (uint16_t)sym; prevlen = (uint32_t)sym; have++; continue; }
-          uint32_t copy, len = 0, eb;
+          uint32_t copyn, len = 0, eb;
           if (sym == 16) eb = 2; else if (sym == 17) eb = 3; else eb = 7;
           NEEDB(eb);
           if (sym == 16) {
             if (have == 0) FAIL(8, pos + eb);
             len = prevlen;
-            copy = 3 + peek(2);
+            copyn = 3 + peek(2);
           } else if (sym == 17) {
-            copy = 3 + peek(3);
+            copyn = 3 + peek(3);
           } else {
-            copy = 11 + peek(7);
+            copyn = 11 + peek(7);
           }
           drop(eb);
-          if (have + copy > total) FAIL(8, pos);
-          for (uint32_t k = lane; k < copy; k += 64) lens[have + k] = (uint16_t)len;
+          if (have + copyn > total) FAIL(8, pos);
+          for (uint32_t k = lane; k < copyn; k += 64) lens[have + k] = (uint16_t)len;
           prevlen = len;
-          have += copy;
+          have += copyn;
         }
         if (iuni(lens[256]) == 0) FAIL(9, pos);
-        Huff lh, dh;
         if (build(lh, lens, (int)nlen, 1)) FAIL(9, pos);
         if (build(dh, lens + nlen, (int)ndist, 2)) FAIL(9, pos);
-        const int rr = codes(lh, dh);
-        if (rr != R_OK) return rr;
       } else {
         FAIL(15, pos);                                      // invalid block type
+      }
+      if (type != 0) {   // one (inlined) decode loop for fixed and dynamic blocks
+        const int rr = codes(lh, dh);
+        if (rr != R_OK) return rr;
       }
     } while (!last);
     // CHECK (Z/inflate.c:1174-1195)
@@ -470,6 +601,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
     const uint32_t t = peek(32);
     const uint32_t want = ((t & 0xff) << 24) | ((t & 0xff00) << 8) | ((t >> 8) & 0xff00) | (t >> 24);
     drop(32);
+    stage_flush();
     flush(true);
     const uint32_t adler = (ad_b << 16) | ad_a;
     if (want != adler) FAIL(16, pos);
@@ -480,6 +612,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
 
   seek(8 * skip);
   const int rr = body();
+  prod += nst;   // literals still in the stage (their ring bytes are never read again)
   InfRes o;
   o.arena_off = (rr == R_OK && to_arena) ? arena_off : ARENA_NONE;
   o.produced = prod;
@@ -497,6 +630,8 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
     const uint64_t cons = (need + 7) >> 3;
     o.consumed = cons > job.in_len ? job.in_len : cons;
   }
+  o.cyc = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() - t_start : 0;
+  o.nlit = nlit; o.nmatch = nmatch; o.cyc_copy = cyc_copy; o.cyc_flush = cyc_flush;
   if (lane == 0) res[j] = o;
 }
 
