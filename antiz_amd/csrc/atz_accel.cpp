@@ -25,6 +25,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <memory>
+#include <thread>
 #include <vector>
 
 #include "../../include/atz_accel.h"
@@ -233,6 +235,26 @@ struct KTimer {   // HIP events bracketing kernel launches on the library stream
   }
 };
 
+// One HIP stream of sweep work with its own buffers, kernel timers and counters.  The sweep runs
+// several pipes at once (streams partitioned among them, one host thread each), so one pipe's
+// launch tails, host gaps and small launches overlap another's work.
+struct Pipe {
+  hipStream_t st = nullptr;
+  KTimer kt;
+  atz_stats_t stats{};
+  DBuf d_trials, d_tres, d_out, d_syms, d_R, d_mjobs, d_cjobs, d_cjobs2, d_cjobs3, d_heads, d_heads2, d_chains,
+      d_diffjobs, d_diffpos, d_diffval, d_diffcnt;
+  uint64_t chain_used = 0, chain_cap = 0;
+  std::vector<uint32_t> streams;   // the streams whose chain tables this pipe owns
+  // diagnostics (ATZ_TIMING): host phase times, per trial kind x level counters
+  double t_list = 0, t_chains = 0, t_trials = 0, t_apply = 0;
+  uint64_t kind[3][10][14] = {};
+  ~Pipe() {
+    if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
+    for (hipEvent_t e : kt.pool) hipEventDestroy(e);
+  }
+};
+
 struct atz_ctx {
   KTimer kt;
   atz_opts_t o{};
@@ -251,20 +273,23 @@ struct atz_ctx {
   const uint8_t* dev_file = nullptr;
   atz_stats_t stats{};
   // chains cache: per record and memlevel
-  std::vector<std::array<uint64_t, 10>> chain_off;
-  uint64_t chain_used = 0;
+  std::vector<std::array<uint64_t, 10>> chain_off;   // offset in the owning pipe's d_chains
+  std::vector<std::unique_ptr<Pipe>> pipes;
 };
 
 // kind: 0 trial, 1 inflate, 2 chains, 3 other, 4 match tables
-static void kbeg(atz_ctx* c, int kind) {
+template <class C>
+static void kbeg(C* c, int kind) {
   hipEvent_t a = c->kt.get(), b = c->kt.get();
   (void)hipEventRecord(a, c->st);
   c->kt.pending.push_back({a, b});
   c->kt.kind.push_back(kind);
 }
-static void kend(atz_ctx* c) { (void)hipEventRecord(c->kt.pending.back().second, c->st); }
+template <class C>
+static void kend(C* c) { (void)hipEventRecord(c->kt.pending.back().second, c->st); }
 // after a stream synchronisation: fold elapsed times into the stats
-static void kcollect(atz_ctx* c) {
+template <class C>
+static void kcollect(C* c) {
   for (size_t i = 0; i < c->kt.pending.size(); i++) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, c->kt.pending[i].first, c->kt.pending[i].second);
@@ -283,7 +308,8 @@ static void kcollect(atz_ctx* c) {
 }
 
 // copy n host bytes into b (device capacity n + slack; the slack is never read from the host)
-static int upload(atz_ctx* c, DBuf& b, const void* h, size_t n, size_t slack = 4096) {
+template <class C>
+static int upload(C* c, DBuf& b, const void* h, size_t n, size_t slack = 4096) {
   if (int r = b.reserve(n + slack)) return r;
   if (n) HIPCHK(hipMemcpyAsync(b.p, h, n, hipMemcpyHostToDevice, c->st));
   return 0;
@@ -691,27 +717,27 @@ static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F) {
 // sweep (8 bytes per position).  When a round would push the cache past its cap the cache is
 // dropped and the round's tables are rebuilt.
 static constexpr uint64_t CHAIN_CACHE_CAP = 48ull << 30;
-static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>& need) {
-  auto words = [&](uint32_t s) { return 2 * ((c->recs[s].infl_len + 63) & ~63ull); };
+static int ensure_chains(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need) {
+  auto words = [&](uint32_t s) { return 2 * ((x->recs[s].infl_len + 63) & ~63ull); };
   uint64_t add = 0;
   for (auto& q : need)
-    if (c->chain_off[q.first][q.second] == ~0ull) add += words(q.first);
-  if ((c->chain_used + add) * 4 > CHAIN_CACHE_CAP) {   // drop the cache
-    for (auto& a : c->chain_off) a.fill(~0ull);
+    if (x->chain_off[q.first][q.second] == ~0ull) add += words(q.first);
+  if ((c->chain_used + add) * 4 > c->chain_cap) {   // drop this pipe's cache
+    for (uint32_t s : c->streams) x->chain_off[s].fill(~0ull);
     c->chain_used = 0;
   }
   std::vector<ChainJob> jobs;
   for (auto& q : need) {
     uint32_t s = q.first;
     int m = q.second;
-    if (c->chain_off[s][m] != ~0ull) continue;
+    if (x->chain_off[s][m] != ~0ull) continue;
     ChainJob jb;
-    jb.infl_off = c->infl_off[s];
-    jb.n = c->recs[s].infl_len;
+    jb.infl_off = x->infl_off[s];
+    jb.n = x->recs[s].infl_len;
     jb.chain_off = c->chain_used;
     jb.memlevel = (uint32_t)m;
     jb.slot = 0;
-    c->chain_off[s][m] = c->chain_used;
+    x->chain_off[s][m] = c->chain_used;
     c->chain_used += words(s);
     jobs.push_back(jb);
   }
@@ -720,7 +746,7 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
   size_t need_bytes = c->chain_used * 4 + 4096;
   if (need_bytes > c->d_chains.n) {
     void* np = nullptr;
-    size_t cap = std::min<size_t>(need_bytes + need_bytes / 2 + (64 << 20), CHAIN_CACHE_CAP + (1ull << 30));
+    size_t cap = std::min<size_t>(need_bytes + need_bytes / 2 + (64 << 20), c->chain_cap + (1ull << 30));
     if (cap < need_bytes) cap = need_bytes;
     if (hipMalloc(&np, cap) != hipSuccess) return ATZ_E_NOMEM;
     if (c->d_chains.p) {
@@ -747,7 +773,7 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
       auto launch = [&](auto kern, size_t off, size_t cnt, const char* nm) -> int {
         if (!cnt) return 0;
         kbeg(c, 2);
-        hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(256), 0, c->st, c->d_infl.as<uint8_t>(), dj + off,
+        hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(), dj + off,
                            c->d_chains.as<uint32_t>(), (uint32_t)cnt);
         kend(c);
         KCHECK(nm);
@@ -769,7 +795,7 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
     for (size_t b0 = 0; b0 < nine.size(); b0 += nb9) {
       const size_t nb = std::min(nb9, nine.size() - b0);
       kbeg(c, 2);
-      hipLaunchKernelGGL(k_buckets_lds9, dim3((uint32_t)nb), dim3(256), 0, c->st, c->d_infl.as<uint8_t>(),
+      hipLaunchKernelGGL(k_buckets_lds9, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
                          c->d_cjobs3.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), c->d_heads2.as<uint32_t>(),
                          (uint32_t)nb);
       kend(c);
@@ -783,7 +809,7 @@ static int ensure_chains(atz_ctx* c, const std::vector<std::pair<uint32_t, int>>
   for (size_t b0 = 0; b0 < big.size(); b0 += batch) {   // launches on one stream reuse the slots in order
     size_t nb = std::min(batch, big.size() - b0);
     kbeg(c, 2);
-    hipLaunchKernelGGL(k_buckets, dim3((uint32_t)nb), dim3(64), 0, c->st, c->d_infl.as<uint8_t>(),
+    hipLaunchKernelGGL(k_buckets, dim3((uint32_t)nb), dim3(64), 0, c->st, x->d_infl.as<uint8_t>(),
                        c->d_cjobs.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), c->d_heads.as<uint64_t>(),
                        (uint32_t)nb);
     kend(c);
@@ -806,11 +832,11 @@ static uint64_t match_prefix(uint64_t n, int memlevel) {
   return std::min(n, x);
 }
 
-static int launch_match(atz_ctx* c, const std::vector<MatchJob>& mj) {
+static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj) {
   if (mj.empty()) return 0;
   if (int r = upload(c, c->d_mjobs, mj.data(), mj.size() * sizeof(MatchJob))) return r;
   kbeg(c, 4);
-  hipLaunchKernelGGL(k_match, dim3((uint32_t)mj.size()), dim3(256), 0, c->st, c->d_infl.as<uint8_t>(),
+  hipLaunchKernelGGL(k_match, dim3((uint32_t)mj.size()), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
                      c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(), c->d_mjobs.as<MatchJob>());
   kend(c);
   KCHECK("k_match");
@@ -821,41 +847,41 @@ static int launch_match(atz_ctx* c, const std::vector<MatchJob>& mj) {
 // Runs the trials tr[k] (k = 0 stored, 1 fast, 2 slow levels); res[k] receives their results.
 // Chain tables must exist.  Match tables are built for a prefix of each trial's positions; a
 // trial that parses past it (TR_NEED_R) gets the rest of its table and is run again.
-static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
+static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
                       std::vector<TrialRes>* res) {
   uint64_t r_tot = 0;
   std::vector<MatchJob> mj;
   for (int k = 0; k < 3; k++)
     for (const Trial& t : tr[k])
-      if (c->recs[t.stream].infl_len >= (1ull << 31)) {   // trial kernels keep 32-bit positions
+      if (x->recs[t.stream].infl_len >= (1ull << 31)) {   // trial kernels keep 32-bit positions
         std::fprintf(stderr, "atz: stream of %llu inflated bytes exceeds the 2 GiB trial limit\n",
-                     (unsigned long long)c->recs[t.stream].infl_len);
+                     (unsigned long long)x->recs[t.stream].infl_len);
         return ATZ_E_ARG;
       }
   for (int k = 1; k < 3; k++)
     for (Trial& t : tr[k]) {
-      const uint64_t n = c->recs[t.stream].infl_len;
+      const uint64_t n = x->recs[t.stream].infl_len;
       t.r_off = r_tot;
       r_tot += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
       t.x_lim = (t.mode & 1) ? n : match_prefix(n, t.memlevel);
       MatchJob m{};
-      m.infl_off = c->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
+      m.infl_off = x->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
       m.p0 = 0; m.p1 = t.x_lim; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
       if (m.p1 > m.p0) mj.push_back(m);
     }
   if (int r = c->d_R.reserve(r_tot * sizeof(uint2) + 4096)) return r;
-  if (int r = launch_match(c, mj)) return r;
+  if (int r = launch_match(x, c, mj)) return r;
   const size_t tot_trials = tr[0].size() + tr[1].size() + tr[2].size();
   if (int r = c->d_trials.reserve(2 * tot_trials * sizeof(Trial) + 64)) return r;
   if (int r = c->d_tres.reserve(2 * tot_trials * sizeof(TrialRes) + 64)) return r;
   auto launch = [&](int k, const Trial* h, size_t cnt, size_t base) -> int {
     HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + base, h, cnt * sizeof(Trial), hipMemcpyHostToDevice, c->st));
     SweepArgs A;
-    A.file = d_cmp; A.infl = c->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint32_t>();
+    A.file = d_cmp; A.infl = x->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint32_t>();
     A.R = c->d_R.as<uint2>();
-    A.streams = c->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
+    A.streams = x->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
     A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
-    A.adler = c->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)cnt;
+    A.adler = x->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)cnt;
     dim3 g((uint32_t)cnt), b(64);
     kbeg(c, 0);
     if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
@@ -888,9 +914,9 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
     for (size_t q = 0; q < tr[k].size(); q++) {
       if (res[k][q].state != TR_NEED_R) continue;
       Trial t = tr[k][q];
-      const uint64_t n = c->recs[t.stream].infl_len;
+      const uint64_t n = x->recs[t.stream].infl_len;
       MatchJob m{};
-      m.infl_off = c->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
+      m.infl_off = x->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
       m.p0 = t.x_lim; m.p1 = n; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
       if (m.p1 > m.p0) mj.push_back(m);
       t.x_lim = n;
@@ -899,7 +925,7 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
       c->stats.n_trials_rerun++;
     }
   if (mj.empty()) return 0;
-  if (int r = launch_match(c, mj)) return r;
+  if (int r = launch_match(x, c, mj)) return r;
   std::vector<TrialRes> rr[3];
   for (int k = 1; k < 3; k++) {
     if (again[k].empty()) continue;
@@ -919,32 +945,12 @@ static int run_trials(atz_ctx* c, const uint8_t* d_cmp, std::vector<Trial>* tr, 
   return 0;
 }
 
-static double g_t_list = 0, g_t_chains = 0, g_t_trials = 0, g_t_apply = 0;
-// per trial kind (stored/fast/slow) x level: count, cycles total/tree/emit/lookup/fallback, parsed bytes, symbols
-static uint64_t g_kind[3][10][14];
-static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
+// The sweep of the streams c->streams on pipe c (per-kind x level counters: count, cycles
+// total/tree/emit/heap/fallback, parsed bytes, symbols, scan/send cycles, parse window phases).
+static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss, size_t target) {
   auto t0 = std::chrono::steady_clock::now();
-  g_t_list = g_t_chains = g_t_trials = g_t_apply = 0;
-  std::memset(g_kind, 0, sizeof(g_kind));
-  const size_t n = c->recs.size();
-  ss.assign(n, StreamState());
-  c->chain_off.assign(n, {});
-  for (auto& a : c->chain_off) a.fill(~0ull);
-  c->chain_used = 0;
-  std::vector<uint32_t> active;
-  for (size_t s = 0; s < n; s++) {
-    list_a(ss[s].list, c->recs[s].type);
-    active.push_back((uint32_t)s);
-  }
-  // device stream table
-  std::vector<StreamDev> sd(n);
-  for (size_t s = 0; s < n; s++) {
-    sd[s].orig_off = c->recs[s].offset; sd[s].infl_off = c->infl_off[s];
-    sd[s].comp_len = c->recs[s].comp_len; sd[s].infl_len = c->recs[s].infl_len;
-  }
-  if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;
-  if (int r = upload(c, c->d_streams, sd.data(), n * sizeof(StreamDev))) return r;
-  SweepOpts so{c->o.recomp_tresh, c->o.sizediff_tresh, c->o.shortcut_len, c->o.mismatch_tol};
+  std::vector<uint32_t> active = c->streams;
+  SweepOpts so{x->o.recomp_tresh, x->o.sizediff_tresh, x->o.shortcut_len, x->o.mismatch_tol};
   uint64_t rounds = 0, ntr = 0, nsc = 0, nhz = 0, nspec = 0;
   std::vector<Trial> tr[3];
   std::vector<TrialRes> trres[3];
@@ -952,7 +958,6 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
   // stops at its j-th trial discards the results of the later ones), K sized so a round fills the
   // GPU.  Results are applied per stream strictly in list order, so the outcome is the
   // reference's sequential one; the speculation only changes how much work runs per launch.
-  const size_t target = 16384;
   while (!active.empty()) {
     rounds++;
     const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, target / active.size()));
@@ -970,7 +975,7 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
         Trial t{};
         t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
         t.best_ident = st.ident;
-        t.out_off = out_tot; t.out_cap = bound(c->recs[s].infl_len, w, m) + 64;
+        t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
         t.sym_off = sym_tot; sym_tot += (1ull << (m + 6)) + 64;
         int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
@@ -980,33 +985,33 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
       }
     }
     auto ta = std::chrono::steady_clock::now();
-    if (int r = ensure_chains(c, need)) return r;
+    if (int r = ensure_chains(x, c, need)) return r;
     HIPCHK(hipStreamSynchronize(c->st));
     auto tb = std::chrono::steady_clock::now();
     for (int k = 1; k < 3; k++)
-      for (Trial& t : tr[k]) t.chain_off = c->chain_off[t.stream][t.memlevel];
+      for (Trial& t : tr[k]) t.chain_off = x->chain_off[t.stream][t.memlevel];
     if (int r = c->d_out.reserve(out_tot + 4096)) return r;
     if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
-    if (int r = run_trials(c, d_file, tr, so, trres)) return r;
+    if (int r = run_trials(x, c, d_file, tr, so, trres)) return r;
     auto tc = std::chrono::steady_clock::now();
-    g_t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
-    g_t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
+    c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
+    c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
     for (int k = 0; k < 3; k++)
       for (size_t q = 0; q < tr[k].size(); q++) {
         const TrialRes& r = trres[k][q];
-        const uint64_t C = c->recs[tr[k][q].stream].comp_len;
+        const uint64_t C = x->recs[tr[k][q].stream].comp_len;
         c->stats.trial_parsed_bytes += r.parsed;
         c->stats.n_fast_fallbacks += r.fallbacks;
         c->stats.trial_cyc_total += r.cyc_total; c->stats.trial_cyc_tree += r.cyc_tree;
         c->stats.trial_cyc_emit += r.cyc_emit; c->stats.trial_blocks += r.blocks;
         c->stats.trial_cyc_heap += r.cyc_heap; c->stats.trial_cyc_fallback += r.cyc_fallback;
         c->stats.trial_symbols += r.symbols;
-        uint64_t* gk = g_kind[k][tr[k][q].clevel];
+        uint64_t* gk = c->kind[k][tr[k][q].clevel];
         gk[0]++; gk[1] += r.cyc_total; gk[2] += r.cyc_tree; gk[3] += r.cyc_emit; gk[4] += r.cyc_heap;
         gk[5] += r.cyc_fallback; gk[6] += r.parsed; gk[7] += r.symbols; gk[8] += r.cyc_scan; gk[9] += r.cyc_send;
         for (int i = 0; i < 4; i++) gk[10 + i] += r.cyc_sec[i];
         // trial input read + compare read (bytes emitted and compared against the original)
-        c->stats.k_trial_alg_bytes += c->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
+        c->stats.k_trial_alg_bytes += x->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
       }
     if (timing_on()) {   // slowest trials of the round (diagnostics)
       std::vector<std::pair<uint64_t, std::pair<int, size_t>>> top;
@@ -1018,7 +1023,7 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
         const TrialRes& r = trres[top[i].second.first][top[i].second.second];
         std::fprintf(stderr, "atz: round %llu slow trial: stream %u I=%llu c%u w%u m%u state %u cyc %.1fM syms %llu blocks %llu "
                      "fallbacks %llu tree %.1fM emit %.1fM\n", (unsigned long long)rounds, t.stream,
-                     (unsigned long long)c->recs[t.stream].infl_len, t.clevel, t.window, t.memlevel, r.state,
+                     (unsigned long long)x->recs[t.stream].infl_len, t.clevel, t.window, t.memlevel, r.state,
                      r.cyc_total / 1e6, (unsigned long long)r.symbols, (unsigned long long)r.blocks,
                      (unsigned long long)r.fallbacks, r.cyc_tree / 1e6, r.cyc_emit / 1e6);
       }
@@ -1030,7 +1035,7 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
     for (size_t a = 0; a < active.size(); a++) {
       const uint32_t s = active[a];
       StreamState& st = ss[s];
-      const uint64_t C = c->recs[s].comp_len;
+      const uint64_t C = x->recs[s].comp_len;
       const uint32_t phase0 = st.phase;
       int64_t last_dj = -1;
       for (size_t j = 0; j < mine[a].size(); j++) {
@@ -1051,10 +1056,10 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
           if (last_dj >= 0) { dj_stream[last_dj] = ~0u; last_dj = -1; }
           if (r.ident == C) fullmatch = true;
           else {
-            if (r.ident + c->o.mismatch_tol >= C) fullmatch = true;
-            if (C - r.ident <= c->o.recomp_tresh) {     // diffs are only ever written for recomp streams
+            if (r.ident + x->o.mismatch_tol >= C) fullmatch = true;
+            if (C - r.ident <= x->o.recomp_tresh) {     // diffs are only ever written for recomp streams
               DiffJob d;
-              d.out_off = t.out_off; d.out_len = r.out_len; d.orig_off = c->recs[s].offset;
+              d.out_off = t.out_off; d.out_len = r.out_len; d.orig_off = x->recs[s].offset;
               d.comp_len = C; d.dst = dpos; d.cap = C - r.ident;
               dpos += d.cap;
               last_dj = (int64_t)dj.size();
@@ -1066,9 +1071,9 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
         st.idx++;
         if (fullmatch) st.idx = (uint32_t)st.list.size();   // testParamRange/tryParams return
         if (st.idx >= st.list.size()) {
-          if (st.phase == 0 && (C - st.ident) >= c->o.mismatch_tol && c->o.brute_window) {
+          if (st.phase == 0 && (C - st.ident) >= x->o.mismatch_tol && x->o.brute_window) {
             st.list.clear();
-            list_b(st.list, c->recs[s].type);
+            list_b(st.list, x->recs[s].type);
             st.idx = 0;
             st.phase = 1;
           } else {
@@ -1108,15 +1113,102 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
     std::vector<uint32_t> next;
     for (uint32_t s : active) if (ss[s].phase != 2) next.push_back(s);
     active.swap(next);
-    g_t_apply += ms_since(tc);
+    c->t_apply += ms_since(tc);
+  }
+  c->stats.n_trials += ntr; c->stats.n_trials_shortcut += nsc; c->stats.n_rounds = rounds; c->stats.n_hazard += nhz;
+  c->stats.n_trials_speculative += nspec;
+  c->stats.sweep_ms = ms_since(t0);
+  return 0;
+}
+
+// Phase 3 driver: streams partitioned over the context's pipes (interleaved, so every pipe gets
+// the same mix of header classes and sizes), one host thread per pipe.
+static int ensure_pipes(atz_ctx* c, size_t np) {
+  while (c->pipes.size() < np) {
+    std::unique_ptr<Pipe> p(new Pipe());
+    if (hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
+    c->pipes.push_back(std::move(p));
+  }
+  return 0;
+}
+static size_t sweep_pipes() {   // ATZ_PIPES=k (1..8), default 2 (measured on C4: 1 390, 2 417, 4 367 MB/s)
+  static size_t v = 0;
+  if (!v) {
+    const char* e = std::getenv("ATZ_PIPES");
+    v = e ? (size_t)std::max(1, std::min(8, std::atoi(e))) : 2;
+  }
+  return v;
+}
+static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
+  auto t0 = std::chrono::steady_clock::now();
+  const size_t n = c->recs.size();
+  ss.assign(n, StreamState());
+  c->chain_off.assign(n, {});
+  for (auto& a : c->chain_off) a.fill(~0ull);
+  for (size_t s = 0; s < n; s++) list_a(ss[s].list, c->recs[s].type);
+  // device stream table
+  std::vector<StreamDev> sd(n);
+  for (size_t s = 0; s < n; s++) {
+    sd[s].orig_off = c->recs[s].offset; sd[s].infl_off = c->infl_off[s];
+    sd[s].comp_len = c->recs[s].comp_len; sd[s].infl_len = c->recs[s].infl_len;
+  }
+  if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;
+  if (int r = upload(c, c->d_streams, sd.data(), n * sizeof(StreamDev))) return r;
+  HIPCHK(hipStreamSynchronize(c->st));
+  const size_t np = std::max<size_t>(1, std::min(sweep_pipes(), (n + 255) / 256));
+  if (int r = ensure_pipes(c, np)) return r;
+  for (size_t g = 0; g < np; g++) {
+    Pipe* p = c->pipes[g].get();
+    p->streams.clear();
+    for (size_t s = g; s < n; s += np) p->streams.push_back((uint32_t)s);
+    p->stats = atz_stats_t{};
+    p->chain_used = 0;
+    p->chain_cap = CHAIN_CACHE_CAP / np;
+    p->t_list = p->t_chains = p->t_trials = p->t_apply = 0;
+    std::memset(p->kind, 0, sizeof(p->kind));
+  }
+  const size_t target = 16384;   // trials per round and pipe
+  std::vector<int> rc(np, 0);
+  if (np == 1) {
+    rc[0] = sweep_pipe(c, c->pipes[0].get(), d_file, ss, target);
+  } else {
+    std::vector<std::thread> th;
+    for (size_t g = 0; g < np; g++)
+      th.emplace_back([&, g]() {
+        if (hipSetDevice(c->dev) != hipSuccess) { rc[g] = ATZ_E_HIP; return; }
+        rc[g] = sweep_pipe(c, c->pipes[g].get(), d_file, ss, target);
+      });
+    for (auto& t : th) t.join();
+  }
+  for (size_t g = 0; g < np; g++) if (rc[g]) return rc[g];
+  // fold the pipes' counters into the context's
+  uint64_t kind[3][10][14] = {};
+  double tch = 0, ttr = 0, tap = 0;
+  for (size_t g = 0; g < np; g++) {
+    const Pipe* p = c->pipes[g].get();
+    const atz_stats_t& q = p->stats;
+    atz_stats_t& t = c->stats;
+    t.n_trials += q.n_trials; t.n_trials_shortcut += q.n_trials_shortcut; t.n_hazard += q.n_hazard;
+    t.n_rounds = std::max(t.n_rounds, q.n_rounds); t.n_trials_speculative += q.n_trials_speculative;
+    t.k_trial_ms += q.k_trial_ms; t.k_chains_ms += q.k_chains_ms; t.k_other_ms += q.k_other_ms; t.k_match_ms += q.k_match_ms;
+    t.k_trial_launches += q.k_trial_launches; t.k_chains_launches += q.k_chains_launches;
+    t.k_match_launches += q.k_match_launches;
+    t.k_trial_alg_bytes += q.k_trial_alg_bytes; t.k_chains_alg_bytes += q.k_chains_alg_bytes;
+    t.trial_parsed_bytes += q.trial_parsed_bytes; t.k_match_positions += q.k_match_positions;
+    t.n_trials_rerun += q.n_trials_rerun; t.n_fast_fallbacks += q.n_fast_fallbacks;
+    t.trial_cyc_total += q.trial_cyc_total; t.trial_cyc_tree += q.trial_cyc_tree; t.trial_cyc_emit += q.trial_cyc_emit;
+    t.trial_blocks += q.trial_blocks; t.trial_cyc_heap += q.trial_cyc_heap; t.trial_cyc_fallback += q.trial_cyc_fallback;
+    t.trial_symbols += q.trial_symbols;
+    tch = std::max(tch, p->t_chains); ttr = std::max(ttr, p->t_trials); tap = std::max(tap, p->t_apply);
+    for (int k = 0; k < 3; k++) for (int l = 0; l < 10; l++) for (int i = 0; i < 14; i++) kind[k][l][i] += p->kind[k][l][i];
   }
   if (timing_on())
     std::fprintf(stderr, "atz: sweep host: chains %.1f ms (incl. kernels), trials %.1f ms (incl. kernels), apply %.1f ms, total %.1f ms\n",
-                 g_t_chains, g_t_trials, g_t_apply, ms_since(t0));
+                 tch, ttr, tap, ms_since(t0));
   if (timing_on())
     for (int k = 0; k < 3; k++)
       for (int l = 0; l < 10; l++) {
-        const uint64_t* gk = g_kind[k][l];
+        const uint64_t* gk = kind[k][l];
         if (!gk[0]) continue;
         std::fprintf(stderr, "atz: kind %d level %d: trials %llu cyc %.3fT (tree %.3fT [heap %.3fT scan %.3fT] emit %.3fT [send %.3fT] fb %.3fT) "
                      "parsed %.1f MB syms %.1f M cyc/byte %.0f\n", k, l, (unsigned long long)gk[0], gk[1] / 1e12,
@@ -1130,8 +1222,6 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
     const uint64_t C = c->recs[s].comp_len;
     st.recomp = (C - st.ident) <= c->o.recomp_tresh && st.ident > 0;
   }
-  c->stats.n_trials = ntr; c->stats.n_trials_shortcut = nsc; c->stats.n_rounds = rounds; c->stats.n_hazard = nhz;
-  c->stats.n_trials_speculative = nspec;
   c->stats.sweep_ms = ms_since(t0);
   return 0;
 }
@@ -1254,16 +1344,24 @@ static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, 
   }
   c->chain_off.assign(n, {});
   for (auto& a : c->chain_off) a.fill(~0ull);
-  c->chain_used = 0;
+  if (int r = ensure_pipes(c, 1)) return r;
+  HIPCHK(hipStreamSynchronize(c->st));   // d_infl (context stream) before the pipe's kernels
+  Pipe* p = c->pipes[0].get();
+  p->streams.clear();
+  for (size_t s = 0; s < n; s++) p->streams.push_back((uint32_t)s);
+  p->chain_used = 0;
+  p->chain_cap = CHAIN_CACHE_CAP;
   std::vector<std::pair<uint32_t, int>> need;
   for (size_t s = 0; s < n; s++) if ((params[s] >> 16) > 0) need.push_back({(uint32_t)s, (int)(params[s] & 0xff)});
-  if (int r = ensure_chains(c, need)) return r;
+  if (int r = ensure_chains(c, p, need)) return r;
+  HIPCHK(hipStreamSynchronize(p->st));
   std::vector<StreamDev> sd(n);
   for (size_t s = 0; s < n; s++) {
     sd[s].orig_off = 0; sd[s].infl_off = off[s]; sd[s].comp_len = 0; sd[s].infl_len = ins[s].second;
   }
   if (int r = upload(c, c->d_streams, sd.data(), n * sizeof(StreamDev))) return r;
   if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;
+  HIPCHK(hipStreamSynchronize(c->st));
   std::vector<Trial> tr[3];
   std::vector<uint32_t> idx[3];
   uint64_t out_tot = 0, sym_tot = 0;
@@ -1279,19 +1377,19 @@ static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, 
     tr[kind].push_back(t);
     idx[kind].push_back((uint32_t)s);
   }
-  if (int r = c->d_out.reserve(out_tot + 4096)) return r;
-  if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
+  if (int r = p->d_out.reserve(out_tot + 4096)) return r;
+  if (int r = p->d_syms.reserve(sym_tot * 4 + 4096)) return r;
   // zero-length "file" for the compare side
   if (int r = c->d_tmp.reserve(4096)) return r;
   SweepOpts so{0, 0, 0, 0};
   std::vector<TrialRes> rr[3];
-  if (int r = run_trials(c, c->d_tmp.as<uint8_t>(), tr, so, rr)) return r;
+  if (int r = run_trials(c, p, c->d_tmp.as<uint8_t>(), tr, so, rr)) return r;
   for (int k = 0; k < 3; k++) {
     for (size_t q = 0; q < tr[k].size(); q++) {
       if (rr[k][q].state != TR_FULL) return ATZ_E_INTERNAL;
       std::vector<uint8_t>& o = outs[idx[k][q]];
       o.resize(rr[k][q].out_len);
-      HIPCHK(hipMemcpy(o.data(), c->d_out.as<uint8_t>() + tr[k][q].out_off, o.size(), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(o.data(), p->d_out.as<uint8_t>() + tr[k][q].out_off, o.size(), hipMemcpyDeviceToHost));
     }
   }
   return 0;
