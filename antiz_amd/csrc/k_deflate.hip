@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void k_buckets_lds9(const uint8_t* __restrict_
 // (NIL after the slide), which the parse checks.  nice_match is clamped to the lookahead, i.e.
 // to n - p near the end; bytes beyond the input can only extend candidates that already reach
 // n - p, which break at nice_match first.
-static constexpr uint32_t HOLE_SLOTS_M = 2048;   // == HOLE_SLOTS (fast-level hash slots)
+static constexpr uint32_t HOLE_SLOTS_M = 1024;   // == HOLE_SLOTS (fast-level hash slots; a collision only makes the hole check conservative)
 
 // 16 bytes at byte offset x of a 4-byte aligned buffer: 5 aligned dword loads (independent, one
 // round trip) joined with v_alignbyte.  Reads up to 4 bytes past x + 16 (buffers carry slack).
@@ -491,17 +491,26 @@ __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl,
 // k_trial
 static constexpr int NLC = 286, NDC = 30, NBLC = 19, HEAPN = 2 * NLC + 1;
 static constexpr uint32_t LOOKMIN = 262;
-static constexpr uint32_t BITMAP_BITS = 65536;  // fast-mode insertion ring (positions mod 65536), in HBM/L2
+// fast-mode insertion ring, position mod 32768: queries are for chain nodes newer than p - MAX_DIST
+// (> p - 32768, so unambiguous); an older node only ever decides "no match within reach", which
+// holds whatever its (aliased) bit says, since every newer node is examined first
+static constexpr uint32_t BITMAP_BITS = 32768;
 static constexpr uint32_t HOLE_SLOTS = HOLE_SLOTS_M;   // fast mode: latest skipped position per hash slot
 
 struct TreeWork {      // one tree under construction (zlib's ct_data / heap / depth in LDS)
   uint32_t heap[HEAPN + 1];  // packed keys (freq:16 | depth:5 | node:10) in [1, heap_len]; node ids from heap_max
   uint16_t dad[HEAPN];
-  uint16_t anc[2][HEAPN];    // pointer-jumping scratch (depth computation)
-  uint8_t dep[2][HEAPN];
   uint16_t freq[NLC];        // leaf frequencies (forced leaves set to 1)
   uint8_t len[NLC];          // leaf code lengths
   uint16_t bl_count[16];
+};
+
+// Pointer-jumping scratch of gen_bitlen.  It lives in the match-table ring's LDS (the parse is
+// paused while a block is flushed; the ring is reloaded from HBM afterwards), which keeps the
+// trial kernels' LDS small enough for more waves per CU.
+struct TreeScratch {
+  uint16_t anc[2][HEAPN];
+  uint8_t dep[2][HEAPN];
 };
 
 struct BitOut {
@@ -546,6 +555,7 @@ struct TrialSharedSlow {
   TrialShared t;
   uint64_t ring[RING_SLOW];   // match-table entries (.x low, .y high) of the positions around the window
 };
+static_assert(sizeof(TreeScratch) <= RING_SLOW * sizeof(uint64_t), "tree scratch overlays the ring");
 
 struct SweepArgs {
   const uint8_t* file;          // original compressed bytes
@@ -668,7 +678,7 @@ __device__ __forceinline__ void pq_down(LDS uint32_t* heap, int heap_len, int k,
 
 // build_tree + gen_bitlen (Z/trees.c:488-565, 617-699) from w.freq[0..elems).  Leaves' lengths land
 // in w.len, bl_count in w.bl_count; opt_len / static_len accumulate as in zlib.  Returns max_code.
-__device__ __noinline__ int build_tree(LDS TreeWork& w, int elems, int max_length, const CONSTANT uint8_t* xbits,
+__device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, int elems, int max_length, const CONSTANT uint8_t* xbits,
                                        int xbase, const CONSTANT uint8_t* stlen, uint64_t& opt_len,
                                        uint64_t& static_len, LDS uint64_t& cyc_heap, int lane) {
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -726,15 +736,15 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, int elems, int max_lengt
   for (int i = lane; i < nn; i += 64) {
     const bool in_tree = i >= elems || (i <= max_code && w.freq[i] != 0);
     const bool r = (uint32_t)i == root || !in_tree;   // leaves outside the tree: never followed
-    w.anc[0][i] = r ? (uint16_t)root : w.dad[i];
-    w.dep[0][i] = r ? 0 : 1;
+    sc.anc[0][i] = r ? (uint16_t)root : w.dad[i];
+    sc.dep[0][i] = r ? 0 : 1;
   }
   int cur = 0;
   for (int round = 0; round < 5; round++) {
     for (int i = lane; i < nn; i += 64) {
-      const uint32_t a = w.anc[cur][i];
-      w.dep[cur ^ 1][i] = (uint8_t)(w.dep[cur][i] + w.dep[cur][a]);
-      w.anc[cur ^ 1][i] = w.anc[cur][a];
+      const uint32_t a = sc.anc[cur][i];
+      sc.dep[cur ^ 1][i] = (uint8_t)(sc.dep[cur][i] + sc.dep[cur][a]);
+      sc.anc[cur ^ 1][i] = sc.anc[cur][a];
     }
     cur ^= 1;
   }
@@ -746,7 +756,7 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, int elems, int max_lengt
     uint32_t bits = 0;
     if (i < nn) {
       in_tree = i >= elems || (i <= max_code && w.freq[i] != 0);   // internal node or leaf in the heap
-      bits = w.dep[cur][i];
+      bits = sc.dep[cur][i];
     }
     const bool capped = in_tree && (uint32_t)i != root && bits > (uint32_t)max_length;
     overflow += __popcll(__ballot(capped));
@@ -893,6 +903,22 @@ __device__ __forceinline__ uint32_t dcode_extra(uint32_t d) { return d < 2 ? 0u 
 __device__ __forceinline__ uint32_t dcode_base(uint32_t d) { return d < 2 ? d : ((2 + (d & 1)) << dcode_extra(d)); }  // base_dist[d]
 
 
+// Early-exit test after output progress: returns TR_* state to stop with, or ~0u to continue.
+__device__ inline uint32_t early_exit(const LDS BitOut& b, const SweepOpts& o, uint64_t best_ident, bool full_needed) {
+  if (b.overflow) return TR_OVERFLOW;
+  if (full_needed) return ~0u;
+  if (b.shortcut) {
+    uint64_t seen = b.pos < b.shortcut ? b.pos : b.shortcut;
+    uint64_t mism = seen - b.eq_sc;
+    uint64_t thr = o.shortcut_len - o.recomp_tresh;   // uint64 wrap as in main.cpp:649
+    if (thr > b.shortcut || mism > b.shortcut - thr) return TR_SHORTCUT;
+  }
+  if (b.pos > b.clen + o.sizediff_tresh) return TR_SIZEDIFF;
+  uint64_t seen = b.pos < b.clen ? b.pos : b.clen;
+  if (b.clen - (seen - b.eq_all) <= best_ident) return TR_CANT_BEAT;
+  return ~0u;
+}
+
 // Lane-parallel compress_block (Z/trees.c:1060-1105): 128 symbols per step, two per lane (one
 // 8-byte load), bit offsets by a wave prefix sum, words assembled with LDS atomics.
 static constexpr uint32_t SYM_PER_LANE = 2;
@@ -929,10 +955,13 @@ __device__ __forceinline__ void stage_or(LDS uint32_t* stage, uint32_t off, uint
   if ((uint32_t)(lo >> 32)) __atomic_fetch_or(&stage[wi + 1], (uint32_t)(lo >> 32), __ATOMIC_RELAXED);
   if (hi) __atomic_fetch_or(&stage[wi + 2], hi, __ATOMIC_RELAXED);
 }
+// The trial's outcome gates (early_exit) are monotone in the output emitted so far, so they are
+// tested after every step: a bailed trial stops inside its first block instead of emitting all of
+// it.  Returns true when the trial is decided (the caller re-evaluates early_exit).
 template <typename C16, typename C8>
-__device__ void compress_block(LDS BitOut& b, LDS TrialShared& s, const GLOBAL uint32_t* syms, uint32_t nsym,
-                               C16 lc, C8 ll, C16 dc, C8 dl,
-                               int lane) {
+__device__ bool compress_block(LDS BitOut& b, LDS TrialShared& s, const GLOBAL uint32_t* syms, uint32_t nsym,
+                               C16 lc, C8 ll, C16 dc, C8 dl, const SweepOpts& o, uint64_t best_ident,
+                               bool full_needed, int lane) {
   // the symbols were stored by other lanes during the parse: order those HBM stores before the reads
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   for (uint32_t base = 0; base <= nsym; base += 64 * SYM_PER_LANE) {
@@ -966,7 +995,9 @@ __device__ void compress_block(LDS BitOut& b, LDS TrialShared& s, const GLOBAL u
     const uint32_t lastw = s.stage[full >> 2];
     b.bb = rem ? ((lastw >> (8 * (full & 3))) & 0xff) & ((1u << rem) - 1) : 0;
     b.bc = rem;
+    if (!full_needed && early_exit(b, o, best_ident, false) != ~0u) return true;
   }
+  return false;
 }
 
 struct Lz {
@@ -1023,10 +1054,11 @@ __device__ inline uint32_t common_len(const uint8_t* in, uint64_t a, uint64_t b,
 // _tr_flush_block (Z/trees.c:907-1004) + FLUSH_BLOCK_ONLY bookkeeping
 // The parse state is passed by value so that it never leaves registers (a reference to it here
 // would put the whole parse state in scratch memory).  Returns the overlay-hazard bit.
-__device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, const GLOBAL uint32_t* syms,
+__device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch& sc, LDS BitOut& b, const GLOBAL uint32_t* syms,
                                              const GLOBAL uint8_t* in,
                                              int64_t block_start, uint64_t p, uint64_t S, uint32_t last_lit,
-                                             uint32_t level, uint32_t lbs, int last, int lane) {
+                                             uint32_t level, uint32_t lbs, int last, SweepOpts opt,
+                                             uint64_t best_ident, bool full_needed, int lane) {
   uint32_t hazard = 0;
   const uint64_t c0 = clock64();
   const bool bufok = block_start >= (int64_t)S;
@@ -1036,13 +1068,13 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, 
   if (level > 0) {
     // literal/length tree
     for (int i = lane; i < NLC; i += 64) s.w.freq[i] = (uint16_t)s.lfreq[i];
-    lmax = build_tree(s.w, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
+    lmax = build_tree(s.w, sc, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
                       opt_len, static_len, b.cyc_heap, lane);
     gen_codes(s.w, lmax, s.lcode, s.llen, lane);
     for (int i = lmax + 1 + lane; i < NLC + 2; i += 64) s.llen[i] = 0;
     // distance tree
     for (int i = lane; i < NDC; i += 64) s.w.freq[i] = (uint16_t)s.dfreq[i];
-    dmax = build_tree(s.w, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
+    dmax = build_tree(s.w, sc, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
                       opt_len, static_len, b.cyc_heap, lane);
     gen_codes(s.w, dmax, s.dcode, s.dlen, lane);
     for (int i = dmax + 1 + lane; i < NDC + 2; i += 64) s.dlen[i] = 0;
@@ -1052,7 +1084,7 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, 
     if (lane == 0) { scan_tree(s.bfreq, s.llen, lmax); scan_tree(s.bfreq, s.dlen, dmax); }
     b.cyc_scan += STEP_CLOCK() - cs0;
     for (int i = lane; i < NBLC; i += 64) s.w.freq[i] = (uint16_t)s.bfreq[i];
-    int bmax = build_tree(s.w, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, opt_len, static_len, b.cyc_heap, lane);
+    int bmax = build_tree(s.w, sc, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, opt_len, static_len, b.cyc_heap, lane);
     gen_codes(s.w, bmax, s.bcode, s.blen, lane);
     for (int i = bmax + 1 + lane; i < NBLC + 2; i += 64) s.blen[i] = 0;
     for (max_blindex = NBLC - 1; max_blindex >= 3; max_blindex--)
@@ -1086,11 +1118,13 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, 
         s.stage[k] = wv;
       }
       emit_bytes_from_stage(b, s.stage, nb, lane);
+      if (!full_needed && early_exit(b, opt, best_ident, false) != ~0u) break;
     }
   } else if (static_lenb == opt_lenb) {
     put_bits(b, s.stage, (1u << 1) + (uint32_t)last, 3, lane);
     compress_block(b, s, syms, last_lit, (const CONSTANT uint16_t*)c_t.st_lcode, (const CONSTANT uint8_t*)c_t.st_llen,
-                   (const CONSTANT uint16_t*)c_t.st_dcode, (const CONSTANT uint8_t*)c_t.st_dlen, lane);
+                   (const CONSTANT uint16_t*)c_t.st_dcode, (const CONSTANT uint8_t*)c_t.st_dlen, opt, best_ident,
+                   full_needed, lane);
   } else {
     int lcodes = lmax + 1, dcodes = dmax + 1, blcodes = max_blindex + 1;
     put_bits(b, s.stage, (2u << 1) + (uint32_t)last, 3, lane);
@@ -1104,7 +1138,7 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, 
     b.cyc_send += STEP_CLOCK() - cs0;
     flush_bits_bytes(b, s.stage, lane);
     compress_block(b, s, syms, last_lit, (const LDS uint16_t*)s.lcode, (const LDS uint8_t*)s.llen,
-                   (const LDS uint16_t*)s.dcode, (const LDS uint8_t*)s.dlen, lane);
+                   (const LDS uint16_t*)s.dcode, (const LDS uint8_t*)s.dlen, opt, best_ident, full_needed, lane);
   }
   // 1.2.8 pending_buf/d_buf overlay condition (conservative, cf. oracle/ora_deflate.c)
   if (b.pos - blk_start_bytes > (uint64_t)lbs + 2ull * last_lit && last_lit) hazard = 1;
@@ -1115,22 +1149,6 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS BitOut& b, 
   if (last) windup(b, s.stage, lane);
   b.cyc_emit += clock64() - c1;
   return hazard;
-}
-
-// Early-exit test after output progress: returns TR_* state to stop with, or ~0u to continue.
-__device__ inline uint32_t early_exit(const LDS BitOut& b, const SweepOpts& o, uint64_t best_ident, bool full_needed) {
-  if (b.overflow) return TR_OVERFLOW;
-  if (full_needed) return ~0u;
-  if (b.shortcut) {
-    uint64_t seen = b.pos < b.shortcut ? b.pos : b.shortcut;
-    uint64_t mism = seen - b.eq_sc;
-    uint64_t thr = o.shortcut_len - o.recomp_tresh;   // uint64 wrap as in main.cpp:649
-    if (thr > b.shortcut || mism > b.shortcut - thr) return TR_SHORTCUT;
-  }
-  if (b.pos > b.clen + o.sizediff_tresh) return TR_SIZEDIFF;
-  uint64_t seen = b.pos < b.clen ? b.pos : b.clen;
-  if (b.clen - (seen - b.eq_all) <= best_ident) return TR_CANT_BEAT;
-  return ~0u;
 }
 
 // The parse path through a window of 64 lanes (lane i = position wb + i).  Lane i's node kind:
@@ -1231,11 +1249,6 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   if (lane == 0) s.lfreq[256] = 1;
   uint32_t hazard = 0;
   // Symbols and block statistics are tallied straight into HBM (syms) and LDS (lfreq / dfreq).
-  auto FLUSH = [&](int last) {
-    hazard |= uni(flush_block(s, b, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, lane));
-    z.last_lit = 0;
-    z.block_start = z.p;
-  };
   uint32_t state = ~0u;
   uint64_t fallbacks = 0, cyc_fb = 0;
   uint64_t csec[4] = {0, 0, 0, 0};   // diagnostics (ATZ_STEP_CLOCKS)
@@ -1268,6 +1281,19 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   uint32_t hi = 0;
   uint64_t pf = 0;
   if (KIND != 0 && n) pf = Rt[lane];
+  auto FLUSH = [&](int last) {
+    hazard |= uni(flush_block(s, *(LDS TreeScratch*)ring, b, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in,
+                              (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, A.o, tr.best_ident,
+                              full_needed, lane));
+    z.last_lit = 0;
+    z.block_start = z.p;
+    if constexpr (KIND != 0) {   // the tree scratch overlaid the ring: reload its resident chunks
+      for (uint32_t c0 = hi >= RING_SLOW ? hi - RING_SLOW : 0u; c0 < hi; c0 += 64) {
+        const uint32_t pos = c0 + (uint32_t)lane;
+        if (pos < n) ring[pos & (RING_SLOW - 1)] = Rt[pos];
+      }
+    }
+  };
   if constexpr (KIND == 0) {
     // deflate_stored (Z/deflate.c:1564-1619)
     uint64_t max_block = 0xffff;
