@@ -231,39 +231,35 @@ __global__ __launch_bounds__(256) void k_buckets_lds(const uint8_t* __restrict__
   for (uint32_t g = wave * q; g < (wave + 1) * q; g += 64) word[g + lane] = (word[g + lane] + off) << 16;
   __syncthreads();
   if (wave != 0) return;
-  uint32_t hn = lane < (int)nh ? hash((uint32_t)lane) : 0x3ffffffu;
+  // In-order assignment, 64 positions at a time: one LDS atomic per lane gives (bucket base,
+  // assigned so far).  Lanes of one batch that share a hash receive their ranks in an undefined
+  // order; a read-back after the batch's atomics shows them (the count moved by more than one),
+  // and only those groups (rare: ~6 % of batches at hash_bits 15) are re-ranked by lane.
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t hn = lane < (int)nh ? hash((uint32_t)lane) : 0u;
   for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
     const uint32_t h = hn;
-    const uint32_t pn = b0 + 64 + lane;
-    hn = pn < nh ? hash(pn) : 0x3ffffffu;
-    uint32_t key = (h << 6) | (uint32_t)lane;
-    for (int k = 2; k <= 64; k <<= 1)
-      for (int st = k >> 1; st > 0; st >>= 1) {
-        const uint32_t o = __shfl_xor(key, st, 64);
-        const bool up = (lane & k) == 0, lower = (lane & st) == 0;
-        const uint32_t mn = key < o ? key : o, mx = key < o ? o : key;
-        key = (lower == up) ? mn : mx;
-      }
-    const uint32_t kh = key >> 6;
-    const uint32_t mypos = b0 + (key & 63);
-    const uint32_t pk = __shfl_up(key, 1, 64), nk = __shfl_down(key, 1, 64);
-    const bool first = lane == 0 || (pk >> 6) != kh;
-    const bool last = lane == 63 || (nk >> 6) != kh;
-    const bool real = kh != 0x3ffffffu;
-    const uint64_t fm = __ballot(first);
-    const uint64_t below = fm & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-    const uint32_t gstart = 63 - (uint32_t)__clzll((long long)below);
-    const uint64_t lm = __ballot(last);
-    const uint64_t above = lm & (~0ull << lane);
-    const uint32_t gend = (uint32_t)__ffsll((unsigned long long)above) - 1;
+    const uint32_t p = b0 + (uint32_t)lane;
+    const uint32_t pn = p + 64;
+    hn = pn < nh ? hash(pn) : 0u;
+    const bool real = p < nh;
     uint32_t old = 0;
-    if (real && first) old = atomicAdd(&word[kh], gend - gstart + 1);
-    old = __shfl(old, (int)gstart, 64);
+    if (real) old = atomicAdd(&word[h], 1u);
+    const uint32_t cur = real ? __hip_atomic_load(&word[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+    uint32_t r = old & 0xffffu;
+    uint64_t todo = __ballot(real && (cur & 0xffffu) != r + 1u);
+    while (todo) {
+      const int l0 = __ffsll((unsigned long long)todo) - 1;
+      const uint32_t hh = (uint32_t)__builtin_amdgcn_readlane((int)h, l0);
+      const uint64_t g = __ballot(real && h == hh);
+      const uint32_t end = (uint32_t)__builtin_amdgcn_readlane((int)cur, l0) & 0xffffu;
+      if (real && h == hh) r = end - (uint32_t)__popcll(g) + (uint32_t)__popcll(g & lt);
+      todo &= ~g;
+    }
     if (real) {
-      const uint32_t r = (old & 0xffffu) + (uint32_t)lane - gstart;
       const uint32_t at = (old >> 16) + r;
-      sidx[mypos] = at;
-      bpos[at] = mypos | (r == 0 ? BUCKET_FIRST : 0u);
+      sidx[p] = at;
+      bpos[at] = p | (r == 0 ? BUCKET_FIRST : 0u);
     }
   }
 }
@@ -328,46 +324,36 @@ __global__ __launch_bounds__(256) void k_buckets_lds9(const uint8_t* __restrict_
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   if (wave != 0) return;
-  uint32_t hn = lane < (int)nh ? hash((uint32_t)lane) : 0xffffffffu;
-  uint32_t bn = hn != 0xffffffffu ? base[hn] : 0u;
+  // in-order assignment as in k_buckets_lds (one atomic per lane on the hash's 16-bit field, a
+  // read-back to find the lanes that shared a field, re-ranked by lane)
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t hn = lane < (int)nh ? hash((uint32_t)lane) : 0u;
+  uint32_t bn = lane < (int)nh ? base[hn] : 0u;
   for (uint32_t b0 = 0; b0 < nh; b0 += 64) {
     const uint32_t h = hn, bh = bn;
-    const uint32_t pn = b0 + 64 + lane;
-    hn = pn < nh ? hash(pn) : 0xffffffffu;
-    bn = hn != 0xffffffffu ? base[hn] : 0u;
-    const bool real = h != 0xffffffffu;
-    // sort (hash, lane) so equal hashes form groups in position order
-    uint64_t key = ((uint64_t)(real ? h : 0x1ffffu) << 6) | (uint32_t)lane;
-    for (int k = 2; k <= 64; k <<= 1)
-      for (int st = k >> 1; st > 0; st >>= 1) {
-        const uint32_t lo = __shfl_xor((uint32_t)key, st, 64), hi = __shfl_xor((uint32_t)(key >> 32), st, 64);
-        const uint64_t o = ((uint64_t)hi << 32) | lo;
-        const bool up = (lane & k) == 0, lower = (lane & st) == 0;
-        const uint64_t mn = key < o ? key : o, mx = key < o ? o : key;
-        key = (lower == up) ? mn : mx;
-      }
-    const uint32_t src = (uint32_t)(key & 63);
-    const uint32_t kh = (uint32_t)(key >> 6);
-    const uint32_t mypos = b0 + src;
-    const uint32_t mybase = __shfl(bh, (int)src, 64);
-    const uint32_t pk = __shfl_up(kh, 1, 64), nk = __shfl_down(kh, 1, 64);
-    const bool first = lane == 0 || pk != kh;
-    const bool last = lane == 63 || nk != kh;
-    const bool rl = kh != 0x1ffffu;
-    const uint64_t fm = __ballot(first);
-    const uint64_t below = fm & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-    const uint32_t gstart = 63 - (uint32_t)__clzll((long long)below);
-    const uint64_t lm = __ballot(last);
-    const uint64_t above = lm & (~0ull << lane);
-    const uint32_t gend = (uint32_t)__ffsll((unsigned long long)above) - 1;
+    const uint32_t p = b0 + (uint32_t)lane;
+    const uint32_t pn = p + 64;
+    hn = pn < nh ? hash(pn) : 0u;
+    bn = pn < nh ? base[hn] : 0u;
+    const bool real = p < nh;
+    const uint32_t sh = 16u * (h & 1u);
     uint32_t old = 0;
-    if (rl && first) old = atomicAdd(&pair[kh >> 1], (gend - gstart + 1) << (16 * (kh & 1)));
-    old = (__shfl(old, (int)gstart, 64) >> (16 * (kh & 1))) & 0xffffu;
-    if (rl) {
-      const uint32_t r = old + (uint32_t)lane - gstart;
-      const uint32_t at = mybase + r;
-      sidx[mypos] = at;
-      bpos[at] = mypos | (r == 0 ? BUCKET_FIRST : 0u);
+    if (real) old = atomicAdd(&pair[h >> 1], 1u << sh);
+    const uint32_t cur = real ? __hip_atomic_load(&pair[h >> 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+    uint32_t r = (old >> sh) & 0xffffu;
+    uint64_t todo = __ballot(real && ((cur >> sh) & 0xffffu) != r + 1u);
+    while (todo) {
+      const int l0 = __ffsll((unsigned long long)todo) - 1;
+      const uint32_t hh = (uint32_t)__builtin_amdgcn_readlane((int)h, l0);
+      const uint64_t g = __ballot(real && h == hh);
+      const uint32_t end = ((uint32_t)__builtin_amdgcn_readlane((int)cur, l0) >> (16u * (hh & 1u))) & 0xffffu;
+      if (real && h == hh) r = end - (uint32_t)__popcll(g) + (uint32_t)__popcll(g & lt);
+      todo &= ~g;
+    }
+    if (real) {
+      const uint32_t at = bh + r;
+      sidx[p] = at;
+      bpos[at] = p | (r == 0 ? BUCKET_FIRST : 0u);
     }
   }
 }
