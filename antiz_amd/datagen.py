@@ -149,7 +149,7 @@ def _c4_piece(args):
         c = int(rng.integers(1, 10))
         m = int(rng.integers(1, 10))
         w = 15 if wrange is None else int(rng.integers(wrange[0], wrange[1] + 1))
-        payload = int(rng.integers(20000, 30001))
+        payload = int(rng.integers(12500, 18751))   # ~10 KB compressed, 100k streams ~ 1 GB
         gap = int(rng.integers(0, 65))
         out.append(rng.integers(0, 256, size=gap, dtype=np.uint8).tobytes())
         out.append(zstream(text(rng, payload), c, w, m))

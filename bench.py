@@ -89,7 +89,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--streams", type=int, default=100000, help="streams per rank (C4: 100000 = 1 GB)")
-    ap.add_argument("--cpu-sample-streams", type=int, default=3000)
+    ap.add_argument("--cpu-sample-streams", type=int, default=8000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cache", default=os.environ.get("ATZ_BENCH_CACHE", "/tmp/atz_bench_cache"))
     args = ap.parse_args()

@@ -1,0 +1,29 @@
+#!/bin/bash
+# One GPU call: parity suite, default bench line (with CPU baseline), rocprofv3 kernel stats of one
+# step, and separate PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic.  Every GPU step has its
+# own time limit; the chain stops at the first failure.
+# usage: tools/gpu_measure.sh <tag> [stages...]   stages: test bench prof pmc (default: all)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+TAG=${1:-run}; shift
+STAGES=${*:-"test bench prof pmc"}
+O=gpurun_out/$TAG; mkdir -p $O
+has() { [[ " $STAGES " == *" $1 "* ]]; }
+# workload generated once, before any timed/profiled run
+timeout -k 10 300 python3 -c "
+import sys; sys.path.insert(0,'.')
+from antiz_amd import datagen; print(datagen.cached('c4','/tmp/atz_bench_cache',seed=4,n_streams=100000))" > $O/gen.log 2>&1 || exit 1
+if has test; then
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/test.log 2>&1 || exit 2
+fi
+if has bench; then
+  timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || exit 3
+fi
+if has prof; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o p --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu > $O/prof.json 2> $O/prof.err || exit 4
+fi
+if has pmc; then
+  timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmcf -o p --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu > $O/pmcf.json 2> $O/pmcf.err || exit 5
+  timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -d $O/pmcw -o p --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu > $O/pmcw.json 2> $O/pmcw.err || exit 6
+fi
+echo done
