@@ -350,7 +350,7 @@ static bool timing_on() {
 }
 
 static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, const std::vector<InfJob>& jobs,
-                            std::vector<InfRes>& res, uint64_t arena_cap = 0) {
+                            std::vector<InfRes>& res, uint64_t arena_cap = 0, bool full_ring = false) {
   res.resize(jobs.size());
   if (jobs.empty()) return 0;
   if (int r = upload(c, c->d_jobs, jobs.data(), jobs.size() * sizeof(InfJob))) return r;
@@ -361,15 +361,41 @@ static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, con
     HIPCHK(hipMemsetAsync(c->d_arena_used.p, 0, 8, c->st));
   }
   uint32_t n = (uint32_t)jobs.size();
+  // The 8 KiB-ring decoder needs an HBM copy of its output for matches beyond the ring: every job
+  // writes to a destination or an arena slot.  Jobs without output use the 32 KiB ring.
+  bool small = !full_ring;
+  for (const InfJob& jb : jobs) small = small && jb.out_off != NO_OUT;
   kbeg(c, 1);
-  hipLaunchKernelGGL(k_inflate, dim3(n), dim3(64), 0, c->st, d_in,
-                     d_out, c->d_jobs.as<InfJob>(), c->d_res.as<InfRes>(), n, c->d_arena.as<uint8_t>(),
-                     c->d_arena_used.as<unsigned long long>(), arena_cap);
+  if (small)
+    hipLaunchKernelGGL(k_inflate<INF_RING_SMALL>, dim3(n), dim3(64), 0, c->st, d_in,
+                       d_out, c->d_jobs.as<InfJob>(), c->d_res.as<InfRes>(), n, c->d_arena.as<uint8_t>(),
+                       c->d_arena_used.as<unsigned long long>(), arena_cap);
+  else
+    hipLaunchKernelGGL(k_inflate<INF_RING_FULL>, dim3(n), dim3(64), 0, c->st, d_in,
+                       d_out, c->d_jobs.as<InfJob>(), c->d_res.as<InfRes>(), n, c->d_arena.as<uint8_t>(),
+                       c->d_arena_used.as<unsigned long long>(), arena_cap);
   kend(c);
   KCHECK("k_inflate");
   HIPCHK(hipMemcpyAsync(res.data(), c->d_res.p, n * sizeof(InfRes), hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
   kcollect(c);
+  if (small) {   // jobs whose far history was lost (arena full / slot overflowed): 32 KiB ring, no slot
+    std::vector<InfJob> rj;
+    std::vector<uint32_t> ri;
+    for (uint32_t k = 0; k < n; k++)
+      if (res[k].status == INF_RETRY) {
+        InfJob jb = jobs[k];
+        if (jb.out_off == ARENA_OUT) { jb.out_off = NO_OUT; jb.out_cap = 0; }
+        rj.push_back(jb);
+        ri.push_back(k);
+      }
+    if (!rj.empty()) {
+      std::vector<InfRes> rr;
+      if (int r = run_inflate_jobs(c, d_in, d_out, rj, rr, 0, true)) return r;
+      for (size_t q = 0; q < ri.size(); q++) res[ri[q]] = rr[q];
+      c->stats.n_inflate_retries += rj.size();
+    }
+  }
   for (uint32_t k = 0; k < n; k++)   // bytes read + bytes written (when kept)
     c->stats.k_inflate_alg_bytes += res[k].consumed + (jobs[k].out_off == NO_OUT ? 0 : res[k].produced);
   if (timing_on() && ATZ_INF_CLOCKS) {   // diagnostics build: clocks per job / per symbol
@@ -518,7 +544,9 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
         fidx.push_back(k);
       }
     std::vector<InfRes> fr, vr;
-    const uint64_t arena_cap = std::min<uint64_t>(16ull << 30, std::max<uint64_t>(256ull << 20, 6 * F));
+    // a slot (ARENA_SLOT) is claimed at a candidate's first flush (4 KiB of output): room for a slot
+    // per ~64 input bytes, capped -- slots are only written as far as the output goes
+    const uint64_t arena_cap = std::min<uint64_t>(64ull << 30, std::max<uint64_t>(1ull << 30, 16 * F));
     if (int r = run_inflate_jobs(c, d_file, nullptr, fjobs, fr, arena_cap)) return r;
     if (!vjobs.empty()) {
       if (int r = upload(c, c->d_virt, virt.data(), virt.size())) return r;

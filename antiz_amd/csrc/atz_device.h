@@ -18,7 +18,7 @@ static constexpr uint64_t NO_OUT = ~0ull;
 static constexpr uint64_t ARENA_OUT = ~1ull;   // output into the arena: a slot of out_cap bytes claimed at first flush
 static constexpr uint64_t ARENA_NONE = ~0ull;
 
-enum : uint32_t { INF_END = 0, INF_ERROR = 1, INF_NEED = 2 };
+enum : uint32_t { INF_END = 0, INF_ERROR = 1, INF_NEED = 2, INF_RETRY = 3 };   // RETRY: rerun with the 32 KiB ring
 
 struct InfRes {
   uint32_t status;    // INF_*

@@ -15,9 +15,20 @@
 
 namespace atz {
 
-static constexpr uint32_t RING = 32768;        // history ring per wave (LDS)
-static constexpr uint32_t RMASK = RING - 1;
-static constexpr uint32_t FLUSH_AT = 16384;    // flush ring to HBM / Adler every 16 KiB
+// History: the last RING output bytes live in an LDS ring per wave.  RING = 32 KiB holds the whole
+// deflate window.  A smaller ring (INF_RING_SMALL) raises occupancy from 4 to 16 waves per CU (measured on C4: k_inflate 396 -> 154 ms; a 16 KiB ring at 8 waves/CU: 257 ms) (the
+// decode is a serial per-stream chain, so resident waves are the throughput); a match reaching further
+// back than the ring reads the bytes from the job's output in HBM, which the ring flushes every RING/2
+// bytes.  A job that has no such output left (no slot, or its slot overflowed) stops with INF_RETRY and
+// the host runs it again with the 32 KiB ring.
+static constexpr uint32_t INF_RING_FULL = 32768;
+#ifndef INF_RING_SMALL_BYTES
+#define INF_RING_SMALL_BYTES 8192
+#endif
+static constexpr uint32_t INF_RING_SMALL = INF_RING_SMALL_BYTES;
+#ifndef INF_SMALL_WAVES
+#define INF_SMALL_WAVES 4   // waves per SIMD the small-ring decoder is register-bounded for (C4 k_inflate: 3 -> 183 ms, 4 -> 154 ms)
+#endif
 #ifndef ATZ_INF_CLOCKS
 #define ATZ_INF_CLOCKS 0                       // 1: per-job clocks and symbol counts in InfRes
 #endif
@@ -149,19 +160,23 @@ struct Huff {
   }
 };
 
-enum { R_OK = 0, R_ERR = -1, R_NEED = -2 };
+enum { R_OK = 0, R_ERR = -1, R_NEED = -2, R_RETRY = -3 };
 
+template <uint32_t RING>
 struct InfShared {
   uint8_t ring[RING];
   uint16_t lens[320];
   uint16_t sort[384];
 };
 
-__global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_base, uint8_t* __restrict__ out_base,
+template <uint32_t RING>
+__global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) void k_inflate(const uint8_t* __restrict__ in_base, uint8_t* __restrict__ out_base,
                                                const InfJob* __restrict__ jobs, InfRes* __restrict__ res,
                                                uint32_t njobs, uint8_t* __restrict__ arena,
                                                unsigned long long* __restrict__ arena_used, uint64_t arena_cap) {
-  __shared__ InfShared sh;
+  constexpr uint32_t RMASK = RING - 1;
+  constexpr uint32_t FLUSH_AT = RING / 2;   // unflushed bytes stay <= FLUSH_AT + 258 + 64 < RING
+  __shared__ InfShared<RING> sh;
   const int lane = threadIdx.x;
   const uint32_t j = blockIdx.x;
   if (j >= njobs) return;
@@ -284,10 +299,27 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
     if (ATZ_INF_CLOCKS) nlit++;
     if (nst == 64) stage_flush();
   };
-  // copy `len` bytes from `dist` back (dist <= prod); the stage must be empty
-  auto copy = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) {
+  // copy `len` bytes from `dist` back (dist <= prod); the stage must be empty.  False: the source is
+  // beyond the ring and no HBM copy of it exists (R_RETRY).
+  auto copy = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) -> bool {
     if (ATZ_INF_CLOCKS) nmatch++;
-    if (dist >= len) {
+    if (RING < INF_RING_FULL && dist > RING) {
+      // Far source: [prod - dist, prod - dist + len) ends at least RING - 258 bytes back, so it was
+      // flushed (unflushed bytes < RING/2 + 322) -- if this job's output still exists.  dist > RING
+      // > len, so the copy does not overlap itself.  The flush's stores are drained first and the
+      // loads are agent-coherent (L1 bypassed: a line may have been cached before it was complete).
+      const uint64_t src = prod - dist;
+      const uint64_t valid = flushed < out_cap ? flushed : out_cap;
+      if (!out || src + len > valid) return false;
+      __builtin_amdgcn_s_waitcnt(0);
+      for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        if (i < len) {
+          const uint8_t v = __hip_atomic_load(out + src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ring[(prod + i) & RMASK] = v;
+        }
+      }
+    } else if (dist >= len) {
       for (uint32_t i0 = 0; i0 < len; i0 += 64) {
         const uint32_t i = i0 + lane;
         uint8_t v = 0;
@@ -306,6 +338,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
     }
     prod += len;
     if (prod - flushed >= FLUSH_AT) flush(false);
+    return true;
   };
 
   // inflate_table acceptance (Z/inftrees.c:32-141); type 0 CODES, 1 LENS, 2 DISTS. Returns 0 / -1.
@@ -455,13 +488,12 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
           const uint64_t tc0 = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
           stage_flush();
           if ((uint64_t)dist > prod) { errneed = pos0 + used; errcode = 14; rc = R_ERR; break; }   // too far back
-          copy(len, dist);
+          if (!copy(len, dist)) { rc = R_RETRY; break; }
           if (ATZ_INF_CLOCKS) cyc_copy += __builtin_amdgcn_s_memtime() - tc0;
         }
         pos = pos0 + used;
         if (bc <= 32) refill();
-        if (rc == R_OK) return R_OK;
-        if (rc == R_ERR) return R_ERR;
+        if (rc != 1) return rc;
         continue;
       }
       // ---- careful path (the last 8 input bytes): zlib's NEEDBITS points exactly
@@ -487,7 +519,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
       drop(de);
       stage_flush();
       if ((uint64_t)dist > prod) FAIL(14, pos);            // invalid distance too far back
-      copy(len, dist);
+      if (!copy(len, dist)) return R_RETRY;
     }
   };
 
@@ -617,7 +649,11 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in_b
   o.arena_off = (rr == R_OK && to_arena) ? arena_off : ARENA_NONE;
   o.produced = prod;
   o.err = errcode;
-  if (rr == R_OK && !overflow) {
+  if (rr == R_RETRY) {
+    o.status = INF_RETRY;
+    o.consumed = 0;
+    o.arena_off = ARENA_NONE;
+  } else if (rr == R_OK && !overflow) {
     o.status = INF_END;
     o.consumed = (pos - skip_bits) >> 3;
   } else if (rr == R_NEED) {

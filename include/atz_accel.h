@@ -73,6 +73,7 @@ typedef struct {
     uint64_t trial_cyc_heap, trial_cyc_fallback, trial_symbols;   /* heap: ATZ_STEP_CLOCKS builds only */
     uint64_t n_trials_speculative;                       /* trials run ahead of a stream's stop and discarded */
     uint64_t n_reinflated;                               /* recorded streams inflated again (scan output not kept) */
+    uint64_t n_inflate_retries;                          /* inflates rerun with the 32 KiB history ring */
 } atz_stats_t;
 
 enum {
