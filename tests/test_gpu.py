@@ -180,3 +180,34 @@ def test_roundtrip_large_mixed(atz):
         out, st = c.precompress(data)
         assert st["n_streams"] > 1000
         assert c.reconstruct(out) == data
+
+
+def test_far_history_and_ring_retry(atz):
+    """The 8 KiB-ring decoder: matches beyond the ring read the job's HBM output; a stream longer than
+    its 64 KiB arena slot loses that copy and is rerun on the 32 KiB ring.  Streams with long-distance
+    matches (a repeated 20 KiB block) of 30 KiB .. 400 KiB output, at every window, must give the
+    oracle's .atz bytes."""
+    rng = random.Random(11)
+    parts = []
+    for k, (n, w) in enumerate([(30000, 15), (90000, 15), (400000, 15), (70000, 14), (50000, 13)]):
+        block = _libs.text(rng, 20000)
+        d = (block * (n // len(block) + 1))[:n]
+        s, _ = _libs.ora_deflate(d, [6, 9, 1, 4, 6][k], w, 8)
+        parts.append(bytes(rng.getrandbits(8) for _ in range(17)) + s)
+    data = b"".join(parts)
+    rc, ref, st_ref = _libs.ora_precompress(data, chunksize=1 << 22)
+    assert rc == 0
+    with atz.Context(chunksize=1 << 22) as c:
+        out, st = c.precompress(data)
+        assert st["n_streams"] == 5
+        assert st["n_inflate_retries"] >= 1, st       # the 400 KiB stream overflowed its slot
+        assert sha(out) == sha(ref)
+        assert c.reconstruct(out) == data
+    # direct batch inflate into exact destinations (far reads from the destination buffer)
+    with atz.Context() as c:
+        offs, lens, pos = [], [], 0
+        for p in parts:
+            offs.append(pos + 17); lens.append(len(p) - 17); pos += len(p)
+        got = c.inflate_batch(data, list(zip(offs, lens)))
+        for (rc2, cons, prod), l in zip(got, lens):
+            assert rc2 == 0 and cons == l
