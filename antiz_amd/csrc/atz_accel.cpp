@@ -260,7 +260,7 @@ struct atz_ctx {
   atz_opts_t o{};
   int dev = 0;
   hipStream_t st = nullptr;
-  DBuf d_file, d_pos, d_cnt, d_jobs, d_res, d_virt, d_infl, d_chains, d_heads, d_streams, d_trials,
+  DBuf d_file, d_pos, d_cnt, d_hbase, d_jobs, d_res, d_virt, d_infl, d_chains, d_heads, d_streams, d_trials,
       d_tres, d_out, d_syms, d_adler, d_meta, d_segs, d_atz, d_diffjobs, d_diffpos, d_diffval, d_diffcnt,
       d_cjobs, d_cjobs2, d_cjobs3, d_heads2, d_tmp, d_R, d_mjobs, d_ins, d_arena, d_arena_used;
   // last scan
@@ -350,13 +350,14 @@ static bool timing_on() {
 }
 
 static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, const std::vector<InfJob>& jobs,
-                            std::vector<InfRes>& res, uint64_t arena_cap = 0, bool full_ring = false) {
+                            std::vector<InfRes>& res, uint64_t arena_cap = 0, bool full_ring = false,
+                            bool arena_reset = true) {
   res.resize(jobs.size());
   if (jobs.empty()) return 0;
   if (int r = upload(c, c->d_jobs, jobs.data(), jobs.size() * sizeof(InfJob))) return r;
   if (int r = c->d_res.reserve(jobs.size() * sizeof(InfRes))) return r;
   if (int r = c->d_arena_used.reserve(64)) return r;
-  if (arena_cap) {
+  if (arena_cap && arena_reset) {
     if (int r = c->d_arena.reserve(arena_cap)) return r;
     HIPCHK(hipMemsetAsync(c->d_arena_used.p, 0, 8, c->st));
   }
@@ -460,39 +461,50 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       pos += gg;
     }
   }
-  // ---- all header pairs of the file (GPU) ----
-  uint64_t cap = F / 8 + 1024;
-  if (int r = c->d_pos.reserve(cap * 8)) return r;
-  if (int r = c->d_cnt.reserve(64)) return r;
-  HIPCHK(hipMemsetAsync(c->d_cnt.p, 0, 8, c->st));
+  // ---- all header pairs of the file, in file order (GPU: count pass, host prefix, write pass),
+  // packed position << 5 | header type ----
+  std::vector<uint64_t> pairs;
   {
-    uint64_t blocks = (F + 256 * 16 - 1) / (256 * 16);
-    if (blocks > 8192) blocks = 8192;
-    if (blocks == 0) blocks = 1;
+    const uint64_t nb = std::max<uint64_t>(1, std::min<uint64_t>(8192, (F + 65535) / 65536));
+    const uint64_t seg = ((F + nb - 1) / nb + 4095) & ~4095ull;
+    if (int r = c->d_cnt.reserve(nb * 4 + 64)) return r;
+    if (int r = c->d_hbase.reserve(nb * 8 + 64)) return r;
     kbeg(c, 3);
-    hipLaunchKernelGGL(k_find_headers, dim3((uint32_t)blocks), dim3(256), 0, c->st, d_file, F,
-                       c->d_pos.as<uint64_t>(), c->d_cnt.as<unsigned long long>(), cap);
+    hipLaunchKernelGGL(k_headers_ordered, dim3((uint32_t)nb), dim3(256), 0, c->st, d_file, F, seg,
+                       c->d_cnt.as<uint32_t>(), nullptr, nullptr, 0);
     kend(c);
-    KCHECK("k_find_headers");
+    KCHECK("k_headers_ordered");
+    std::vector<uint32_t> cnt(nb);
+    HIPCHK(hipMemcpyAsync(cnt.data(), c->d_cnt.p, nb * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    std::vector<uint64_t> hb(nb);
+    uint64_t npairs = 0;
+    for (uint64_t b = 0; b < nb; b++) { hb[b] = npairs; npairs += cnt[b]; }
+    if (npairs) {
+      if (int r = upload(c, c->d_hbase, hb.data(), nb * 8)) return r;
+      if (int r = c->d_pos.reserve(npairs * 8 + 64)) return r;
+      kbeg(c, 3);
+      hipLaunchKernelGGL(k_headers_ordered, dim3((uint32_t)nb), dim3(256), 0, c->st, d_file, F, seg,
+                         nullptr, c->d_hbase.as<uint64_t>(), c->d_pos.as<uint64_t>(), 1);
+      kend(c);
+      KCHECK("k_headers_ordered");
+      pairs.resize(npairs);
+      HIPCHK(hipMemcpyAsync(pairs.data(), c->d_pos.p, npairs * 8, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipStreamSynchronize(c->st));
+    }
+    kcollect(c);
   }
-  TMARK("scan: layout+find launch");
-  uint64_t npairs = 0;
-  HIPCHK(hipMemcpyAsync(&npairs, c->d_cnt.p, 8, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
-  kcollect(c);
-  if (npairs > cap) return ATZ_E_INTERNAL;
-  std::vector<uint64_t> pairs(npairs);
-  if (npairs) {
-    HIPCHK(hipMemcpy(pairs.data(), c->d_pos.p, npairs * 8, hipMemcpyDeviceToHost));
-    std::sort(pairs.begin(), pairs.end());
-  }
-  TMARK("scan: pairs d2h+sort");
+  TMARK("scan: layout+ordered pairs");
   // ---- candidates per chunk: i >= 1 are file pairs, i == 0 uses buffer[0] ----
-  struct Cand { uint32_t chunk; uint64_t i; int type; uint64_t job; };
+  // Cand.job: index into fjobs (file-backed, output kept in an arena slot) or VJOB | index into
+  // vjobs (materialized buffers: chunk starts whose buffer[0] is not the file byte)
+  static constexpr uint64_t VJOB = 1ull << 63;
+  struct Cand { uint32_t chunk; int32_t type; uint64_t i; uint64_t job; };
   std::vector<Cand> cands;
-  std::vector<InfJob> jobs, vjobs;     // file-backed jobs / jobs on materialized buffers (i==0, b0 != file)
-  std::vector<uint64_t> vjob_of;       // job index -> vjobs index (+1), 0 if file-backed
+  std::vector<InfJob> fjobs, vjobs;
   std::vector<uint8_t> virt;
+  cands.reserve(pairs.size() + chunks.size());
+  fjobs.reserve(pairs.size() + chunks.size());
   {
     size_t pi = 0;
     for (uint32_t j = 0; j < chunks.size(); j++) {
@@ -501,62 +513,45 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       int t0 = header_type_host(ch.b0, h[ch.co + 1]);
       if (t0 >= 0) {
         InfJob jb;
-        jb.in_len = ch.len; jb.out_off = NO_OUT; jb.out_cap = 0;
+        jb.in_len = ch.len;
         if (ch.b0_file) {
-          jb.in_off = ch.co;
-          vjob_of.push_back(0);
+          jb.in_off = ch.co; jb.out_off = ARENA_OUT; jb.out_cap = ARENA_SLOT;
+          cands.push_back({j, t0, 0, fjobs.size()});
+          fjobs.push_back(jb);
         } else {
-          jb.in_off = virt.size();
+          jb.in_off = virt.size(); jb.out_off = NO_OUT; jb.out_cap = 0;
           std::vector<uint8_t> v;
           chunk_bytes(h, ch, v);
           virt.insert(virt.end(), v.begin(), v.end());
           virt.resize((virt.size() + 3) & ~(size_t)3);
+          cands.push_back({j, t0, 0, VJOB | vjobs.size()});
           vjobs.push_back(jb);
-          vjob_of.push_back(vjobs.size());
         }
-        cands.push_back({j, 0, t0, jobs.size()});
-        jobs.push_back(jb);
       }
-      uint64_t lo = ch.co + 1, hi = ch.co + ch.len - 2;   // file pairs scanned as i = 1 .. len-2
-      while (pi < pairs.size() && pairs[pi] < lo) pi++;
-      size_t pj = pi;
-      while (pj < pairs.size() && pairs[pj] <= hi) {
-        uint64_t p = pairs[pj];
-        InfJob jb;
-        jb.in_off = p; jb.in_len = ch.co + ch.len - p; jb.out_off = NO_OUT; jb.out_cap = 0;
-        cands.push_back({j, p - ch.co, header_type_host(h[p], h[p + 1]), jobs.size()});
-        jobs.push_back(jb);
-        vjob_of.push_back(0);
-        pj++;
+      const uint64_t lo = ch.co + 1, hi = ch.co + ch.len - 2;   // file pairs scanned as i = 1 .. len-2
+      const uint64_t end = ch.co + ch.len;
+      while (pi < pairs.size() && (pairs[pi] >> 5) < lo) pi++;
+      for (; pi < pairs.size() && (pairs[pi] >> 5) <= hi; pi++) {
+        const uint64_t p = pairs[pi] >> 5;
+        cands.push_back({j, (int32_t)(pairs[pi] & 31), p - ch.co, fjobs.size()});
+        fjobs.push_back({p, end - p, ARENA_OUT, ARENA_SLOT});
       }
     }
   }
   TMARK("scan: candidate jobs");
-  std::vector<InfRes> res;
+  std::vector<InfRes> fr, vr;
+  // a slot (ARENA_SLOT) is claimed at a candidate's first flush (4 KiB of output): room for a slot
+  // per ~64 input bytes, capped -- slots are only written as far as the output goes
+  const uint64_t arena_cap = std::min<uint64_t>(64ull << 30, std::max<uint64_t>(1ull << 30, 16 * F));
   {
-    std::vector<InfJob> fjobs;
-    std::vector<size_t> fidx;
-    for (size_t k = 0; k < jobs.size(); k++)
-      if (!vjob_of[k]) {
-        fjobs.push_back(jobs[k]);
-        fjobs.back().out_off = ARENA_OUT;     // keep the output of candidates that are streams
-        fjobs.back().out_cap = ARENA_SLOT;
-        fidx.push_back(k);
-      }
-    std::vector<InfRes> fr, vr;
-    // a slot (ARENA_SLOT) is claimed at a candidate's first flush (4 KiB of output): room for a slot
-    // per ~64 input bytes, capped -- slots are only written as far as the output goes
-    const uint64_t arena_cap = std::min<uint64_t>(64ull << 30, std::max<uint64_t>(1ull << 30, 16 * F));
     if (int r = run_inflate_jobs(c, d_file, nullptr, fjobs, fr, arena_cap)) return r;
     if (!vjobs.empty()) {
       if (int r = upload(c, c->d_virt, virt.data(), virt.size())) return r;
       if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, vjobs, vr)) return r;
     }
-    res.resize(jobs.size());
-    for (size_t q = 0; q < fidx.size(); q++) res[fidx[q]] = fr[q];
-    for (size_t k = 0; k < jobs.size(); k++) if (vjob_of[k]) res[k] = vr[vjob_of[k] - 1];
   }
-  c->stats.n_candidates = jobs.size();
+  auto result = [&](const Cand& cd) -> const InfRes& { return (cd.job & VJOB) ? vr[cd.job & ~VJOB] : fr[cd.job]; };
+  c->stats.n_candidates = cands.size();
   TMARK("scan: candidate inflate");
   // ---- per-chunk candidate index ranges ----
   std::vector<size_t> cbeg(chunks.size() + 1, cands.size());
@@ -569,7 +564,7 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
     for (size_t k = cbeg[j]; k < cbeg[j + 1]; k++) {
       const Cand& cd = cands[k];
       if (cd.i < i) continue;
-      const InfRes& r = res[cd.job];
+      const InfRes& r = result(cd);
       if (r.consumed <= 16) continue;
       if (r.status == INF_END) {
         if (out) out->push_back({cd.i + ch.co, r.consumed, r.produced, cd.type, 0, r.arena_off});
@@ -606,7 +601,8 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       else add_file(ch.co + cd.i, ch.len - cd.i);
       add_byte(nx.b0);
       add_file(nx.co + 1, nx.len - 1);
-      jb.in_len = out - jb.in_off; jb.out_off = NO_OUT; jb.out_cap = 0;
+      // output into arena slots after the scan's (8 KiB-ring decoder); the bytes are not used
+      jb.in_len = out - jb.in_off; jb.out_off = ARENA_OUT; jb.out_cap = ARENA_SLOT;
       cj.push_back(jb);
       cj_chunk.push_back(j);
       out = (out + 3) & ~3ull;
@@ -623,7 +619,7 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       kend(c);
       KCHECK("k_gather");
       std::vector<InfRes> cr;
-      if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, cj, cr)) return r;
+      if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, cj, cr, arena_cap, false, false)) return r;
       for (size_t q = 0; q < cj.size(); q++) cont0[cj_chunk[q]] = cr[q];
     }
     c->stats.n_continuations = cj.size();
@@ -631,7 +627,16 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
   TMARK("scan: continuations");
   // ---- sequential replay (main.cpp:205-246 over searchInfile's chunk sequence) ----
   bool need_more = false;
-  struct Pend { uint64_t off; int type; int state; std::vector<uint8_t> bytes; uint64_t in, out; long spec_chunk; int refills; } pd{};
+  // pending stream: its bytes are chunk j0 from i0 plus the napp following chunk buffers (size
+  // bytes); they are materialized only for a second refill (rare)
+  struct Pend { uint64_t off; int type; int state; uint32_t j0, napp; uint64_t i0, size; uint64_t in, out; long spec_chunk; int refills; } pd{};
+  auto materialize = [&](const Pend& q, std::vector<uint8_t>& v) {
+    v.clear();
+    const Chunk& c0 = chunks[q.j0];
+    if (q.i0 == 0) chunk_bytes(h, c0, v);
+    else v.assign(h + c0.co + q.i0, h + c0.co + c0.len);
+    for (uint32_t k = 1; k <= q.napp; k++) chunk_bytes(h, chunks[q.j0 + k], v);
+  };
   for (uint32_t j = 0; j < chunks.size(); j++) {
     const Chunk& ch = chunks[j];
     uint64_t i = 0;
@@ -643,14 +648,16 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
         if (pd.refills == 0 && pd.spec_chunk == (long)j - 1) {
           rr = cont0[j - 1];
         } else {
-          std::vector<uint8_t> v = pd.bytes;
+          std::vector<uint8_t> v;
+          materialize(pd, v);
           chunk_bytes(h, ch, v);
           if (int r = inflate_bytes(c, v, rr)) return r;
         }
-        chunk_bytes(h, ch, pd.bytes);
+        pd.napp++;
+        pd.size += ch.len;
         pd.refills++;
         pd.state = (int)rr.status; pd.in = rr.consumed; pd.out = rr.produced;
-        avail = pd.bytes.size() - rr.consumed;
+        avail = pd.size - rr.consumed;
         st = (int)rr.status;
       } else if (pd.state == INF_END) {  // inflate() in DONE mode returns Z_STREAM_END again
         avail = ch.len; st = INF_END;
@@ -668,11 +675,10 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       if (k >= 0) {
         const Cand& cd = cands[k];
         need_more = true;
-        pd.off = cd.i + ch.co; pd.type = cd.type; pd.state = (int)res[cd.job].status;
-        pd.in = res[cd.job].consumed; pd.out = res[cd.job].produced;
-        pd.bytes.clear();
-        if (cd.i == 0) chunk_bytes(h, ch, pd.bytes);
-        else pd.bytes.assign(h + ch.co + cd.i, h + ch.co + ch.len);
+        pd.off = cd.i + ch.co; pd.type = cd.type; pd.state = (int)result(cd).status;
+        pd.in = result(cd).consumed; pd.out = result(cd).produced;
+        pd.j0 = j; pd.i0 = cd.i; pd.napp = 0;
+        pd.size = cd.i == 0 ? ch.len : ch.len - cd.i;
         pd.spec_chunk = (i == 0 && pend0[j] == k) ? (long)j : -2;
         pd.refills = 0;
       }
@@ -1603,10 +1609,12 @@ int atz_inflate_batch(atz_ctx_t* c, const uint8_t* buf, uint64_t len, const uint
   std::vector<InfJob> jobs(n);
   for (uint64_t k = 0; k < n; k++) {
     if (offs[k] + lens[k] > len) return ATZ_E_ARG;
-    jobs[k].in_off = offs[k]; jobs[k].in_len = lens[k]; jobs[k].out_off = NO_OUT; jobs[k].out_cap = 0;
+    // the scan's configuration: output into arena slots (8 KiB-ring decoder, 32 KiB-ring reruns)
+    jobs[k].in_off = offs[k]; jobs[k].in_len = lens[k]; jobs[k].out_off = ARENA_OUT; jobs[k].out_cap = ARENA_SLOT;
   }
   std::vector<InfRes> res;
-  if (int r = run_inflate_jobs(c, c->d_tmp.as<uint8_t>(), nullptr, jobs, res)) return r;
+  const uint64_t arena_cap = std::min<uint64_t>(64ull << 30, std::max<uint64_t>(256ull << 20, n * ARENA_SLOT));
+  if (int r = run_inflate_jobs(c, c->d_tmp.as<uint8_t>(), nullptr, jobs, res, arena_cap)) return r;
   for (uint64_t k = 0; k < n; k++) { status[k] = res[k].status; consumed[k] = res[k].consumed; produced[k] = res[k].produced; }
   return ATZ_OK;
 }

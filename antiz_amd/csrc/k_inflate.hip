@@ -96,6 +96,64 @@ __global__ __launch_bounds__(256) void k_find_headers(const uint8_t* __restrict_
   }
 }
 
+// Ordered variant: block b owns the contiguous segment [b*seg, (b+1)*seg) (seg a multiple of 4 KiB)
+// and walks it 4 KiB at a time, lane l testing the 16 pairs starting at l*16.  count mode writes the
+// block's total to cnt[b]; write mode writes (position << 5 | header type) in file order from base[b]
+// on (block-wide exclusive prefix per step), so the list needs no sort.
+__global__ __launch_bounds__(256) void k_headers_ordered(const uint8_t* __restrict__ f, uint64_t n, uint64_t seg,
+                                                         uint32_t* __restrict__ cnt, const uint64_t* __restrict__ base,
+                                                         uint64_t* __restrict__ out, int write) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint64_t s0 = (uint64_t)blockIdx.x * seg;
+  const uint64_t s1 = s0 + seg < n ? s0 + seg : n;
+  uint64_t o = write ? base[blockIdx.x] : 0;
+  uint32_t total = 0;
+  for (uint64_t sb = s0; sb < s1; sb += 4096) {
+    const uint64_t p = sb + (uint64_t)t * 16;
+    uint32_t hits = 0;
+    if (p < s1) {
+      uint8_t b[17];
+      if (p + 17 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(f + p);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t x = k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+          b[4 * k] = x & 0xff; b[4 * k + 1] = (x >> 8) & 0xff; b[4 * k + 2] = (x >> 16) & 0xff; b[4 * k + 3] = x >> 24;
+        }
+        b[16] = f[p + 16];
+      } else {
+        for (int k = 0; k < 17; k++) b[k] = p + k < n ? f[p + k] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (p + k < s1 && p + k + 1 < n && header_type(b[k], b[k + 1]) >= 0) hits |= 1u << k;
+    }
+    const uint32_t c = __popc(hits);
+    uint32_t incl = c;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d, 64);
+      if ((int)lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t before = 0, step = 0;
+    for (uint32_t k = 0; k < 4; k++) { const uint32_t v = wsum[k]; if (k < w) before += v; step += v; }
+    __syncthreads();
+    if (write) {
+      uint64_t q = o + before + incl - c;
+      while (hits) {
+        const int k = __ffs(hits) - 1;
+        hits &= hits - 1;
+        out[q++] = ((p + k) << 5) | (uint64_t)header_type(f[p + k], f[p + k + 1]);   // position << 5 | type
+      }
+    }
+    o += step;
+    total += step;
+  }
+  if (!write && t == 0) cnt[blockIdx.x] = total;
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_inflate: one wavefront per job, everything inlined into the kernel so the decoder state stays
 // in (wave-uniform) SGPRs -- a by-reference state struct crossing a call would live in scratch.
