@@ -246,6 +246,7 @@ struct Pipe {
       d_diffjobs, d_diffpos, d_diffval, d_diffcnt;
   uint64_t chain_used = 0, chain_cap = 0;
   std::vector<uint32_t> streams;   // the streams whose chain tables this pipe owns
+  int id = 0;
   // diagnostics (ATZ_TIMING): host phase times, per trial kind x level counters
   double t_list = 0, t_chains = 0, t_trials = 0, t_apply = 0;
   uint64_t kind[3][10][14] = {};
@@ -343,11 +344,12 @@ struct Chunk {
 
 static constexpr uint64_t ARENA_SLOT = 65536;   // arena slot per scan candidate (longer outputs are re-inflated)
 
-static bool timing_on() {
+static int timing_level() {   // ATZ_TIMING=1: phase timings, 2: + per-round sweep timeline
   static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_TIMING"); v = e && *e == '1'; }
-  return v == 1;
+  if (v < 0) { const char* e = std::getenv("ATZ_TIMING"); v = e ? std::atoi(e) : 0; }
+  return v;
 }
+static bool timing_on() { return timing_level() >= 1; }
 
 static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, const std::vector<InfJob>& jobs,
                             std::vector<InfRes>& res, uint64_t arena_cap = 0, bool full_ring = false,
@@ -866,14 +868,44 @@ static uint64_t match_prefix(uint64_t n, int memlevel) {
   return std::min(n, x);
 }
 
-static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj) {
-  if (mj.empty()) return 0;
+// Jobs whose walks touch at most 32 KiB of their stream run on k_match_lds (stream bytes staged in
+// LDS), one launch per staged-size class so the dynamic LDS -- and with it the blocks per CU --
+// fits the class; longer ones walk the stream in HBM (k_match).
+static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
+  if (mj0.empty()) return 0;
+  static const uint64_t cls[] = {4096, 8192, 12288, 16384, 24576, 32768};
+  constexpr int NC = 6;
+  auto class_of = [&](const MatchJob& m) -> int {
+    const uint64_t b = std::min<uint64_t>(m.p1 + 258 + 24, m.n);
+    for (int k = 0; k < NC; k++) if (b <= cls[k]) return k;
+    return NC;
+  };
+  std::vector<MatchJob> mj;
+  mj.reserve(mj0.size());
+  size_t cnt[NC + 1] = {};
+  for (const MatchJob& m : mj0) cnt[class_of(m)]++;
+  size_t beg[NC + 2] = {};
+  for (int k = 0; k <= NC; k++) beg[k + 1] = beg[k] + cnt[k];
+  mj.resize(mj0.size());
+  {
+    size_t at[NC + 1];
+    for (int k = 0; k <= NC; k++) at[k] = beg[k];
+    for (const MatchJob& m : mj0) mj[at[class_of(m)]++] = m;
+  }
   if (int r = upload(c, c->d_mjobs, mj.data(), mj.size() * sizeof(MatchJob))) return r;
-  kbeg(c, 4);
-  hipLaunchKernelGGL(k_match, dim3((uint32_t)mj.size()), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
-                     c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(), c->d_mjobs.as<MatchJob>());
-  kend(c);
-  KCHECK("k_match");
+  for (int k = 0; k <= NC; k++) {
+    if (!cnt[k]) continue;
+    kbeg(c, 4);
+    if (k < NC)
+      hipLaunchKernelGGL(k_match_lds, dim3((uint32_t)cnt[k]), dim3(256), (uint32_t)(cls[k] + 64), c->st,
+                         x->d_infl.as<uint8_t>(), c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(),
+                         c->d_mjobs.as<MatchJob>() + beg[k]);
+    else
+      hipLaunchKernelGGL(k_match, dim3((uint32_t)cnt[k]), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
+                         c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(), c->d_mjobs.as<MatchJob>() + beg[k]);
+    kend(c);
+    KCHECK("k_match");
+  }
   for (const MatchJob& m : mj) c->stats.k_match_positions += m.p1 - m.p0;
   return 0;
 }
@@ -881,8 +913,14 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj) {
 // Runs the trials tr[k] (k = 0 stored, 1 fast, 2 slow levels); res[k] receives their results.
 // Chain tables must exist.  Match tables are built for a prefix of each trial's positions; a
 // trial that parses past it (TR_NEED_R) gets the rest of its table and is run again.
+static uint64_t full_tables_below() {   // ATZ_FULL_BELOW=n: rounds of <= n trials build whole match tables
+  static int64_t v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_FULL_BELOW"); v = e ? std::atoll(e) : 0; }
+  return (uint64_t)v;
+}
 static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
                       std::vector<TrialRes>* res) {
+  const bool full = tr[0].size() + tr[1].size() + tr[2].size() <= full_tables_below();
   uint64_t r_tot = 0;
   std::vector<MatchJob> mj;
   for (int k = 0; k < 3; k++)
@@ -897,7 +935,7 @@ static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Tri
       const uint64_t n = x->recs[t.stream].infl_len;
       t.r_off = r_tot;
       r_tot += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
-      t.x_lim = (t.mode & 1) ? n : match_prefix(n, t.memlevel);
+      t.x_lim = ((t.mode & 1) || full) ? n : match_prefix(n, t.memlevel);
       MatchJob m{};
       m.infl_off = x->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
       m.p0 = 0; m.p1 = t.x_lim; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
@@ -994,6 +1032,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
   // reference's sequential one; the speculation only changes how much work runs per launch.
   while (!active.empty()) {
     rounds++;
+    const auto tl0 = std::chrono::steady_clock::now();
     const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, target / active.size()));
     std::vector<std::pair<uint32_t, int>> need;
     for (int k = 0; k < 3; k++) tr[k].clear();
@@ -1019,6 +1058,8 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       }
     }
     auto ta = std::chrono::steady_clock::now();
+    size_t nbuild = 0;
+    for (auto& q : need) nbuild += x->chain_off[q.first][q.second] == ~0ull;
     if (int r = ensure_chains(x, c, need)) return r;
     HIPCHK(hipStreamSynchronize(c->st));
     auto tb = std::chrono::steady_clock::now();
@@ -1030,6 +1071,12 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     auto tc = std::chrono::steady_clock::now();
     c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
     c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
+    if (timing_level() >= 2)
+      std::fprintf(stderr, "atz: pipe %d round %llu at %.1f ms: active %zu K %u trials %zu/%zu/%zu list %.1f chains %.1f (%zu builds) trials %.1f ms\n",
+                   c->id, (unsigned long long)rounds, std::chrono::duration<double, std::milli>(ta - t0).count(), active.size(), K,
+                   tr[0].size(), tr[1].size(), tr[2].size(), std::chrono::duration<double, std::milli>(ta - tl0).count(),
+                   std::chrono::duration<double, std::milli>(tb - ta).count(), nbuild,
+                   std::chrono::duration<double, std::milli>(tc - tb).count());
     for (int k = 0; k < 3; k++)
       for (size_t q = 0; q < tr[k].size(); q++) {
         const TrialRes& r = trres[k][q];
@@ -1160,6 +1207,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
 static int ensure_pipes(atz_ctx* c, size_t np) {
   while (c->pipes.size() < np) {
     std::unique_ptr<Pipe> p(new Pipe());
+    p->id = (int)c->pipes.size();
     if (hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
     c->pipes.push_back(std::move(p));
   }

@@ -375,7 +375,8 @@ static constexpr uint32_t HOLE_SLOTS_M = 1024;   // == HOLE_SLOTS (fast-level ha
 
 // 16 bytes at byte offset x of a 4-byte aligned buffer: 5 aligned dword loads (independent, one
 // round trip) joined with v_alignbyte.  Reads up to 4 bytes past x + 16 (buffers carry slack).
-__device__ __forceinline__ void load16(const uint32_t* in32, uint32_t x, uint32_t v[4]) {
+template <typename P>
+__device__ __forceinline__ void load16(P in32, uint32_t x, uint32_t v[4]) {
   const uint32_t w = x >> 2, sh = x & 3;
   const uint32_t a0 = in32[w], a1 = in32[w + 1], a2 = in32[w + 2], a3 = in32[w + 3], a4 = in32[w + 4];
   v[0] = __builtin_amdgcn_alignbyte(a1, a0, sh);
@@ -384,8 +385,8 @@ __device__ __forceinline__ void load16(const uint32_t* in32, uint32_t x, uint32_
   v[3] = __builtin_amdgcn_alignbyte(a4, a3, sh);
 }
 // number of equal leading bytes (0..16) of the 16 bytes at a and at b (pb: b's bytes if preloaded)
-__device__ __forceinline__ uint32_t match16(const uint32_t* in32, uint32_t a, uint32_t b, const uint32_t* pb,
-                                            int) {
+template <typename P>
+__device__ __forceinline__ uint32_t match16(P in32, uint32_t a, uint32_t b, const uint32_t* pb, int) {
   uint32_t va[4], vb[4];
   load16(in32, a, va);
   if (pb) { vb[0] = pb[0]; vb[1] = pb[1]; vb[2] = pb[2]; vb[3] = pb[3]; }
@@ -398,11 +399,11 @@ __device__ __forceinline__ uint32_t match16(const uint32_t* in32, uint32_t a, ui
   return 16;
 }
 
-__global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl, const uint32_t* __restrict__ chains,
-                                              uint2* __restrict__ R, const MatchJob* __restrict__ jobs) {
-  const MatchJob jb = jobs[blockIdx.x];
-  const uint8_t* in = infl + jb.infl_off;
-  const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);   // stream bases are 256-byte aligned
+// One trial's positions [p0, p1) on 256 lanes.  Candidate bytes are read through in32: the stream in
+// HBM, or its first bytes staged in LDS (k_match_lds).
+template <typename P>
+__device__ __forceinline__ void match_positions(const MatchJob& jb, const uint8_t* __restrict__ in, P in32,
+                                                const uint32_t* __restrict__ chains, uint2* __restrict__ R) {
   const uint32_t n = (uint32_t)jb.n, npad = (n + 63) & ~63u;
   const uint32_t* sidx = chains + jb.chain_off;
   const uint32_t* bpos = sidx + npad;
@@ -471,6 +472,30 @@ __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl,
     else o.y = (bq > 2 ? (bq << 23) | (dq << 8) : 0u) | valid;
     r[p] = o;
   }
+}
+
+__global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl, const uint32_t* __restrict__ chains,
+                                              uint2* __restrict__ R, const MatchJob* __restrict__ jobs) {
+  const MatchJob jb = jobs[blockIdx.x];
+  const uint8_t* in = infl + jb.infl_off;
+  match_positions(jb, in, reinterpret_cast<const uint32_t*>(in), chains, R);   // stream bases are 256-byte aligned
+}
+
+// Same, with the stream bytes the walks can touch ([0, p1 + 258 + 20), rounded to dwords) staged in
+// LDS first (dynamic LDS, sized per launch by the host for the longest staged range): every candidate
+// compare is then 5 ds_read_b32 instead of 5 L2/HBM loads.
+__global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ infl, const uint32_t* __restrict__ chains,
+                                                  uint2* __restrict__ R, const MatchJob* __restrict__ jobs) {
+  extern __shared__ uint32_t dyn_lds[];
+  const MatchJob jb = jobs[blockIdx.x];
+  const uint8_t* in = infl + jb.infl_off;
+  const uint32_t* g32 = reinterpret_cast<const uint32_t*>(in);
+  LDS uint32_t* l32 = (LDS uint32_t*)dyn_lds;
+  const uint64_t want = jb.p1 + 258 + 24;
+  const uint32_t nw = (uint32_t)(((want < jb.n ? want : jb.n) + 3) >> 2);
+  for (uint32_t w = threadIdx.x; w < nw + 8; w += 256) l32[w] = w < nw ? g32[w] : 0u;
+  __syncthreads();
+  match_positions(jb, in, (const LDS uint32_t*)l32, chains, R);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -822,53 +847,6 @@ __device__ __noinline__ void gen_codes(const LDS TreeWork& w, int max_code, LDS 
   }
 }
 
-__device__ inline int tl(const LDS uint8_t* ln, int n, int guard) { return n == guard ? 0xffff : ln[n]; }
-
-__device__ void scan_tree(LDS uint32_t* bfreq, const LDS uint8_t* ln, int max_code) {  // Z/trees.c:705-748
-  int prevlen = -1, curlen, nextlen = ln[0], count = 0, max_count = 7, min_count = 4;
-  int guard = max_code + 1;
-  if (nextlen == 0) { max_count = 138; min_count = 3; }
-  for (int n = 0; n <= max_code; n++) {
-    curlen = nextlen; nextlen = tl(ln, n + 1, guard);
-    if (++count < max_count && curlen == nextlen) continue;
-    else if (count < min_count) bfreq[curlen] += (uint32_t)count;
-    else if (curlen != 0) { if (curlen != prevlen) bfreq[curlen]++; bfreq[16]++; }
-    else if (count <= 10) bfreq[17]++;
-    else bfreq[18]++;
-    count = 0; prevlen = curlen;
-    if (nextlen == 0) { max_count = 138; min_count = 3; }
-    else if (curlen == nextlen) { max_count = 6; min_count = 3; }
-    else { max_count = 7; min_count = 4; }
-  }
-}
-
-__device__ void send_tree(LDS BitOut& b, LDS TrialShared& s, const LDS uint8_t* ln, int max_code, int lane) {
-  int prevlen = -1, curlen, nextlen = ln[0], count = 0, max_count = 7, min_count = 4;
-  int guard = max_code + 1;
-  if (nextlen == 0) { max_count = 138; min_count = 3; }
-  for (int n = 0; n <= max_code; n++) {
-    curlen = nextlen; nextlen = tl(ln, n + 1, guard);
-    if (++count < max_count && curlen == nextlen) continue;
-    else if (count < min_count) {
-      do { put_bits(b, s.stage, s.bcode[curlen], s.blen[curlen], lane); } while (--count != 0);
-    } else if (curlen != 0) {
-      if (curlen != prevlen) { put_bits(b, s.stage, s.bcode[curlen], s.blen[curlen], lane); count--; }
-      put_bits(b, s.stage, s.bcode[16], s.blen[16], lane);
-      put_bits(b, s.stage, (uint32_t)(count - 3), 2, lane);
-    } else if (count <= 10) {
-      put_bits(b, s.stage, s.bcode[17], s.blen[17], lane);
-      put_bits(b, s.stage, (uint32_t)(count - 3), 3, lane);
-    } else {
-      put_bits(b, s.stage, s.bcode[18], s.blen[18], lane);
-      put_bits(b, s.stage, (uint32_t)(count - 11), 7, lane);
-    }
-    count = 0; prevlen = curlen;
-    if (nextlen == 0) { max_count = 138; min_count = 3; }
-    else if (curlen == nextlen) { max_count = 6; min_count = 3; }
-    else { max_count = 7; min_count = 4; }
-  }
-}
-
 __device__ __forceinline__ uint32_t len_code(uint32_t len) {   // _length_code[len], len = length - 3
   if (len < 8) return len;
   if (len == 255) return 28;
@@ -941,6 +919,110 @@ __device__ __forceinline__ void stage_or(LDS uint32_t* stage, uint32_t off, uint
   if ((uint32_t)(lo >> 32)) __atomic_fetch_or(&stage[wi + 1], (uint32_t)(lo >> 32), __ATOMIC_RELAXED);
   if (hi) __atomic_fetch_or(&stage[wi + 2], hi, __ATOMIC_RELAXED);
 }
+// Appends one bit string per lane (v, nb bits; lane order) to the output: bit offsets by a wave
+// prefix sum, words assembled in the staging buffer with LDS atomics (as in compress_block).
+__device__ __forceinline__ void emit_lane_bits(LDS BitOut& b, LDS uint32_t* stage, uint64_t v, uint32_t nb, int lane) {
+  uint32_t incl = nb;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += t;
+  }
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  if (total == 0) return;
+  for (int i = lane; i < (int)STAGE_WORDS; i += 64) stage[i] = 0;
+  if (lane == 0) { stage[0] = (uint32_t)b.bb; stage[1] = (uint32_t)(b.bb >> 32); }
+  stage_or(stage, b.bc + incl - nb, v, nb);
+  const uint32_t all = b.bc + total;
+  const uint32_t full = all >> 3;
+  emit_bytes_from_stage(b, stage, full, lane);
+  const uint32_t rem = all & 7;
+  const uint32_t lastw = stage[full >> 2];
+  b.bb = rem ? ((lastw >> (8 * (full & 3))) & 0xff) & ((1u << rem) - 1) : 0;
+  b.bc = rem;
+}
+
+// scan_tree / send_tree (Z/trees.c:705-799), lane-parallel.  zlib walks the code lengths
+// ln[0..max_code] once, cutting each run of equal lengths into chunks; the cut points depend only
+// on the run: a run of v != 0 is cut after 7, then every 6 elements (max_count 7, then 6 while the
+// run goes on); a run of zeros every 138.  A chunk of `cnt` elements is coded as cnt literal v codes
+// if cnt < min_count (4 for the first chunk of a nonzero run, else 3), else as [v] REP_3_6+2 bits
+// (v only in the run's first chunk, where prevlen != v), REPZ_3_10+3 or REPZ_11_138+7.  So every
+// element finds its run (ballot masks of run starts; max_code + 1 is zlib's guard) and a chunk's
+// first element contributes the chunk: send = its bits in element order, else its bl_tree counts.
+__device__ void rle_tree(LDS BitOut& b, LDS TrialShared& s, const LDS uint8_t* ln, int max_code, bool send, int lane) {
+  const int N = max_code + 1;   // elements; position N acts as a run start (the guard)
+  const int G = N / 64 + 1;     // groups covering 0..N (N <= 286: at most 5)
+  uint64_t M[5];
+#pragma unroll
+  for (int g = 0; g < 5; g++) {
+    M[g] = 0;
+    if (g < G) {
+      const int n = 64 * g + lane;
+      bool st = false;
+      if (n == 0 || n == N) st = true;
+      else if (n < N) st = ln[n] != ln[n - 1];
+      M[g] = __ballot(st);
+    }
+  }
+  for (int g = 0; g < G; g++) {
+    const int n = 64 * g + lane;
+    uint64_t v64 = 0;
+    uint32_t nb = 0;
+    if (n < N) {
+      // run start: highest start <= n; run end: lowest start > n
+      int st = -1, en = -1;
+      const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
+#pragma unroll
+      for (int h = 4; h >= 0; h--)
+        if (st < 0 && h <= g) {
+          const uint64_t m = h == g ? (M[h] & le) : M[h];
+          if (m) st = 64 * h + 63 - __clzll((long long)m);
+        }
+#pragma unroll
+      for (int h = 0; h < 5; h++)
+        if (en < 0 && h >= g) {
+          const uint64_t m = h == g ? (M[h] & ~le) : M[h];
+          if (m) en = 64 * h + __ffsll((unsigned long long)m) - 1;
+        }
+      const uint32_t v = ln[n];
+      const int k = n - st, R = en - st;
+      int cnt = 0, minc = 3;
+      bool first = false;
+      if (v != 0) {
+        if (k == 0) { cnt = R < 7 ? R : 7; minc = 4; first = true; }
+        else if (k >= 7 && (k - 7) % 6 == 0) cnt = R - k < 6 ? R - k : 6;
+      } else if (k % 138 == 0) {
+        cnt = R - k < 138 ? R - k : 138;
+      }
+      if (cnt) {
+        if (!send) {
+          if (cnt < minc) __atomic_fetch_add(&s.bfreq[v], (uint32_t)cnt, __ATOMIC_RELAXED);
+          else if (v != 0) {
+            if (first) __atomic_fetch_add(&s.bfreq[v], 1u, __ATOMIC_RELAXED);
+            __atomic_fetch_add(&s.bfreq[16], 1u, __ATOMIC_RELAXED);
+          } else __atomic_fetch_add(&s.bfreq[cnt <= 10 ? 17 : 18], 1u, __ATOMIC_RELAXED);
+        } else {
+          const uint32_t cv = s.bcode[v], cl = s.blen[v];
+          if (cnt < minc) {
+            for (int q = 0; q < cnt; q++) { v64 |= (uint64_t)cv << nb; nb += cl; }
+          } else if (v != 0) {
+            if (first) { v64 = cv; nb = cl; }
+            v64 |= (uint64_t)s.bcode[16] << nb; nb += s.blen[16];
+            v64 |= (uint64_t)(cnt - (first ? 1 : 0) - 3) << nb; nb += 2;
+          } else if (cnt <= 10) {
+            v64 = s.bcode[17]; nb = s.blen[17];
+            v64 |= (uint64_t)(cnt - 3) << nb; nb += 3;
+          } else {
+            v64 = s.bcode[18]; nb = s.blen[18];
+            v64 |= (uint64_t)(cnt - 11) << nb; nb += 7;
+          }
+        }
+      }
+    }
+    if (send) emit_lane_bits(b, s.stage, v64, nb, lane);
+  }
+}
+
 // The trial's outcome gates (early_exit) are monotone in the output emitted so far, so they are
 // tested after every step: a bailed trial stops inside its first block instead of emitting all of
 // it.  Returns true when the trial is decided (the caller re-evaluates early_exit).
@@ -1067,7 +1149,8 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
     // bit length tree
     for (int i = lane; i < NBLC; i += 64) s.bfreq[i] = 0;
     const uint64_t cs0 = STEP_CLOCK();
-    if (lane == 0) { scan_tree(s.bfreq, s.llen, lmax); scan_tree(s.bfreq, s.dlen, dmax); }
+    rle_tree(b, s, s.llen, lmax, false, lane);
+    rle_tree(b, s, s.dlen, dmax, false, lane);
     b.cyc_scan += STEP_CLOCK() - cs0;
     for (int i = lane; i < NBLC; i += 64) s.w.freq[i] = (uint16_t)s.bfreq[i];
     int bmax = build_tree(s.w, sc, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, opt_len, static_len, b.cyc_heap, lane);
@@ -1119,8 +1202,8 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
     put_bits(b, s.stage, (uint32_t)(blcodes - 4), 4, lane);
     for (int r = 0; r < blcodes; r++) put_bits(b, s.stage, s.blen[bl_order((uint32_t)r)], 3, lane);
     const uint64_t cs0 = STEP_CLOCK();
-    send_tree(b, s, s.llen, lcodes - 1, lane);
-    send_tree(b, s, s.dlen, dcodes - 1, lane);
+    rle_tree(b, s, s.llen, lcodes - 1, true, lane);
+    rle_tree(b, s, s.dlen, dcodes - 1, true, lane);
     b.cyc_send += STEP_CLOCK() - cs0;
     flush_bits_bytes(b, s.stage, lane);
     compress_block(b, s, syms, last_lit, (const LDS uint16_t*)s.lcode, (const LDS uint8_t*)s.llen,
