@@ -27,6 +27,7 @@
 #include <string>
 #include <memory>
 #include <thread>
+#include <functional>
 #include <vector>
 
 #include "../../include/atz_accel.h"
@@ -238,12 +239,20 @@ struct KTimer {   // HIP events bracketing kernel launches on the library stream
 // One HIP stream of sweep work with its own buffers, kernel timers and counters.  The sweep runs
 // several pipes at once (streams partitioned among them, one host thread each), so one pipe's
 // launch tails, host gaps and small launches overlap another's work.
+struct ChainBufs {   // bucket-build job lists and scratch (one set per HIP stream that builds)
+  DBuf d_cjobs, d_cjobs2, d_cjobs3, d_heads, d_heads2;
+};
 struct Pipe {
   hipStream_t st = nullptr;
   KTimer kt;
   atz_stats_t stats{};
-  DBuf d_trials, d_tres, d_out, d_syms, d_R, d_mjobs, d_cjobs, d_cjobs2, d_cjobs3, d_heads, d_heads2, d_chains,
-      d_diffjobs, d_diffpos, d_diffval, d_diffcnt;
+  DBuf d_trials, d_tres, d_out, d_syms, d_R, d_mjobs, d_chains, d_diffjobs, d_diffpos, d_diffval, d_diffcnt;
+  ChainBufs cb[2];   // [0] builds on st, [1] prefetch builds on pst
+  // next-round bucket builds run ahead on their own stream while this round's trials run
+  hipStream_t pst = nullptr;
+  hipEvent_t pev = nullptr;
+  bool pev_pending = false;
+  KTimer pkt;
   uint64_t chain_used = 0, chain_cap = 0;
   std::vector<uint32_t> streams;   // the streams whose chain tables this pipe owns
   int id = 0;
@@ -251,8 +260,11 @@ struct Pipe {
   double t_list = 0, t_chains = 0, t_trials = 0, t_apply = 0;
   uint64_t kind[3][10][14] = {};
   ~Pipe() {
+    if (pst) { hipStreamSynchronize(pst); hipStreamDestroy(pst); }
     if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
+    if (pev) hipEventDestroy(pev);
     for (hipEvent_t e : kt.pool) hipEventDestroy(e);
+    for (hipEvent_t e : pkt.pool) hipEventDestroy(e);
   }
 };
 
@@ -753,15 +765,49 @@ static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F) {
 // sweep (8 bytes per position).  When a round would push the cache past its cap the cache is
 // dropped and the round's tables are rebuilt.
 static constexpr uint64_t CHAIN_CACHE_CAP = 48ull << 30;
+// prefetch builds finished: fold their kernel times into the pipe's counters
+static int chains_prefetch_collect(Pipe* c) {
+  if (!c->pev_pending) return 0;
+  HIPCHK(hipEventSynchronize(c->pev));
+  c->pev_pending = false;
+  std::swap(c->kt, c->pkt);
+  kcollect(c);
+  std::swap(c->kt, c->pkt);
+  return 0;
+}
+static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need, ChainBufs& B,
+                            bool prefetch);
+// Builds the missing tables of `need` on the pipe's stream (after any prefetch builds in flight).
 static int ensure_chains(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need) {
+  if (c->pev_pending) HIPCHK(hipStreamWaitEvent(c->st, c->pev, 0));
+  return ensure_chains_on(x, c, need, c->cb[0], false);
+}
+// Speculative builds for the next round on the prefetch stream; skipped when they would need the
+// cache dropped or grown (both are only done between rounds, on the pipe's stream).
+static int chains_prefetch(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need) {
+  if (int r = chains_prefetch_collect(c)) return r;
+  std::swap(c->st, c->pst);
+  std::swap(c->kt, c->pkt);
+  int r = ensure_chains_on(x, c, need, c->cb[1], true);
+  std::swap(c->st, c->pst);
+  std::swap(c->kt, c->pkt);
+  if (r) return r;
+  HIPCHK(hipEventRecord(c->pev, c->pst));
+  c->pev_pending = true;
+  return 0;
+}
+static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need, ChainBufs& B,
+                            bool prefetch) {
   auto words = [&](uint32_t s) { return 2 * ((x->recs[s].infl_len + 63) & ~63ull); };
   uint64_t add = 0;
   for (auto& q : need)
     if (x->chain_off[q.first][q.second] == ~0ull) add += words(q.first);
   if ((c->chain_used + add) * 4 > c->chain_cap) {   // drop this pipe's cache
+    if (prefetch) return 0;
     for (uint32_t s : c->streams) x->chain_off[s].fill(~0ull);
     c->chain_used = 0;
   }
+  if (prefetch && (c->chain_used + add) * 4 + 4096 > c->d_chains.n) return 0;
   std::vector<ChainJob> jobs;
   for (auto& q : need) {
     uint32_t s = q.first;
@@ -786,6 +832,7 @@ static int ensure_chains(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32
     if (cap < need_bytes) cap = need_bytes;
     if (hipMalloc(&np, cap) != hipSuccess) return ATZ_E_NOMEM;
     if (c->d_chains.p) {
+      if (int r = chains_prefetch_collect(c)) return r;
       HIPCHK(hipMemcpyAsync(np, c->d_chains.p, c->d_chains.n, hipMemcpyDeviceToDevice, c->st));
       HIPCHK(hipStreamSynchronize(c->st));
       (void)hipFree(c->d_chains.p);
@@ -804,8 +851,8 @@ static int ensure_chains(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32
     all.insert(all.end(), small.begin(), small.end());
     all.insert(all.end(), mid.begin(), mid.end());
     if (!all.empty()) {
-      if (int r = upload(c, c->d_cjobs2, all.data(), all.size() * sizeof(ChainJob))) return r;
-      const ChainJob* dj = c->d_cjobs2.as<ChainJob>();
+      if (int r = upload(c, B.d_cjobs2, all.data(), all.size() * sizeof(ChainJob))) return r;
+      const ChainJob* dj = B.d_cjobs2.as<ChainJob>();
       auto launch = [&](auto kern, size_t off, size_t cnt, const char* nm) -> int {
         if (!cnt) return 0;
         kbeg(c, 2);
@@ -825,28 +872,28 @@ static int ensure_chains(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32
   big.swap(rest);
   if (!nine.empty()) {
     const size_t nb9 = 4096;
-    if (int r = c->d_heads2.reserve(nb9 * 65536 * 4)) return r;
+    if (int r = B.d_heads2.reserve(nb9 * 65536 * 4)) return r;
     for (size_t k = 0; k < nine.size(); k++) nine[k].slot = (uint32_t)(k % nb9);
-    if (int r = upload(c, c->d_cjobs3, nine.data(), nine.size() * sizeof(ChainJob))) return r;
+    if (int r = upload(c, B.d_cjobs3, nine.data(), nine.size() * sizeof(ChainJob))) return r;
     for (size_t b0 = 0; b0 < nine.size(); b0 += nb9) {
       const size_t nb = std::min(nb9, nine.size() - b0);
       kbeg(c, 2);
       hipLaunchKernelGGL(k_buckets_lds9, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
-                         c->d_cjobs3.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), c->d_heads2.as<uint32_t>(),
+                         B.d_cjobs3.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), B.d_heads2.as<uint32_t>(),
                          (uint32_t)nb);
       kend(c);
       KCHECK("k_buckets_lds9");
     }
   }
   const size_t batch = 4096;   // scratch: 65536 x 8-byte words per job slot
-  if (!big.empty() && (int)c->d_heads.reserve(batch * 65536 * 8)) return ATZ_E_NOMEM;
+  if (!big.empty() && (int)B.d_heads.reserve(batch * 65536 * 8)) return ATZ_E_NOMEM;
   for (size_t k = 0; k < big.size(); k++) big[k].slot = (uint32_t)(k % batch);
-  if (int r = upload(c, c->d_cjobs, big.data(), big.size() * sizeof(ChainJob))) return r;
+  if (int r = upload(c, B.d_cjobs, big.data(), big.size() * sizeof(ChainJob))) return r;
   for (size_t b0 = 0; b0 < big.size(); b0 += batch) {   // launches on one stream reuse the slots in order
     size_t nb = std::min(batch, big.size() - b0);
     kbeg(c, 2);
     hipLaunchKernelGGL(k_buckets, dim3((uint32_t)nb), dim3(64), 0, c->st, x->d_infl.as<uint8_t>(),
-                       c->d_cjobs.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), c->d_heads.as<uint64_t>(),
+                       B.d_cjobs.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), B.d_heads.as<uint64_t>(),
                        (uint32_t)nb);
     kend(c);
     KCHECK("k_buckets");
@@ -868,9 +915,9 @@ static uint64_t match_prefix(uint64_t n, int memlevel) {
   return std::min(n, x);
 }
 
-// Jobs whose walks touch at most 32 KiB of their stream run on k_match_lds (stream bytes staged in
-// LDS), one launch per staged-size class so the dynamic LDS -- and with it the blocks per CU --
-// fits the class; longer ones walk the stream in HBM (k_match).
+// Jobs whose walks touch at most 32 KiB of their stream run on k_match_lds (stream bytes and the
+// 16-bit prev[] chain staged in LDS: 3 bytes per staged position), one launch per size class so the
+// dynamic LDS -- and with it the blocks per CU -- fits the class; longer ones walk in HBM (k_match).
 static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
   if (mj0.empty()) return 0;
   static const uint64_t cls[] = {4096, 8192, 12288, 16384, 24576, 32768};
@@ -897,7 +944,7 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
     if (!cnt[k]) continue;
     kbeg(c, 4);
     if (k < NC)
-      hipLaunchKernelGGL(k_match_lds, dim3((uint32_t)cnt[k]), dim3(256), (uint32_t)(cls[k] + 64), c->st,
+      hipLaunchKernelGGL(k_match_lds, dim3((uint32_t)cnt[k]), dim3(256), (uint32_t)(3 * cls[k] + 64), c->st,
                          x->d_infl.as<uint8_t>(), c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(),
                          c->d_mjobs.as<MatchJob>() + beg[k]);
     else
@@ -913,13 +960,18 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
 // Runs the trials tr[k] (k = 0 stored, 1 fast, 2 slow levels); res[k] receives their results.
 // Chain tables must exist.  Match tables are built for a prefix of each trial's positions; a
 // trial that parses past it (TR_NEED_R) gets the rest of its table and is run again.
+static bool chain_prefetch_on() {   // ATZ_CHAIN_PREFETCH=0 disables the next-round bucket builds
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_CHAIN_PREFETCH"); v = e ? std::atoi(e) : 0; }   // off: measured 739 -> 708 MB/s on C4 (bucket builds compete with the trials)
+  return v != 0;
+}
 static uint64_t full_tables_below() {   // ATZ_FULL_BELOW=n: rounds of <= n trials build whole match tables
   static int64_t v = -1;
   if (v < 0) { const char* e = std::getenv("ATZ_FULL_BELOW"); v = e ? std::atoll(e) : 0; }
   return (uint64_t)v;
 }
 static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
-                      std::vector<TrialRes>* res) {
+                      std::vector<TrialRes>* res, const std::function<int()>& while_running = nullptr) {
   const bool full = tr[0].size() + tr[1].size() + tr[2].size() <= full_tables_below();
   uint64_t r_tot = 0;
   std::vector<MatchJob> mj;
@@ -976,6 +1028,8 @@ static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Tri
     if (!tr[k].empty())
       HIPCHK(hipMemcpyAsync(res[k].data(), c->d_tres.as<TrialRes>() + bases[k], tr[k].size() * sizeof(TrialRes),
                             hipMemcpyDeviceToHost, c->st));
+  if (while_running)
+    if (int r = while_running()) return r;
   HIPCHK(hipStreamSynchronize(c->st));
   kcollect(c);
   // second pass: complete the match tables of the trials that need them and run those again
@@ -1067,7 +1121,21 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       for (Trial& t : tr[k]) t.chain_off = x->chain_off[t.stream][t.memlevel];
     if (int r = c->d_out.reserve(out_tot + 4096)) return r;
     if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
-    if (int r = run_trials(x, c, d_file, tr, so, trres)) return r;
+    // while the trials run: the bucket tables the next round will likely need (each stream's next
+    // K list entries, as if it goes on) are built on the prefetch stream
+    auto prefetch = [&]() -> int {
+      if (!chain_prefetch_on()) return 0;
+      std::vector<std::pair<uint32_t, int>> nx;
+      for (size_t a = 0; a < active.size(); a++) {
+        const StreamState& st = ss[active[a]];
+        for (uint32_t j = K; j < 2 * K && st.idx + j < st.list.size(); j++) {
+          const uint32_t pp = st.list[st.idx + j];
+          if ((pp >> 16) != 0 && x->chain_off[active[a]][pp & 0xff] == ~0ull) nx.push_back({active[a], (int)(pp & 0xff)});
+        }
+      }
+      return nx.empty() ? 0 : chains_prefetch(x, c, nx);
+    };
+    if (int r = run_trials(x, c, d_file, tr, so, trres, prefetch)) return r;
     auto tc = std::chrono::steady_clock::now();
     c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
     c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
@@ -1196,6 +1264,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     active.swap(next);
     c->t_apply += ms_since(tc);
   }
+  if (int r = chains_prefetch_collect(c)) return r;
   c->stats.n_trials += ntr; c->stats.n_trials_shortcut += nsc; c->stats.n_rounds = rounds; c->stats.n_hazard += nhz;
   c->stats.n_trials_speculative += nspec;
   c->stats.sweep_ms = ms_since(t0);
@@ -1209,6 +1278,8 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
     std::unique_ptr<Pipe> p(new Pipe());
     p->id = (int)c->pipes.size();
     if (hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
+    if (hipStreamCreateWithFlags(&p->pst, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
+    if (hipEventCreateWithFlags(&p->pev, hipEventDisableTiming) != hipSuccess) return ATZ_E_HIP;
     c->pipes.push_back(std::move(p));
   }
   return 0;

@@ -481,21 +481,95 @@ __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl,
   match_positions(jb, in, reinterpret_cast<const uint32_t*>(in), chains, R);   // stream bases are 256-byte aligned
 }
 
-// Same, with the stream bytes the walks can touch ([0, p1 + 258 + 20), rounded to dwords) staged in
-// LDS first (dynamic LDS, sized per launch by the host for the longest staged range): every candidate
-// compare is then 5 ds_read_b32 instead of 5 L2/HBM loads.
+// k_match_lds: the same walks with everything they touch in LDS.  The block stages the stream bytes
+// the walks can read ([0, p1 + 258 + 24)) and, for every position q < p1, its predecessor in its
+// hash bucket (prev[q] = bpos[sidx[q] - 1], NIL if q opens its bucket: zlib's prev[] chain), gathered
+// from the bucket arrays with all loads in flight at once.  A walk is then a chain of LDS reads
+// instead of dependent HBM round trips.  Host-side size classes keep positions < 32 Ki (16-bit).
+static constexpr uint32_t PREV_NIL = 0xffffu;
 __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ infl, const uint32_t* __restrict__ chains,
                                                   uint2* __restrict__ R, const MatchJob* __restrict__ jobs) {
   extern __shared__ uint32_t dyn_lds[];
   const MatchJob jb = jobs[blockIdx.x];
   const uint8_t* in = infl + jb.infl_off;
   const uint32_t* g32 = reinterpret_cast<const uint32_t*>(in);
-  LDS uint32_t* l32 = (LDS uint32_t*)dyn_lds;
+  const uint32_t n = (uint32_t)jb.n, npad = (n + 63) & ~63u;
+  const uint32_t* sidx = chains + jb.chain_off;
+  const uint32_t* bpos = sidx + npad;
   const uint64_t want = jb.p1 + 258 + 24;
-  const uint32_t nw = (uint32_t)(((want < jb.n ? want : jb.n) + 3) >> 2);
+  const uint32_t nw = (uint32_t)(((want < n ? want : n) + 3) >> 2);
+  LDS uint32_t* l32 = (LDS uint32_t*)dyn_lds;
+  LDS uint16_t* prv = (LDS uint16_t*)(l32 + nw + 8);
   for (uint32_t w = threadIdx.x; w < nw + 8; w += 256) l32[w] = w < nw ? g32[w] : 0u;
+  const uint32_t nh = n >= 3 ? n - 2 : 0;
+  const uint32_t P = (uint32_t)jb.p1 < nh ? (uint32_t)jb.p1 : nh;   // candidates and walk starts are < P
+  for (uint32_t q0 = 0; q0 < P; q0 += 1024) {
+    uint32_t ix[4], a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) { const uint32_t q = q0 + 256 * u + threadIdx.x; ix[u] = q < P ? sidx[q] : 1u; }
+#pragma unroll
+    for (int u = 0; u < 4; u++) { a[u] = bpos[ix[u]]; b[u] = ix[u] ? bpos[ix[u] - 1] : 0u; }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t q = q0 + 256 * u + threadIdx.x;
+      if (q < P) prv[q] = (a[u] & BUCKET_FIRST) ? (uint16_t)PREV_NIL : (uint16_t)(b[u] & ~BUCKET_FIRST);
+    }
+  }
   __syncthreads();
-  match_positions(jb, in, (const LDS uint32_t*)l32, chains, R);
+  const LDS uint32_t* in32 = l32;
+  auto byte = [&](uint32_t x) -> uint32_t { return (in32[x >> 2] >> (8 * (x & 3))) & 0xffu; };
+  uint2* r = R + jb.r_off;
+  const uint32_t B = c_cfg[jb.level][3], nice = c_cfg[jb.level][2], Bq = B >> 2;
+  const uint32_t maxdist = (1u << jb.window) - 262;
+  const uint32_t hbits = jb.memlevel + 7u, hmask = (1u << hbits) - 1u, hshift = (hbits + 2u) / 3u;
+  for (uint32_t p = (uint32_t)jb.p0 + threadIdx.x; p < (uint32_t)jb.p1; p += 256) {
+    uint32_t bf = 2, df = 0, bq = 2, dq = 0, valid = 0, slot = 0, budget_out = 0;
+    uint32_t reach = p;
+    const uint32_t s0 = byte(p);
+    if (p + 3 <= n) {
+      slot = (((s0 << (2 * hshift)) ^ (byte(p + 1) << hshift) ^ byte(p + 2)) & hmask) & (HOLE_SLOTS_M - 1);
+      const uint32_t lim = p > maxdist ? p - maxdist : 0u;   // walk continues to q only if q > lim
+      uint32_t cur = prv[p];
+      if (cur != PREV_NIL && cur >= 1 && cur + maxdist >= p) {   // hash_head valid
+        valid = 1;
+        const uint32_t left = n - p;
+        const uint32_t cap = left < 258 ? left : 258u;
+        const uint32_t nn = nice < cap ? nice : cap;
+        uint32_t pv[4];
+        load16(in32, p, pv);
+        for (uint32_t i = 0;;) {
+          reach = cur;
+          const uint32_t nx = prv[cur];                        // next node, read ahead of the compare
+          const bool more = nx != PREV_NIL;
+          uint32_t len = match16(in32, cur, p, pv, 0);
+          if (len == 16)
+            while (len < cap) {
+              const uint32_t l2 = match16(in32, cur + len, p + len, nullptr, 0);
+              len += l2;
+              if (l2 < 16) break;
+            }
+          if (len > cap) len = cap;
+          if (len > bf) {
+            bf = len; df = p - cur;
+            if (i < Bq) { bq = len; dq = df; }
+            if (len >= nn) break;
+          }
+          if (++i == B) {
+            budget_out = (more && nx > lim) ? 1u : 0u;
+            break;
+          }
+          if (!more) break;
+          cur = nx;
+          if (cur <= lim) break;
+        }
+      }
+    }
+    uint2 o;
+    o.x = (bf > 2 ? (bf << 23) | (df << 8) : 0u) | s0;
+    if (jb.fast) o.y = ((p - reach) << 16) | (budget_out << 12) | (slot << 1) | valid;
+    else o.y = (bq > 2 ? (bq << 23) | (dq << 8) : 0u) | valid;
+    r[p] = o;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -714,10 +788,55 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, int
     if (stlen) static_len -= stlen[node];
   }
   const uint64_t ch0 = STEP_CLOCK();
-  for (int n = heap_len / 2; n >= 1; n--) pq_down(heap, heap_len, n, lane);
-  // combine the two least frequent nodes until one is left (Z/trees.c:663-690)
   int heap_max = HEAPN;
   uint32_t node = (uint32_t)elems;
+  uint32_t root;
+  if (heap_len <= 63) {
+    // The whole heap in one VGPR (heap[i] in lane i): every sift level is two v_readlane and a
+    // lane select, no LDS round trip.  Same steps, same tie-breaks as the LDS heap below.
+    uint32_t H = lane <= heap_len ? heap[lane] : 0xffffffffu;
+    auto rd = [&](int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)H, i); };
+    auto wr = [&](int i, uint32_t v) { H = lane == i ? v : H; };
+    auto down = [&](int len, int k) {
+      const uint32_t v = rd(k), vk = v >> 10;
+      for (;;) {
+        int j = k << 1;
+        if (j > len) break;
+        uint32_t hj = rd(j);
+        if (j < len) {
+          const uint32_t hj1 = rd(j + 1);
+          if ((hj1 >> 10) <= (hj >> 10)) { j++; hj = hj1; }
+        }
+        if (vk <= (hj >> 10)) break;
+        wr(k, hj);
+        k = j;
+      }
+      wr(k, v);
+    };
+    for (int n = heap_len / 2; n >= 1; n--) down(heap_len, n);
+    do {
+      const uint32_t kn = rd(1);
+      wr(1, rd(heap_len));
+      heap_len--;
+      down(heap_len, 1);
+      const uint32_t km = rd(1);
+      const uint32_t dn = (kn >> 10) & 31u, dm = (km >> 10) & 31u;
+      if (lane == 0) {
+        heap[--heap_max] = kn & 1023u;
+        heap[--heap_max] = km & 1023u;
+        w.dad[kn & 1023u] = (uint16_t)node;
+        w.dad[km & 1023u] = (uint16_t)node;
+      } else {
+        heap_max -= 2;
+      }
+      wr(1, tkey((kn >> 15) + (km >> 15), (dn >= dm ? dn : dm) + 1u, node));
+      node++;
+      down(heap_len, 1);
+    } while (heap_len >= 2);
+    root = rd(1) & 1023u;
+  } else {
+  for (int n = heap_len / 2; n >= 1; n--) pq_down(heap, heap_len, n, lane);
+  // combine the two least frequent nodes until one is left (Z/trees.c:663-690)
   do {
     const uint32_t kn = uni(heap[1]);
     heap[1] = uni(heap[heap_len]);
@@ -737,7 +856,8 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, int
     node++;
     pq_down(heap, heap_len, 1, lane);
   } while (heap_len >= 2);
-  const uint32_t root = uni(heap[1]) & 1023u;
+  root = uni(heap[1]) & 1023u;
+  }
   if (lane == 0) cyc_heap += STEP_CLOCK() - ch0;
   --heap_max;
   if (lane == 0) heap[heap_max] = root;
