@@ -970,8 +970,38 @@ static uint64_t full_tables_below() {   // ATZ_FULL_BELOW=n: rounds of <= n tria
   if (v < 0) { const char* e = std::getenv("ATZ_FULL_BELOW"); v = e ? std::atoll(e) : 0; }
   return (uint64_t)v;
 }
+static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
+                           std::vector<TrialRes>* res, const std::function<int()>& while_running);
+// A launch lasts as long as its slowest wave, so the trials go in longest-expected-first order
+// (classic LPT): low memLevels mean many blocks (one tree build each), fast levels mean hole
+// fallbacks, and the work grows with the stream.  Results come back in the caller's order.
 static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
                       std::vector<TrialRes>* res, const std::function<int()>& while_running = nullptr) {
+  std::vector<Trial> tp[3];
+  std::vector<uint32_t> perm[3];
+  std::vector<TrialRes> rp[3];
+  for (int k = 0; k < 3; k++) {
+    const size_t n = tr[k].size();
+    perm[k].resize(n);
+    std::vector<uint64_t> key(n);
+    for (size_t q = 0; q < n; q++) {
+      const Trial& t = tr[k][q];
+      key[q] = x->recs[t.stream].infl_len * (uint64_t)(k == 1 ? 3 : 1) * (uint64_t)(10 - t.memlevel);
+      perm[k][q] = (uint32_t)q;
+    }
+    std::stable_sort(perm[k].begin(), perm[k].end(), [&](uint32_t a, uint32_t b) { return key[a] > key[b]; });
+    tp[k].resize(n);
+    for (size_t q = 0; q < n; q++) tp[k][q] = tr[k][perm[k][q]];
+  }
+  if (int r = run_trials_impl(x, c, d_cmp, tp, so, rp, while_running)) return r;
+  for (int k = 0; k < 3; k++) {
+    res[k].resize(tr[k].size());
+    for (size_t q = 0; q < tr[k].size(); q++) res[k][perm[k][q]] = rp[k][q];
+  }
+  return 0;
+}
+static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
+                           std::vector<TrialRes>* res, const std::function<int()>& while_running) {
   const bool full = tr[0].size() + tr[1].size() + tr[2].size() <= full_tables_below();
   uint64_t r_tot = 0;
   std::vector<MatchJob> mj;
