@@ -252,6 +252,7 @@ struct Pipe {
   hipStream_t pst = nullptr;
   hipEvent_t pev = nullptr;
   bool pev_pending = false;
+  hipEvent_t fev0 = nullptr, fev1 = nullptr;   // fast-level trials forked onto pst and joined back
   KTimer pkt;
   uint64_t chain_used = 0, chain_cap = 0;
   std::vector<uint32_t> streams;   // the streams whose chain tables this pipe owns
@@ -263,6 +264,8 @@ struct Pipe {
     if (pst) { hipStreamSynchronize(pst); hipStreamDestroy(pst); }
     if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
     if (pev) hipEventDestroy(pev);
+    if (fev0) hipEventDestroy(fev0);
+    if (fev1) hipEventDestroy(fev1);
     for (hipEvent_t e : kt.pool) hipEventDestroy(e);
     for (hipEvent_t e : pkt.pool) hipEventDestroy(e);
   }
@@ -960,6 +963,11 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
 // Runs the trials tr[k] (k = 0 stored, 1 fast, 2 slow levels); res[k] receives their results.
 // Chain tables must exist.  Match tables are built for a prefix of each trial's positions; a
 // trial that parses past it (TR_NEED_R) gets the rest of its table and is run again.
+static bool split_kinds() {
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_SPLIT_KINDS"); v = e ? std::atoi(e) : 0; }   // off: 772 -> 735 MB/s on C4
+  return v != 0;
+}
 static bool chain_prefetch_on() {   // ATZ_CHAIN_PREFETCH=0 disables the next-round bucket builds
   static int v = -1;
   if (v < 0) { const char* e = std::getenv("ATZ_CHAIN_PREFETCH"); v = e ? std::atoi(e) : 0; }   // off: measured 739 -> 708 MB/s on C4 (bucket builds compete with the trials)
@@ -1045,15 +1053,36 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
     KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
     return 0;
   };
+  // ATZ_SPLIT_KINDS=1: fast-level trials on the pipe's second stream, concurrently with the
+  // slow-level launch (overlapping the two tails; measured slower, so off by default)
+  bool forked = false;
+  auto launch_kind = [&](int k, const Trial* h, size_t cnt, size_t base) -> int {
+    if (k != 1 || !split_kinds()) return launch(k, h, cnt, base);
+    HIPCHK(hipEventRecord(c->fev0, c->st));
+    HIPCHK(hipStreamWaitEvent(c->pst, c->fev0, 0));
+    std::swap(c->st, c->pst);
+    const int r = launch(k, h, cnt, base);
+    std::swap(c->st, c->pst);
+    forked = true;
+    return r;
+  };
+  auto join = [&]() -> int {
+    if (!forked) return 0;
+    HIPCHK(hipEventRecord(c->fev1, c->pst));
+    HIPCHK(hipStreamWaitEvent(c->st, c->fev1, 0));
+    forked = false;
+    return 0;
+  };
   size_t base = 0;
   size_t bases[3];
   for (int k = 0; k < 3; k++) {
     bases[k] = base;
     res[k].resize(tr[k].size());
     if (tr[k].empty()) continue;
-    if (int r = launch(k, tr[k].data(), tr[k].size(), base)) return r;
+    if (int r = launch_kind(k, tr[k].data(), tr[k].size(), base)) return r;
     base += tr[k].size();
   }
+  if (int r = join()) return r;
   for (int k = 0; k < 3; k++)
     if (!tr[k].empty())
       HIPCHK(hipMemcpyAsync(res[k].data(), c->d_tres.as<TrialRes>() + bases[k], tr[k].size() * sizeof(TrialRes),
@@ -1085,11 +1114,20 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
   std::vector<TrialRes> rr[3];
   for (int k = 1; k < 3; k++) {
     if (again[k].empty()) continue;
-    if (int r = launch(k, again[k].data(), again[k].size(), base)) return r;
+    if (int r = launch_kind(k, again[k].data(), again[k].size(), base)) return r;
     rr[k].resize(again[k].size());
-    HIPCHK(hipMemcpyAsync(rr[k].data(), c->d_tres.as<TrialRes>() + base, again[k].size() * sizeof(TrialRes),
-                          hipMemcpyDeviceToHost, c->st));
     base += again[k].size();
+  }
+  if (int r = join()) return r;
+  {
+    size_t b2 = base;
+    for (int k = 2; k >= 1; k--) b2 -= again[k].size();
+    for (int k = 1; k < 3; k++) {
+      if (again[k].empty()) continue;
+      HIPCHK(hipMemcpyAsync(rr[k].data(), c->d_tres.as<TrialRes>() + b2, again[k].size() * sizeof(TrialRes),
+                            hipMemcpyDeviceToHost, c->st));
+      b2 += again[k].size();
+    }
   }
   HIPCHK(hipStreamSynchronize(c->st));
   kcollect(c);
@@ -1310,6 +1348,8 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
     if (hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
     if (hipStreamCreateWithFlags(&p->pst, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
     if (hipEventCreateWithFlags(&p->pev, hipEventDisableTiming) != hipSuccess) return ATZ_E_HIP;
+    if (hipEventCreateWithFlags(&p->fev0, hipEventDisableTiming) != hipSuccess) return ATZ_E_HIP;
+    if (hipEventCreateWithFlags(&p->fev1, hipEventDisableTiming) != hipSuccess) return ATZ_E_HIP;
     c->pipes.push_back(std::move(p));
   }
   return 0;
@@ -1350,7 +1390,8 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
     p->t_list = p->t_chains = p->t_trials = p->t_apply = 0;
     std::memset(p->kind, 0, sizeof(p->kind));
   }
-  const size_t target = 16384;   // trials per round and pipe
+  static size_t target = 0;   // trials per round and pipe (ATZ_TARGET: tuning)
+  if (!target) { const char* e = std::getenv("ATZ_TARGET"); target = e ? (size_t)std::max(256, std::atoi(e)) : 4096; }   // C4: 16384 758, 8192 774, 4096 787 MB/s
   std::vector<int> rc(np, 0);
   if (np == 1) {
     rc[0] = sweep_pipe(c, c->pipes[0].get(), d_file, ss, target);
