@@ -586,7 +586,6 @@ struct TreeWork {      // one tree under construction (zlib's ct_data / heap / d
   uint32_t heap[HEAPN + 1];  // packed keys (freq:16 | depth:5 | node:10) in [1, heap_len]; node ids from heap_max
   uint16_t dad[HEAPN];
   uint16_t freq[NLC];        // leaf frequencies (forced leaves set to 1)
-  uint8_t len[NLC];          // leaf code lengths
   uint16_t bl_count[16];
 };
 
@@ -618,14 +617,15 @@ struct BitOut {
 static constexpr uint32_t STAGE_WORDS = 196;   // 64 * SYM_PER_LANE * 48 / 32 + 2 (+ pad)
 struct TrialShared {
   BitOut b;              // output / compare state of the trial (in LDS: the flush helpers take it by LDS reference)
-  uint32_t lfreq[NLC];
-  uint32_t dfreq[NDC];
+  uint32_t lfreq2[(NLC + 1) / 2];   // block frequencies, two 16-bit counts per word (symbol 2i low)
+  uint32_t dfreq2[NDC / 2];
   uint16_t lcode[NLC]; uint8_t llen[NLC + 2];
   uint16_t dcode[NDC]; uint8_t dlen[NDC + 2];
   uint16_t bcode[NBLC]; uint8_t blen[NBLC + 2];
   uint32_t bfreq[NBLC];
   TreeWork w;
-  uint32_t stage[STAGE_WORDS];   // bit-packing staging words (128 symbols x <= 48 bits + carry)
+  // the bit-packing staging words (STAGE_WORDS) live in the match-table ring's LDS: they are only
+  // used while a block is emitted, when the parse is paused (like TreeScratch during build_tree)
 };
 
 struct TrialSharedFast {
@@ -641,6 +641,7 @@ struct TrialSharedSlow {
   uint64_t ring[RING_SLOW];   // match-table entries (.x low, .y high) of the positions around the window
 };
 static_assert(sizeof(TreeScratch) <= RING_SLOW * sizeof(uint64_t), "tree scratch overlays the ring");
+static_assert(STAGE_WORDS * 4 <= RING_SLOW * sizeof(uint64_t), "emission staging overlays the ring");
 
 struct SweepArgs {
   const uint8_t* file;          // original compressed bytes
@@ -763,7 +764,7 @@ __device__ __forceinline__ void pq_down(LDS uint32_t* heap, int heap_len, int k,
 
 // build_tree + gen_bitlen (Z/trees.c:488-565, 617-699) from w.freq[0..elems).  Leaves' lengths land
 // in w.len, bl_count in w.bl_count; opt_len / static_len accumulate as in zlib.  Returns max_code.
-__device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, int elems, int max_length, const CONSTANT uint8_t* xbits,
+__device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, LDS uint8_t* lenv, int elems, int max_length, const CONSTANT uint8_t* xbits,
                                        int xbase, const CONSTANT uint8_t* stlen, uint64_t& opt_len,
                                        uint64_t& static_len, LDS uint64_t& cyc_heap, int lane) {
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -775,7 +776,7 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, int
     const uint32_t f = n < elems ? w.freq[n] : 0u;
     const uint64_t m = __ballot(f != 0);
     if (f) heap[heap_len + 1 + __popcll(m & lt)] = tkey(f, 0, (uint32_t)n);
-    else if (n < elems) w.len[n] = 0;
+    else if (n < elems) lenv[n] = 0;
     if (m) max_code = g + 63 - __clzll((long long)m);
     heap_len += __popcll(m);
   }
@@ -893,7 +894,7 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, int
     overflow += __popcll(__ballot(capped));
     if (bits > (uint32_t)max_length) bits = (uint32_t)max_length;
     const bool leaf = in_tree && i <= max_code;
-    if (leaf) w.len[i] = (uint8_t)bits;
+    if (leaf) lenv[i] = (uint8_t)bits;
     for (int b = 1; b <= 15; b++) {
       const uint32_t c = (uint32_t)__popcll(__ballot(leaf && bits == (uint32_t)b));
       if (lane == b) blc += c;
@@ -916,7 +917,7 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, int
       while (cnt != 0) {
         const uint32_t m = uni(heap[--h]);
         if ((int)m > max_code) continue;
-        if (lane == 0) w.len[m] = (uint8_t)bits;
+        if (lane == 0) lenv[m] = (uint8_t)bits;
         cnt--;
       }
     }
@@ -927,7 +928,7 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, int
   for (int n = lane; n < elems && n <= max_code; n += 64) {
     const uint32_t f = w.freq[n];
     if (f) {
-      const uint32_t l = w.len[n];
+      const uint32_t l = lenv[n];
       const uint32_t xb = (xbits && n >= xbase) ? xbits[n - xbase] : 0u;
       o += (uint64_t)f * (l + xb);
       if (stlen) st += (uint64_t)f * (stlen[n] + xb);
@@ -953,8 +954,7 @@ __device__ __noinline__ void gen_codes(const LDS TreeWork& w, int max_code, LDS 
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (int g = 0; g <= max_code; g += 64) {
     const int n = g + lane;
-    const uint32_t l = n <= max_code ? w.len[n] : 0u;
-    if (n <= max_code) lens[n] = (uint8_t)l;
+    const uint32_t l = n <= max_code ? lens[n] : 0u;   // build_tree left the lengths here
     uint32_t mine = 0;
     for (int b = 1; b <= 15; b++) {
       const uint64_t m = __ballot(l == (uint32_t)b);
@@ -1069,7 +1069,8 @@ __device__ __forceinline__ void emit_lane_bits(LDS BitOut& b, LDS uint32_t* stag
 // (v only in the run's first chunk, where prevlen != v), REPZ_3_10+3 or REPZ_11_138+7.  So every
 // element finds its run (ballot masks of run starts; max_code + 1 is zlib's guard) and a chunk's
 // first element contributes the chunk: send = its bits in element order, else its bl_tree counts.
-__device__ void rle_tree(LDS BitOut& b, LDS TrialShared& s, const LDS uint8_t* ln, int max_code, bool send, int lane) {
+__device__ void rle_tree(LDS BitOut& b, LDS TrialShared& s, LDS uint32_t* stage, const LDS uint8_t* ln, int max_code, bool send,
+                         int lane) {
   const int N = max_code + 1;   // elements; position N acts as a run start (the guard)
   const int G = N / 64 + 1;     // groups covering 0..N (N <= 286: at most 5)
   uint64_t M[5];
@@ -1139,7 +1140,7 @@ __device__ void rle_tree(LDS BitOut& b, LDS TrialShared& s, const LDS uint8_t* l
         }
       }
     }
-    if (send) emit_lane_bits(b, s.stage, v64, nb, lane);
+    if (send) emit_lane_bits(b, stage, v64, nb, lane);
   }
 }
 
@@ -1147,7 +1148,7 @@ __device__ void rle_tree(LDS BitOut& b, LDS TrialShared& s, const LDS uint8_t* l
 // tested after every step: a bailed trial stops inside its first block instead of emitting all of
 // it.  Returns true when the trial is decided (the caller re-evaluates early_exit).
 template <typename C16, typename C8>
-__device__ bool compress_block(LDS BitOut& b, LDS TrialShared& s, const GLOBAL uint32_t* syms, uint32_t nsym,
+__device__ bool compress_block(LDS BitOut& b, LDS TrialShared& s, LDS uint32_t* stage, const GLOBAL uint32_t* syms, uint32_t nsym,
                                C16 lc, C8 ll, C16 dc, C8 dl, const SweepOpts& o, uint64_t best_ident,
                                bool full_needed, int lane) {
   // the symbols were stored by other lanes during the parse: order those HBM stores before the reads
@@ -1171,16 +1172,16 @@ __device__ bool compress_block(LDS BitOut& b, LDS TrialShared& s, const GLOBAL u
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (total == 0) break;
     // stage words: word 0..1 seeded with the pending bits
-    for (int i = lane; i < (int)STAGE_WORDS; i += 64) s.stage[i] = 0;
-    if (lane == 0) { s.stage[0] = (uint32_t)b.bb; s.stage[1] = (uint32_t)(b.bb >> 32); }
+    for (int i = lane; i < (int)STAGE_WORDS; i += 64) stage[i] = 0;
+    if (lane == 0) { stage[0] = (uint32_t)b.bb; stage[1] = (uint32_t)(b.bb >> 32); }
     const uint32_t off = b.bc + incl - nb;
-    stage_or(s.stage, off, v0, n0);
-    stage_or(s.stage, off + n0, v1, n1);
+    stage_or(stage, off, v0, n0);
+    stage_or(stage, off + n0, v1, n1);
     const uint32_t all = b.bc + total;
     const uint32_t full = all >> 3;
-    emit_bytes_from_stage(b, s.stage, full, lane);
+    emit_bytes_from_stage(b, stage, full, lane);
     const uint32_t rem = all & 7;
-    const uint32_t lastw = s.stage[full >> 2];
+    const uint32_t lastw = stage[full >> 2];
     b.bb = rem ? ((lastw >> (8 * (full & 3))) & 0xff) & ((1u << rem) - 1) : 0;
     b.bc = rem;
     if (!full_needed && early_exit(b, o, best_ident, false) != ~0u) return true;
@@ -1248,6 +1249,7 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
                                              uint32_t level, uint32_t lbs, int last, SweepOpts opt,
                                              uint64_t best_ident, bool full_needed, int lane) {
   uint32_t hazard = 0;
+  LDS uint32_t* const stage = (LDS uint32_t*)&sc;   // emission staging overlays the tree scratch
   const uint64_t c0 = clock64();
   const bool bufok = block_start >= (int64_t)S;
   const uint64_t stored_len = (uint64_t)((int64_t)p - block_start);
@@ -1255,25 +1257,25 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
   int lmax = 0, dmax = 0, max_blindex = 0;
   if (level > 0) {
     // literal/length tree
-    for (int i = lane; i < NLC; i += 64) s.w.freq[i] = (uint16_t)s.lfreq[i];
-    lmax = build_tree(s.w, sc, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
+    for (int i = lane; i < NLC; i += 64) s.w.freq[i] = (uint16_t)(s.lfreq2[i >> 1] >> (16 * (i & 1)));
+    lmax = build_tree(s.w, sc, s.llen, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
                       opt_len, static_len, b.cyc_heap, lane);
     gen_codes(s.w, lmax, s.lcode, s.llen, lane);
     for (int i = lmax + 1 + lane; i < NLC + 2; i += 64) s.llen[i] = 0;
     // distance tree
-    for (int i = lane; i < NDC; i += 64) s.w.freq[i] = (uint16_t)s.dfreq[i];
-    dmax = build_tree(s.w, sc, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
+    for (int i = lane; i < NDC; i += 64) s.w.freq[i] = (uint16_t)(s.dfreq2[i >> 1] >> (16 * (i & 1)));
+    dmax = build_tree(s.w, sc, s.dlen, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
                       opt_len, static_len, b.cyc_heap, lane);
     gen_codes(s.w, dmax, s.dcode, s.dlen, lane);
     for (int i = dmax + 1 + lane; i < NDC + 2; i += 64) s.dlen[i] = 0;
     // bit length tree
     for (int i = lane; i < NBLC; i += 64) s.bfreq[i] = 0;
     const uint64_t cs0 = STEP_CLOCK();
-    rle_tree(b, s, s.llen, lmax, false, lane);
-    rle_tree(b, s, s.dlen, dmax, false, lane);
+    rle_tree(b, s, stage, s.llen, lmax, false, lane);
+    rle_tree(b, s, stage, s.dlen, dmax, false, lane);
     b.cyc_scan += STEP_CLOCK() - cs0;
     for (int i = lane; i < NBLC; i += 64) s.w.freq[i] = (uint16_t)s.bfreq[i];
-    int bmax = build_tree(s.w, sc, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, opt_len, static_len, b.cyc_heap, lane);
+    int bmax = build_tree(s.w, sc, s.blen, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, opt_len, static_len, b.cyc_heap, lane);
     gen_codes(s.w, bmax, s.bcode, s.blen, lane);
     for (int i = bmax + 1 + lane; i < NBLC + 2; i += 64) s.blen[i] = 0;
     for (max_blindex = NBLC - 1; max_blindex >= 3; max_blindex--)
@@ -1290,10 +1292,10 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
   b.cyc_tree += c1 - c0;
   b.blocks++;
   if (stored_len + 4 <= opt_lenb && bufok) {
-    put_bits(b, s.stage, (uint32_t)last, 3, lane);
-    windup(b, s.stage, lane);
+    put_bits(b, stage, (uint32_t)last, 3, lane);
+    windup(b, stage, lane);
     uint32_t len = (uint32_t)stored_len;
-    put_bits(b, s.stage, (len & 0xffff) | ((~len & 0xffff) << 16), 32, lane);
+    put_bits(b, stage, (len & 0xffff) | ((~len & 0xffff) << 16), 32, lane);
     // copy the block's input bytes (now byte aligned, bc == 0)
     const GLOBAL uint8_t* src = in + block_start;
     for (uint64_t o = 0; o < stored_len; o += 256) {
@@ -1304,38 +1306,38 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
           uint32_t at = 4 * k + q;
           if (at < nb) wv |= (uint32_t)src[o + at] << (8 * q);
         }
-        s.stage[k] = wv;
+        stage[k] = wv;
       }
-      emit_bytes_from_stage(b, s.stage, nb, lane);
+      emit_bytes_from_stage(b, stage, nb, lane);
       if (!full_needed && early_exit(b, opt, best_ident, false) != ~0u) break;
     }
   } else if (static_lenb == opt_lenb) {
-    put_bits(b, s.stage, (1u << 1) + (uint32_t)last, 3, lane);
-    compress_block(b, s, syms, last_lit, (const CONSTANT uint16_t*)c_t.st_lcode, (const CONSTANT uint8_t*)c_t.st_llen,
+    put_bits(b, stage, (1u << 1) + (uint32_t)last, 3, lane);
+    compress_block(b, s, stage, syms, last_lit, (const CONSTANT uint16_t*)c_t.st_lcode, (const CONSTANT uint8_t*)c_t.st_llen,
                    (const CONSTANT uint16_t*)c_t.st_dcode, (const CONSTANT uint8_t*)c_t.st_dlen, opt, best_ident,
                    full_needed, lane);
   } else {
     int lcodes = lmax + 1, dcodes = dmax + 1, blcodes = max_blindex + 1;
-    put_bits(b, s.stage, (2u << 1) + (uint32_t)last, 3, lane);
-    put_bits(b, s.stage, (uint32_t)(lcodes - 257), 5, lane);
-    put_bits(b, s.stage, (uint32_t)(dcodes - 1), 5, lane);
-    put_bits(b, s.stage, (uint32_t)(blcodes - 4), 4, lane);
-    for (int r = 0; r < blcodes; r++) put_bits(b, s.stage, s.blen[bl_order((uint32_t)r)], 3, lane);
+    put_bits(b, stage, (2u << 1) + (uint32_t)last, 3, lane);
+    put_bits(b, stage, (uint32_t)(lcodes - 257), 5, lane);
+    put_bits(b, stage, (uint32_t)(dcodes - 1), 5, lane);
+    put_bits(b, stage, (uint32_t)(blcodes - 4), 4, lane);
+    for (int r = 0; r < blcodes; r++) put_bits(b, stage, s.blen[bl_order((uint32_t)r)], 3, lane);
     const uint64_t cs0 = STEP_CLOCK();
-    rle_tree(b, s, s.llen, lcodes - 1, true, lane);
-    rle_tree(b, s, s.dlen, dcodes - 1, true, lane);
+    rle_tree(b, s, stage, s.llen, lcodes - 1, true, lane);
+    rle_tree(b, s, stage, s.dlen, dcodes - 1, true, lane);
     b.cyc_send += STEP_CLOCK() - cs0;
-    flush_bits_bytes(b, s.stage, lane);
-    compress_block(b, s, syms, last_lit, (const LDS uint16_t*)s.lcode, (const LDS uint8_t*)s.llen,
+    flush_bits_bytes(b, stage, lane);
+    compress_block(b, s, stage, syms, last_lit, (const LDS uint16_t*)s.lcode, (const LDS uint8_t*)s.llen,
                    (const LDS uint16_t*)s.dcode, (const LDS uint8_t*)s.dlen, opt, best_ident, full_needed, lane);
   }
   // 1.2.8 pending_buf/d_buf overlay condition (conservative, cf. oracle/ora_deflate.c)
   if (b.pos - blk_start_bytes > (uint64_t)lbs + 2ull * last_lit && last_lit) hazard = 1;
   // init_block
-  for (int i = lane; i < NLC; i += 64) s.lfreq[i] = 0;
-  for (int i = lane; i < NDC; i += 64) s.dfreq[i] = 0;
-  if (lane == 0) s.lfreq[256] = 1;
-  if (last) windup(b, s.stage, lane);
+  for (int i = lane; i < (NLC + 1) / 2; i += 64) s.lfreq2[i] = 0;
+  for (int i = lane; i < NDC / 2; i += 64) s.dfreq2[i] = 0;
+  if (lane == 0) s.lfreq2[128] = 1;   // END_BLOCK (symbol 256: low half)
+  if (last) windup(b, stage, lane);
   b.cyc_emit += clock64() - c1;
   return hazard;
 }
@@ -1408,6 +1410,7 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t cnt, uint64_t lt, uin
 template <int KIND, typename SH>
 __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   LDS TrialShared& s = *(LDS TrialShared*)&shm.t;
+  LDS uint32_t* const stg = (LDS uint32_t*)shm.ring;   // emission staging (overlays the ring)
   const uint32_t t = blockIdx.x;
   const Trial tr = A.trials[t];
   const StreamDev sd = A.streams[tr.stream];
@@ -1433,9 +1436,9 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   b.cyc_tree = b.cyc_emit = b.blocks = 0;
   b.cyc_heap = b.cyc_scan = b.cyc_send = 0;
   const uint64_t cstart = clock64();
-  for (int i = lane; i < NLC; i += 64) s.lfreq[i] = 0;
-  for (int i = lane; i < NDC; i += 64) s.dfreq[i] = 0;
-  if (lane == 0) s.lfreq[256] = 1;
+  for (int i = lane; i < (NLC + 1) / 2; i += 64) s.lfreq2[i] = 0;
+  for (int i = lane; i < NDC / 2; i += 64) s.dfreq2[i] = 0;
+  if (lane == 0) s.lfreq2[128] = 1;   // END_BLOCK
   uint32_t hazard = 0;
   // Symbols and block statistics are tallied straight into HBM (syms) and LDS (lfreq / dfreq).
   uint32_t state = ~0u;
@@ -1447,7 +1450,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     uint32_t lf = z.level < 2 ? 0 : z.level < 6 ? 1 : z.level == 6 ? 2 : 3;
     header |= lf << 6;
     header += 31 - (header % 31);
-    put_bits(b, s.stage, ((header >> 8) & 0xff) | ((header & 0xff) << 8), 16, lane);
+    put_bits(b, stg, ((header >> 8) & 0xff) | ((header & 0xff) << 8), 16, lane);   // < 32 bits: no staging
   }
   // fast and slow kinds: match-table entries of the positions around the parse window in an LDS
   // ring; window slides (fill_window at the top of an iteration when lookahead < MIN_LOOKAHEAD)
@@ -1471,7 +1474,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   uint64_t pf = 0;
   if (KIND != 0 && n) pf = Rt[lane];
   auto FLUSH = [&](int last) {
-    hazard |= uni(flush_block(s, *(LDS TreeScratch*)ring, b, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in,
+    hazard |= uni(flush_block(s, *(LDS TreeScratch*)shm.ring, b, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in,
                               (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, A.o, tr.best_ident,
                               full_needed, lane));
     z.last_lit = 0;
@@ -1560,10 +1563,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       if (lane == 0) {
         syms[z.last_lit] = v;
         if (v >> 8) {
-          __hip_atomic_fetch_add(&s.lfreq[257u + len_code(v & 0xffu)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          __hip_atomic_fetch_add(&s.dfreq[dist_code((v >> 8) - 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&s.lfreq2[(257u + len_code(v & 0xffu)) >> 1], 1u << (16 * ((257u + len_code(v & 0xffu)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&s.dfreq2[(dist_code((v >> 8) - 1u)) >> 1], 1u << (16 * ((dist_code((v >> 8) - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else {
-          __hip_atomic_fetch_add(&s.lfreq[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
       z.last_lit++;
@@ -1653,11 +1656,11 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
             uint32_t v;
             if (wt == 2) {
               v = (D << 8) | (L - 3u);
-              __hip_atomic_fetch_add(&s.lfreq[257u + len_code(L - 3u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              __hip_atomic_fetch_add(&s.dfreq[dist_code(D - 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_fetch_add(&s.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_fetch_add(&s.dfreq2[(dist_code(D - 1u)) >> 1], 1u << (16 * ((dist_code(D - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else {
               v = ex & 0xffu;
-              __hip_atomic_fetch_add(&s.lfreq[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             syms[z.last_lit + (o - base)] = v;
           }
@@ -1880,10 +1883,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           else v = 0x80000000u | (D << 8) | (L - 3u);
           if (v & 0x80000000u) {
             v &= 0x7fffffffu;
-            __hip_atomic_fetch_add(&s.lfreq[257u + len_code(L - 3u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&s.dfreq[dist_code(D - 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.dfreq2[(dist_code(D - 1u)) >> 1], 1u << (16 * ((dist_code(D - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           } else {
-            __hip_atomic_fetch_add(&s.lfreq[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
           syms[z.last_lit + (o + k - base)] = v;
         }
@@ -1923,7 +1926,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         const uint32_t v = prevb;
         if (lane == 0) {
           syms[z.last_lit] = v;
-          __hip_atomic_fetch_add(&s.lfreq[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         z.last_lit++;
         z.nsym++;
@@ -1937,8 +1940,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     // adler32 trailer
     uint32_t ad = A.adler[tr.stream];
     uint32_t be = ((ad >> 24) & 0xff) | ((ad >> 8) & 0xff00) | ((ad << 8) & 0xff0000) | (ad << 24);
-    put_bits(b, s.stage, be, 32, lane);
-    flush_bits_bytes(b, s.stage, lane);
+    put_bits(b, stg, be, 32, lane);   // after the last block: the ring is no longer read
+    flush_bits_bytes(b, stg, lane);
     // final gates (main.cpp:632-681)
     if (b.overflow) state = TR_OVERFLOW;
     else if (full_needed) state = TR_FULL;
@@ -1974,15 +1977,19 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   }
 }
 
-__global__ __launch_bounds__(64) void k_trial_stored(SweepArgs A) {
-  __shared__ struct { TrialShared t; } shm;
+#ifndef TRIAL_SLOW_WAVES
+#define TRIAL_SLOW_WAVES 4   // waves per SIMD the trial kernels (and flush_block, which they share) are register-capped for:
+                             // the slow kind's 10 KB of LDS allows 16 waves per CU
+#endif
+__global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_stored(SweepArgs A) {
+  __shared__ struct { TrialShared t; uint64_t ring[(STAGE_WORDS + 1) / 2]; } shm;   // ring: staging only
   trial_body<0>(A, shm, threadIdx.x);
 }
-__global__ __launch_bounds__(64) void k_trial_fast(SweepArgs A) {
+__global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_fast(SweepArgs A) {
   __shared__ TrialSharedFast shm;
   trial_body<1>(A, shm, threadIdx.x);
 }
-__global__ __launch_bounds__(64) void k_trial_slow(SweepArgs A) {
+__global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_slow(SweepArgs A) {
   __shared__ TrialSharedSlow shm;
   trial_body<2>(A, shm, threadIdx.x);
 }
