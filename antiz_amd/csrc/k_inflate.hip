@@ -319,7 +319,10 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
       const uint64_t want = final ? ((prod + 255) & ~255ull) : out_cap;
       unsigned long long o = 0;
       if (lane == 0) o = atomicAdd(arena_used, (unsigned long long)want);
-      o = __shfl(o, 0, 64);
+      // broadcast with readfirstlane, not a shuffle: the slot (and `out`) must be provably
+      // wave-uniform, or every branch on `out` -- the far-copy check in the hot loop -- makes the
+      // decoder state divergent (VGPRs + exec-mask bookkeeping on every symbol)
+      o = ((uint64_t)iuni((uint32_t)(o >> 32)) << 32) | iuni((uint32_t)o);
       if (o + want <= arena_cap && (final || prod <= out_cap)) { arena_off = o; out = arena + o; }
     }
     uint64_t S = 0, W = 0;
