@@ -503,16 +503,35 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ i
   for (uint32_t w = threadIdx.x; w < nw + 8; w += 256) l32[w] = w < nw ? g32[w] : 0u;
   const uint32_t nh = n >= 3 ? n - 2 : 0;
   const uint32_t P = (uint32_t)jb.p1 < nh ? (uint32_t)jb.p1 : nh;   // candidates and walk starts are < P
-  for (uint32_t q0 = 0; q0 < P; q0 += 1024) {
-    uint32_t ix[4], a[4], b[4];
+  if (4 * P >= nh) {
+    // most positions wanted: one coalesced pass over the bucket array (entry i's predecessor is
+    // entry i - 1 unless i opens its bucket), scattered into LDS -- no dependent gathers
+    for (uint32_t i0 = 0; i0 < nh; i0 += 2048) {
+      uint32_t a[8], b[8];
 #pragma unroll
-    for (int u = 0; u < 4; u++) { const uint32_t q = q0 + 256 * u + threadIdx.x; ix[u] = q < P ? sidx[q] : 1u; }
+      for (int u = 0; u < 8; u++) {
+        const uint32_t i = i0 + 256 * u + threadIdx.x;
+        a[u] = i < nh ? bpos[i] : BUCKET_FIRST | 0x7fffffffu;
+        b[u] = (i < nh && i) ? bpos[i - 1] : 0u;
+      }
 #pragma unroll
-    for (int u = 0; u < 4; u++) { a[u] = bpos[ix[u]]; b[u] = ix[u] ? bpos[ix[u] - 1] : 0u; }
+      for (int u = 0; u < 8; u++) {
+        const uint32_t q = a[u] & ~BUCKET_FIRST;
+        if (q < P) prv[q] = (a[u] & BUCKET_FIRST) ? (uint16_t)PREV_NIL : (uint16_t)(b[u] & ~BUCKET_FIRST);
+      }
+    }
+  } else {
+    for (uint32_t q0 = 0; q0 < P; q0 += 2048) {
+      uint32_t ix[8], a[8], b[8];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const uint32_t q = q0 + 256 * u + threadIdx.x;
-      if (q < P) prv[q] = (a[u] & BUCKET_FIRST) ? (uint16_t)PREV_NIL : (uint16_t)(b[u] & ~BUCKET_FIRST);
+      for (int u = 0; u < 8; u++) { const uint32_t q = q0 + 256 * u + threadIdx.x; ix[u] = q < P ? sidx[q] : 1u; }
+#pragma unroll
+      for (int u = 0; u < 8; u++) { a[u] = bpos[ix[u]]; b[u] = ix[u] ? bpos[ix[u] - 1] : 0u; }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t q = q0 + 256 * u + threadIdx.x;
+        if (q < P) prv[q] = (a[u] & BUCKET_FIRST) ? (uint16_t)PREV_NIL : (uint16_t)(b[u] & ~BUCKET_FIRST);
+      }
     }
   }
   __syncthreads();
