@@ -918,6 +918,10 @@ static uint64_t match_prefix(uint64_t n, int memlevel) {
   return std::min(n, x);
 }
 
+static uint64_t c_cfg_host(uint32_t level) {   // max_chain of a level (Z/deflate.c:131-143)
+  static const uint16_t chain[10] = {0, 4, 8, 32, 16, 32, 128, 256, 1024, 4096};
+  return chain[level < 10 ? level : 9];
+}
 // Jobs whose walks touch at most 32 KiB of their stream run on k_match_lds (stream bytes and the
 // 16-bit prev[] chain staged in LDS: 3 bytes per staged position), one launch per size class so the
 // dynamic LDS -- and with it the blocks per CU -- fits the class; longer ones walk in HBM (k_match).
@@ -930,24 +934,47 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
     for (int k = 0; k < NC; k++) if (b <= cls[k]) return k;
     return NC;
   };
+  // launch groups: classes are merged into groups (one launch each, LDS of the group's largest class)
+  // so a round pays few launch tails; within a launch the longest walks go first (LPT)
+  static int groups = -1;   // ATZ_MATCH_GROUPS: 0 one launch per class, 1 two groups (<= 8 KiB, more), 2 one
+  if (groups < 0) { const char* e = std::getenv("ATZ_MATCH_GROUPS"); groups = e ? std::atoi(e) : 0; }   // C4: 0 847, 1 831, 2 834 MB/s
+  auto group_of = [&](int k) -> int {
+    if (k == NC) return NC;
+    if (groups == 0) return k;
+    if (groups == 1) return k <= 1 ? 1 : NC - 1;
+    return NC - 1;
+  };
   std::vector<MatchJob> mj;
   mj.reserve(mj0.size());
   size_t cnt[NC + 1] = {};
-  for (const MatchJob& m : mj0) cnt[class_of(m)]++;
+  int gmax[NC + 1];
+  for (int k = 0; k <= NC; k++) gmax[k] = -1;
+  for (const MatchJob& m : mj0) {
+    const int k = class_of(m), g = group_of(k);
+    cnt[g]++;
+    gmax[g] = std::max(gmax[g], k);
+  }
   size_t beg[NC + 2] = {};
   for (int k = 0; k <= NC; k++) beg[k + 1] = beg[k] + cnt[k];
   mj.resize(mj0.size());
   {
     size_t at[NC + 1];
     for (int k = 0; k <= NC; k++) at[k] = beg[k];
-    for (const MatchJob& m : mj0) mj[at[class_of(m)]++] = m;
+    for (const MatchJob& m : mj0) mj[at[group_of(class_of(m))]++] = m;
+    auto work = [](const MatchJob& m) -> uint64_t {   // positions x expected chain length
+      const uint64_t chain = std::min<uint64_t>(c_cfg_host(m.level), (m.p1 >> (m.memlevel + 7)) + 1);
+      return (m.p1 - m.p0) * chain;
+    };
+    for (int k = 0; k <= NC; k++)
+      std::stable_sort(mj.begin() + beg[k], mj.begin() + beg[k + 1],
+                       [&](const MatchJob& a, const MatchJob& b) { return work(a) > work(b); });
   }
   if (int r = upload(c, c->d_mjobs, mj.data(), mj.size() * sizeof(MatchJob))) return r;
   for (int k = 0; k <= NC; k++) {
     if (!cnt[k]) continue;
     kbeg(c, 4);
     if (k < NC)
-      hipLaunchKernelGGL(k_match_lds, dim3((uint32_t)cnt[k]), dim3(256), (uint32_t)(3 * cls[k] + 64), c->st,
+      hipLaunchKernelGGL(k_match_lds, dim3((uint32_t)cnt[k]), dim3(256), (uint32_t)(3 * cls[gmax[k]] + 64), c->st,
                          x->d_infl.as<uint8_t>(), c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(),
                          c->d_mjobs.as<MatchJob>() + beg[k]);
     else
