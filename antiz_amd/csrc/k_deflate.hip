@@ -1753,19 +1753,17 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           cand = cand && (uint32_t)__popcll(__ballot(cand) & lt) < room;
           const uint64_t cm = __ballot(cand);
           examined += (uint32_t)__popcll(cm);
-          // match lengths capped at nice (8 bytes per round trip); the first candidate reaching
+          // match lengths capped at nice (16 bytes per round trip); the first candidate reaching
           // nice ends the walk, so capped lengths decide the winner
           uint32_t len = 0;
           bool go = cand;
           while (__ballot(go)) {
             if (go) {
-              uint32_t m = 0;
-#pragma unroll
-              for (int j = 0; j < 8; j++) m |= (in[qc + len + j] == in[f + len + j] ? 1u : 0u) << j;
-              const uint32_t run = (uint32_t)__builtin_ctz(~m);   // matching prefix of the 8
+              // 16 bytes per round trip: 5 aligned dword loads per side (stream bases are 256-byte aligned)
+              const uint32_t run = match16((const GLOBAL uint32_t*)in, qc + len, f + len, nullptr, 0);
               const uint32_t left = nicec - len;
               len += run < left ? run : left;
-              go = run == 8 && len < nicec;
+              go = run == 16 && len < nicec;
             }
           }
           const uint64_t nm = __ballot(cand && len >= nicec);
