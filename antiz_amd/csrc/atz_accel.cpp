@@ -1186,9 +1186,13 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     std::vector<std::pair<uint32_t, int>> need;
     for (int k = 0; k < 3; k++) tr[k].clear();
     // per stream, its trials of this round in list order: (kind, index in tr[kind])
-    std::vector<std::vector<std::pair<int, uint32_t>>> mine(active.size());
+    // flat: stream a's trials are mine[mbeg[a] .. mbeg[a + 1])
+    std::vector<std::pair<int, uint32_t>> mine;
+    std::vector<uint32_t> mbeg(active.size() + 1);
+    mine.reserve(active.size() * K);
     uint64_t out_tot = 0, sym_tot = 0;
     for (size_t a = 0; a < active.size(); a++) {
+      mbeg[a] = (uint32_t)mine.size();
       const uint32_t s = active[a];
       StreamState& st = ss[s];
       for (uint32_t j = 0; j < K && st.idx + j < st.list.size(); j++) {
@@ -1202,10 +1206,11 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         t.sym_off = sym_tot; sym_tot += (1ull << (m + 6)) + 64;
         int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
         if (kind) need.push_back({s, m});
-        mine[a].push_back({kind, (uint32_t)tr[kind].size()});
+        mine.push_back({kind, (uint32_t)tr[kind].size()});
         tr[kind].push_back(t);
       }
     }
+    mbeg[active.size()] = (uint32_t)mine.size();
     auto ta = std::chrono::steady_clock::now();
     size_t nbuild = 0;
     for (auto& q : need) nbuild += x->chain_off[q.first][q.second] == ~0ull;
@@ -1282,10 +1287,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       const uint64_t C = x->recs[s].comp_len;
       const uint32_t phase0 = st.phase;
       int64_t last_dj = -1;
-      for (size_t j = 0; j < mine[a].size(); j++) {
-        if (st.phase != phase0) { nspec += mine[a].size() - j; break; }   // stopped earlier this round
-        const Trial& t = tr[mine[a][j].first][mine[a][j].second];
-        const TrialRes& r = trres[mine[a][j].first][mine[a][j].second];
+      for (uint32_t j = mbeg[a]; j < mbeg[a + 1]; j++) {
+        if (st.phase != phase0) { nspec += mbeg[a + 1] - j; break; }   // stopped earlier this round
+        const Trial& t = tr[mine[j].first][mine[j].second];
+        const TrialRes& r = trres[mine[j].first][mine[j].second];
         st.trials++;
         ntr++;
         if (r.state == TR_SHORTCUT) nsc++;
