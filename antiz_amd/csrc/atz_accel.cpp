@@ -1179,8 +1179,15 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
   // stops at its j-th trial discards the results of the later ones), K sized so a round fills the
   // GPU.  Results are applied per stream strictly in list order, so the outcome is the
   // reference's sequential one; the speculation only changes how much work runs per launch.
+  static size_t chunk = ~(size_t)0;   // ATZ_CHUNK=n: at most n streams per round (the rest wait their turn)
+  if (chunk == ~(size_t)0) { const char* e = std::getenv("ATZ_CHUNK"); chunk = e ? (size_t)std::atoll(e) : 0; }
   while (!active.empty()) {
     rounds++;
+    std::vector<uint32_t> waiting;
+    if (chunk && active.size() > chunk) {
+      waiting.assign(active.begin() + chunk, active.end());
+      active.resize(chunk);
+    }
     const auto tl0 = std::chrono::steady_clock::now();
     const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, target / active.size()));
     std::vector<std::pair<uint32_t, int>> need;
@@ -1360,6 +1367,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       }
     }
     std::vector<uint32_t> next;
+    next.swap(waiting);   // streams that sat this round out go first
     for (uint32_t s : active) if (ss[s].phase != 2) next.push_back(s);
     active.swap(next);
     c->t_apply += ms_since(tc);
