@@ -129,7 +129,7 @@ struct Rec {
 
 struct StreamState {
   // sweep
-  std::vector<uint32_t> list;     // packed (c<<16)|(w<<8)|m
+  const std::vector<uint32_t>* list = nullptr;   // packed (c<<16)|(w<<8)|m: the header type's shared list
   uint32_t idx = 0;
   uint32_t phase = 0;             // 0 = list A, 1 = list B, 2 = done
   uint8_t c = 9, w = 15, m = 9;   // streamOffset ctor defaults (ATZData.h:51-53)
@@ -168,6 +168,16 @@ void list_b(std::vector<uint32_t>& l, int type) {
   if (w == 10) prange(l, 1, 9, 11, 15, 1, 9);
   else if (w == 15) prange(l, 1, 9, 10, 14, 1, 9);
   else { prange(l, 1, 9, 10, w - 1, 1, 9); prange(l, 1, 9, w + 1, 15, 1, 9); }
+}
+
+// The trial lists depend only on the header type (24) and the phase: built once, shared by streams.
+const std::vector<uint32_t>& trial_list(int type, bool brute) {
+  static const std::array<std::array<std::vector<uint32_t>, 24>, 2> L = [] {
+    std::array<std::array<std::vector<uint32_t>, 24>, 2> t;
+    for (int ty = 0; ty < 24; ty++) { list_a(t[0][ty], ty); list_b(t[1][ty], ty); }
+    return t;
+  }();
+  return L[brute ? 1 : 0][type];
 }
 
 uint64_t bound(uint64_t n, int w, int m) {  // deflateBound (Z/deflate.c:566-621), zlib wrapper
@@ -1202,8 +1212,8 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       mbeg[a] = (uint32_t)mine.size();
       const uint32_t s = active[a];
       StreamState& st = ss[s];
-      for (uint32_t j = 0; j < K && st.idx + j < st.list.size(); j++) {
-        uint32_t p = st.list[st.idx + j];
+      for (uint32_t j = 0; j < K && st.idx + j < st.list->size(); j++) {
+        uint32_t p = (*st.list)[st.idx + j];
         int cl = (int)(p >> 16), w = (int)((p >> 8) & 0xff), m = (int)(p & 0xff);
         Trial t{};
         t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
@@ -1235,8 +1245,8 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       std::vector<std::pair<uint32_t, int>> nx;
       for (size_t a = 0; a < active.size(); a++) {
         const StreamState& st = ss[active[a]];
-        for (uint32_t j = K; j < 2 * K && st.idx + j < st.list.size(); j++) {
-          const uint32_t pp = st.list[st.idx + j];
+        for (uint32_t j = K; j < 2 * K && st.idx + j < st.list->size(); j++) {
+          const uint32_t pp = (*st.list)[st.idx + j];
           if ((pp >> 16) != 0 && x->chain_off[active[a]][pp & 0xff] == ~0ull) nx.push_back({active[a], (int)(pp & 0xff)});
         }
       }
@@ -1325,11 +1335,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
           }
         }
         st.idx++;
-        if (fullmatch) st.idx = (uint32_t)st.list.size();   // testParamRange/tryParams return
-        if (st.idx >= st.list.size()) {
+        if (fullmatch) st.idx = (uint32_t)st.list->size();   // testParamRange/tryParams return
+        if (st.idx >= st.list->size()) {
           if (st.phase == 0 && (C - st.ident) >= x->o.mismatch_tol && x->o.brute_window) {
-            st.list.clear();
-            list_b(st.list, x->recs[s].type);
+            st.list = &trial_list(x->recs[s].type, true);
             st.idx = 0;
             st.phase = 1;
           } else {
@@ -1408,7 +1417,7 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
   ss.assign(n, StreamState());
   c->chain_off.assign(n, {});
   for (auto& a : c->chain_off) a.fill(~0ull);
-  for (size_t s = 0; s < n; s++) list_a(ss[s].list, c->recs[s].type);
+  for (size_t s = 0; s < n; s++) ss[s].list = &trial_list(c->recs[s].type, false);
   // device stream table
   std::vector<StreamDev> sd(n);
   for (size_t s = 0; s < n; s++) {
@@ -1514,21 +1523,24 @@ static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::
     put8(h, 0); put8(h, F); put8(h, nrec);
     emit_meta(h);
   }
+  meta.reserve(meta.size() + nrec * 43 + 64);
+  segs.reserve(3 * n + 8);
   for (size_t s = 0; s < n; s++) {
     const StreamState& st = ss[s];
     if (!st.recomp) continue;
     const Rec& r = c->recs[s];
-    std::vector<uint8_t> d;
-    put8(d, r.offset); put8(d, r.comp_len); put8(d, r.infl_len);
-    d.push_back(st.c); d.push_back(st.w); d.push_back(st.m);
+    const size_t m0 = meta.size();   // the stream descriptor goes straight into meta
+    put8(meta, r.offset); put8(meta, r.comp_len); put8(meta, r.infl_len);
+    meta.push_back(st.c); meta.push_back(st.w); meta.push_back(st.m);
     uint64_t nd = st.rawdiff.size();
-    put8(d, nd);
+    put8(meta, nd);
     if (nd) {
-      put8(d, (uint64_t)st.first_diff);
-      for (uint64_t k = 0; k < nd; k++) put8(d, k == 0 ? 0 : (uint64_t)st.rawdiff[k] - st.rawdiff[k - 1]);
-      d.insert(d.end(), st.diffval.begin(), st.diffval.end());
+      put8(meta, (uint64_t)st.first_diff);
+      for (uint64_t k = 0; k < nd; k++) put8(meta, k == 0 ? 0 : (uint64_t)st.rawdiff[k] - st.rawdiff[k - 1]);
+      meta.insert(meta.end(), st.diffval.begin(), st.diffval.end());
     }
-    emit_meta(d);
+    segs.push_back({0, 0, m0, out, meta.size() - m0});
+    out += meta.size() - m0;
     segs.push_back({1, 0, c->infl_off[s], out, r.infl_len});
     out += r.infl_len;
   }
