@@ -426,7 +426,8 @@ static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, con
   }
   for (uint32_t k = 0; k < n; k++)   // bytes read + bytes written (when kept)
     c->stats.k_inflate_alg_bytes += res[k].consumed + (jobs[k].out_off == NO_OUT ? 0 : res[k].produced);
-  if (timing_on() && ATZ_INF_CLOCKS) {   // diagnostics build: clocks per job / per symbol
+#if ATZ_INF_CLOCKS
+  if (timing_on()) {   // diagnostics build: clocks per job / per symbol
     uint64_t cyc = 0, nl = 0, nm = 0, cmax = 0, outb = 0, cc = 0, cf = 0;
     for (uint32_t k = 0; k < n; k++) {
       cyc += res[k].cyc; nl += res[k].nlit; nm += res[k].nmatch; outb += res[k].produced;
@@ -437,6 +438,7 @@ static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, con
                  "%.1f cyc/symbol (copy %.3f Gcyc, flush %.3f Gcyc)\n", n, cyc / 1e9, cmax / 1e6, (unsigned long long)nl,
                  (unsigned long long)nm, (unsigned long long)outb, (nl + nm) ? (double)cyc / (nl + nm) : 0.0, cc / 1e9, cf / 1e9);
   }
+#endif
   return 0;
 }
 

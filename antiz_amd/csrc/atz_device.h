@@ -3,6 +3,10 @@
 #pragma once
 #include <stdint.h>
 
+#ifndef ATZ_INF_CLOCKS
+#define ATZ_INF_CLOCKS 0   // 1: per-job clocks and symbol counts in InfRes (diagnostics builds)
+#endif
+
 namespace atz {
 
 // ---- inflate (k_inflate) -------------------------------------------------------------------
@@ -26,8 +30,10 @@ struct InfRes {
   uint64_t consumed;  // zlib total_in at the stop
   uint64_t produced;  // zlib total_out at the stop
   uint64_t arena_off; // ARENA_OUT jobs: offset of the output slot (ARENA_NONE: none / incomplete)
-  uint64_t cyc, nlit, nmatch;  // diagnostics (ATZ_INF_CLOCKS builds): shader clocks, literals, matches
-  uint64_t cyc_copy, cyc_flush; //   clocks in match copies (incl. the stage write before) / ring flushes
+#if ATZ_INF_CLOCKS   // diagnostics builds only (the scan copies one InfRes per candidate back)
+  uint64_t cyc, nlit, nmatch;  // shader clocks, literals, matches
+  uint64_t cyc_copy, cyc_flush; // clocks in match copies (incl. the stage write before) / ring flushes
+#endif
 };
 
 // ---- deflate trial (k_trial) ---------------------------------------------------------------

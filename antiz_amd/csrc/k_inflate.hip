@@ -727,8 +727,12 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
     const uint64_t cons = (need + 7) >> 3;
     o.consumed = cons > job.in_len ? job.in_len : cons;
   }
-  o.cyc = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() - t_start : 0;
+#if ATZ_INF_CLOCKS
+  o.cyc = __builtin_amdgcn_s_memtime() - t_start;
   o.nlit = nlit; o.nmatch = nmatch; o.cyc_copy = cyc_copy; o.cyc_flush = cyc_flush;
+#else
+  (void)t_start; (void)nlit; (void)nmatch; (void)cyc_copy; (void)cyc_flush;
+#endif
   if (lane == 0) res[j] = o;
 }
 
