@@ -138,6 +138,7 @@ struct StreamState {
   std::vector<uint32_t> rawdiff;  // raw positions of the current best
   std::vector<uint8_t> diffval;
   uint32_t trials = 0;
+  uint32_t full_at = ~0u;         // list index whose trial ran past its match-table prefix: rerun with a full table
   bool recomp = false;
 };
 
@@ -1018,12 +1019,18 @@ static uint64_t full_tables_below() {   // ATZ_FULL_BELOW=n: rounds of <= n tria
   return (uint64_t)v;
 }
 static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
-                           std::vector<TrialRes>* res, const std::function<int()>& while_running);
+                           std::vector<TrialRes>* res, const std::function<int()>& while_running, bool allow_defer);
+static bool defer_rerun() {   // ATZ_DEFER_RERUN=1: TR_NEED_R trials wait for the next round (measured
+  static int v = -1;          // 750 vs 855 MB/s on C4: the stream falls a round behind; off)
+  if (v < 0) { const char* e = std::getenv("ATZ_DEFER_RERUN"); v = e ? std::atoi(e) : 0; }
+  return v != 0;
+}
 // A launch lasts as long as its slowest wave, so the trials go in longest-expected-first order
 // (classic LPT): low memLevels mean many blocks (one tree build each), fast levels mean hole
 // fallbacks, and the work grows with the stream.  Results come back in the caller's order.
 static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
-                      std::vector<TrialRes>* res, const std::function<int()>& while_running = nullptr) {
+                      std::vector<TrialRes>* res, const std::function<int()>& while_running = nullptr,
+                      bool allow_defer = false) {
   std::vector<Trial> tp[3];
   std::vector<uint32_t> perm[3];
   std::vector<TrialRes> rp[3];
@@ -1040,7 +1047,7 @@ static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Tri
     tp[k].resize(n);
     for (size_t q = 0; q < n; q++) tp[k][q] = tr[k][perm[k][q]];
   }
-  if (int r = run_trials_impl(x, c, d_cmp, tp, so, rp, while_running)) return r;
+  if (int r = run_trials_impl(x, c, d_cmp, tp, so, rp, while_running, allow_defer)) return r;
   for (int k = 0; k < 3; k++) {
     res[k].resize(tr[k].size());
     for (size_t q = 0; q < tr[k].size(); q++) res[k][perm[k][q]] = rp[k][q];
@@ -1048,7 +1055,7 @@ static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Tri
   return 0;
 }
 static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
-                           std::vector<TrialRes>* res, const std::function<int()>& while_running) {
+                           std::vector<TrialRes>* res, const std::function<int()>& while_running, bool allow_defer) {
   const bool full = tr[0].size() + tr[1].size() + tr[2].size() <= full_tables_below();
   uint64_t r_tot = 0;
   std::vector<MatchJob> mj;
@@ -1064,7 +1071,7 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
       const uint64_t n = x->recs[t.stream].infl_len;
       t.r_off = r_tot;
       r_tot += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
-      t.x_lim = ((t.mode & 1) || full) ? n : match_prefix(n, t.memlevel);
+      t.x_lim = ((t.mode & 3) || full) ? n : match_prefix(n, t.memlevel);
       MatchJob m{};
       m.infl_off = x->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
       m.p0 = 0; m.p1 = t.x_lim; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
@@ -1130,6 +1137,10 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
     if (int r = while_running()) return r;
   HIPCHK(hipStreamSynchronize(c->st));
   kcollect(c);
+  // Trials that parsed past their table prefix (TR_NEED_R) are rerun below with the rest of their
+  // table.  ATZ_DEFER_RERUN=1 instead hands them back to the sweep, which reschedules them in its
+  // next round with the whole table (slower: their stream falls a round behind).
+  if (defer_rerun() && allow_defer) return 0;
   // second pass: complete the match tables of the trials that need them and run those again
   std::vector<Trial> again[3];
   std::vector<size_t> where[3];
@@ -1220,6 +1231,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         Trial t{};
         t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
         t.best_ident = st.ident;
+        if (st.idx + j == st.full_at) t.mode |= 2;   // host-only bit: whole match table up front
         t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
         t.sym_off = sym_tot; sym_tot += (1ull << (m + 6)) + 64;
@@ -1254,7 +1266,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       }
       return nx.empty() ? 0 : chains_prefetch(x, c, nx);
     };
-    if (int r = run_trials(x, c, d_file, tr, so, trres, prefetch)) return r;
+    if (int r = run_trials(x, c, d_file, tr, so, trres, prefetch, true)) return r;
     auto tc = std::chrono::steady_clock::now();
     c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
     c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
@@ -1310,6 +1322,12 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         if (st.phase != phase0) { nspec += mbeg[a + 1] - j; break; }   // stopped earlier this round
         const Trial& t = tr[mine[j].first][mine[j].second];
         const TrialRes& r = trres[mine[j].first][mine[j].second];
+        if (r.state == TR_NEED_R) {   // deferred rerun: next round, with its whole match table
+          st.full_at = st.idx;
+          nspec += mbeg[a + 1] - j - 1;
+          c->stats.n_trials_rerun++;
+          break;
+        }
         st.trials++;
         ntr++;
         if (r.state == TR_SHORTCUT) nsc++;
@@ -1341,6 +1359,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         if (st.idx >= st.list->size()) {
           if (st.phase == 0 && (C - st.ident) >= x->o.mismatch_tol && x->o.brute_window) {
             st.list = &trial_list(x->recs[s].type, true);
+            st.full_at = ~0u;
             st.idx = 0;
             st.phase = 1;
           } else {
