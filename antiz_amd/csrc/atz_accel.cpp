@@ -438,6 +438,20 @@ static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, con
     std::fprintf(stderr, "atz: k_inflate %u jobs: %.3f Gcyc, max %.2f Mcyc, lit %llu match %llu out %llu, "
                  "%.1f cyc/symbol (copy %.3f Gcyc, flush %.3f Gcyc)\n", n, cyc / 1e9, cmax / 1e6, (unsigned long long)nl,
                  (unsigned long long)nm, (unsigned long long)outb, (nl + nm) ? (double)cyc / (nl + nm) : 0.0, cc / 1e9, cf / 1e9);
+    // where the cycles go: complete streams vs candidates that fail (false headers) by output size
+    uint64_t ce = 0, ne = 0, cfl[4] = {}, nfl[4] = {}, nf = 0, cfar = 0;
+    for (uint32_t k = 0; k < n; k++) nf += res[k].nfar, cfar += res[k].cyc_far;
+    std::fprintf(stderr, "atz: k_inflate far matches (source beyond the LDS ring): %llu, %.3f Gcyc\n",
+                 (unsigned long long)nf, cfar / 1e9);
+    for (uint32_t k = 0; k < n; k++) {
+      if (res[k].status == INF_END && res[k].consumed > 16) { ce += res[k].cyc; ne++; continue; }
+      const int b = res[k].produced < 64 ? 0 : res[k].produced < 1024 ? 1 : res[k].produced < 4096 ? 2 : 3;
+      cfl[b] += res[k].cyc; nfl[b]++;
+    }
+    std::fprintf(stderr, "atz: k_inflate streams %llu: %.3f Gcyc; failing candidates by output <64/<1K/<4K/more: "
+                 "%llu/%llu/%llu/%llu jobs, %.3f/%.3f/%.3f/%.3f Gcyc\n", (unsigned long long)ne, ce / 1e9,
+                 (unsigned long long)nfl[0], (unsigned long long)nfl[1], (unsigned long long)nfl[2], (unsigned long long)nfl[3],
+                 cfl[0] / 1e9, cfl[1] / 1e9, cfl[2] / 1e9, cfl[3] / 1e9);
   }
 #endif
   return 0;

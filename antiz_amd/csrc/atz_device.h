@@ -33,6 +33,7 @@ struct InfRes {
 #if ATZ_INF_CLOCKS   // diagnostics builds only (the scan copies one InfRes per candidate back)
   uint64_t cyc, nlit, nmatch;  // shader clocks, literals, matches
   uint64_t cyc_copy, cyc_flush; // clocks in match copies (incl. the stage write before) / ring flushes
+  uint64_t nfar, cyc_far;       // matches whose source lies beyond the LDS ring (read from HBM), their clocks
 #endif
 };
 

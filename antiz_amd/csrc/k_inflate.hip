@@ -240,7 +240,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
   if (j >= njobs) return;
   const InfJob job = jobs[j];
   const uint64_t t_start = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
-  uint64_t nlit = 0, nmatch = 0, cyc_copy = 0, cyc_flush = 0;
+  uint64_t nlit = 0, nmatch = 0, cyc_copy = 0, cyc_flush = 0, nfar = 0, cyc_far = 0;
   uint8_t* const ring = sh.ring;
   uint16_t* const lens = sh.lens;
   // per-lane shift of the canonical compare: lane l in 1..15 looks at the first l stream bits
@@ -372,6 +372,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
       const uint64_t src = prod - dist;
       const uint64_t valid = flushed < out_cap ? flushed : out_cap;
       if (!out || src + len > valid) return false;
+      const uint64_t tf0 = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
       __builtin_amdgcn_s_waitcnt(0);
       for (uint32_t i0 = 0; i0 < len; i0 += 64) {
         const uint32_t i = i0 + lane;
@@ -380,6 +381,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
           ring[(prod + i) & RMASK] = v;
         }
       }
+      if (ATZ_INF_CLOCKS) { nfar++; cyc_far += __builtin_amdgcn_s_memtime() - tf0; }
     } else if (dist >= len) {
       for (uint32_t i0 = 0; i0 < len; i0 += 64) {
         const uint32_t i = i0 + lane;
@@ -730,8 +732,9 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
 #if ATZ_INF_CLOCKS
   o.cyc = __builtin_amdgcn_s_memtime() - t_start;
   o.nlit = nlit; o.nmatch = nmatch; o.cyc_copy = cyc_copy; o.cyc_flush = cyc_flush;
+  o.nfar = nfar; o.cyc_far = cyc_far;
 #else
-  (void)t_start; (void)nlit; (void)nmatch; (void)cyc_copy; (void)cyc_flush;
+  (void)t_start; (void)nlit; (void)nmatch; (void)cyc_copy; (void)cyc_flush; (void)nfar; (void)cyc_far;
 #endif
   if (lane == 0) res[j] = o;
 }
