@@ -871,9 +871,13 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     c->d_chains.n = cap;
   }
   // hash tables of memLevel <= 8 and streams < 64 Ki positions: LDS kernels; memLevel 9: HBM scratch
-  std::vector<ChainJob> tiny, small, mid, big;
+  static int pk8 = -1;   // ATZ_PK8=1: memLevel 8 on packed 16-bit counters (2 blocks per CU; measured
+                         // 838 vs 852 MB/s on C4: its builds are faster but slow the concurrent trials)
+  if (pk8 < 0) { const char* e = std::getenv("ATZ_PK8"); pk8 = e ? std::atoi(e) : 0; }
+  std::vector<ChainJob> tiny, small, mid, big, eight;
   for (const ChainJob& jb : jobs) {
     const uint32_t hs = 1u << (jb.memlevel + 7);
+    if (pk8 && hs == 32768 && jb.n < 65536) { eight.push_back(jb); continue; }
     (jb.n >= 65536 || hs > 32768 ? big : hs <= 4096 ? tiny : hs <= 16384 ? small : mid).push_back(jb);
   }
   {
@@ -897,22 +901,32 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
       if (int r = launch(k_buckets_lds<32768>, tiny.size() + small.size(), mid.size(), "k_buckets_lds<32768>")) return r;
     }
   }
-  std::vector<ChainJob> nine, rest;   // memLevel 9 with n < 64 Ki: LDS counters + HBM bases
+  std::vector<ChainJob> nine, rest;   // memLevel 9 with n < 64 Ki: packed LDS counters + HBM bases
   for (const ChainJob& jb : big) ((jb.memlevel == 9 && jb.n < 65536) ? nine : rest).push_back(jb);
   big.swap(rest);
-  if (!nine.empty()) {
-    const size_t nb9 = 4096;
-    if (int r = B.d_heads2.reserve(nb9 * 65536 * 4)) return r;
-    for (size_t k = 0; k < nine.size(); k++) nine[k].slot = (uint32_t)(k % nb9);
-    if (int r = upload(c, B.d_cjobs3, nine.data(), nine.size() * sizeof(ChainJob))) return r;
-    for (size_t b0 = 0; b0 < nine.size(); b0 += nb9) {
-      const size_t nb = std::min(nb9, nine.size() - b0);
+  if (!nine.empty() || !eight.empty()) {   // packed counters: memLevel 8 first, then 9
+    const size_t nbs = 4096;   // HBM scratch slots for the bucket bases, reused in launch order
+    if (int r = B.d_heads2.reserve(nbs * 65536 * 4)) return r;
+    std::vector<ChainJob> pk(eight);
+    pk.insert(pk.end(), nine.begin(), nine.end());
+    for (size_t k = 0; k < pk.size(); k++) pk[k].slot = (uint32_t)(k % nbs);
+    if (int r = upload(c, B.d_cjobs3, pk.data(), pk.size() * sizeof(ChainJob))) return r;
+    for (size_t b0 = 0; b0 < pk.size();) {
+      const bool is8 = b0 < eight.size();
+      const size_t end = is8 ? eight.size() : pk.size();
+      const size_t nb = std::min(nbs - b0 % nbs, end - b0);   // a launch never holds two jobs of one slot
       kbeg(c, 2);
-      hipLaunchKernelGGL(k_buckets_lds9, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
-                         B.d_cjobs3.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), B.d_heads2.as<uint32_t>(),
-                         (uint32_t)nb);
+      if (is8)
+        hipLaunchKernelGGL(k_buckets_pk<15>, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
+                           B.d_cjobs3.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), B.d_heads2.as<uint32_t>(),
+                           (uint32_t)nb);
+      else
+        hipLaunchKernelGGL(k_buckets_pk<16>, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
+                           B.d_cjobs3.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), B.d_heads2.as<uint32_t>(),
+                           (uint32_t)nb);
       kend(c);
-      KCHECK("k_buckets_lds9");
+      KCHECK("k_buckets_pk");
+      b0 += nb;
     }
   }
   const size_t batch = 4096;   // scratch: 65536 x 8-byte words per job slot

@@ -264,14 +264,17 @@ __global__ __launch_bounds__(256) void k_buckets_lds(const uint8_t* __restrict__
   }
 }
 
-// memLevel 9 (65536 hashes), streams < 65536 positions: two 16-bit counters per LDS word (128 KiB)
-// for the histogram and then "assigned so far"; the bucket bases go to HBM scratch (read-only after
-// the scan, loaded one batch ahead with the hashes).  No HBM atomics.
-__global__ __launch_bounds__(256) void k_buckets_lds9(const uint8_t* __restrict__ infl,
-                                                     const ChainJob* __restrict__ jobs,
-                                                     uint32_t* __restrict__ chains, uint32_t* __restrict__ scratch,
-                                                     uint32_t njobs) {
-  __shared__ uint32_t pair[32768];   // counters of hashes 2i (low half) and 2i+1 (high half)
+// memLevel 8 / 9 (2^15 / 2^16 hashes), streams < 65536 positions: two 16-bit counters per LDS word
+// (64 / 128 KiB: half the LDS of 32-bit counters) for the histogram and then "assigned so far"; the
+// bucket bases go to HBM scratch (read-only after the scan, loaded one batch ahead with the hashes).
+// No HBM atomics.
+template <uint32_t HBITS>
+__global__ __launch_bounds__(256) void k_buckets_pk(const uint8_t* __restrict__ infl,
+                                                   const ChainJob* __restrict__ jobs,
+                                                   uint32_t* __restrict__ chains, uint32_t* __restrict__ scratch,
+                                                   uint32_t njobs) {
+  constexpr uint32_t PW = (1u << HBITS) / 2, QW = PW / 4;   // pair words, pair words per wave
+  __shared__ uint32_t pair[PW];   // counters of hashes 2i (low half) and 2i+1 (high half)
   __shared__ uint32_t wsum[4];
   const uint32_t j = blockIdx.x;
   if (j >= njobs) return;
@@ -283,8 +286,8 @@ __global__ __launch_bounds__(256) void k_buckets_lds9(const uint8_t* __restrict_
   uint32_t* sidx = chains + jb.chain_off;
   uint32_t* bpos = sidx + npad;
   uint32_t* base = scratch + (uint64_t)jb.slot * 65536;
-  const uint32_t hmask = 65535, hshift = 6;   // hash_bits 16
-  for (uint32_t i = tid; i < 32768; i += 256) pair[i] = 0;
+  const uint32_t hmask = (1u << HBITS) - 1, hshift = (HBITS + 2) / 3;
+  for (uint32_t i = tid; i < PW; i += 256) pair[i] = 0;
   __syncthreads();
   const uint32_t nh = n >= 3 ? n - 2 : 0;
   auto hash = [&](uint32_t p) -> uint32_t {
@@ -295,9 +298,9 @@ __global__ __launch_bounds__(256) void k_buckets_lds9(const uint8_t* __restrict_
     atomicAdd(&pair[h >> 1], 1u << (16 * (h & 1)));
   }
   __syncthreads();
-  // exclusive scan over the 65536 counts (each wave a quarter; lane handles 2 counts per word)
+  // exclusive scan over the 2^HBITS counts (each wave a quarter; lane handles 2 counts per word)
   uint32_t run = 0;
-  for (uint32_t g = wave * 8192; g < (wave + 1) * 8192; g += 64) {
+  for (uint32_t g = wave * QW; g < (wave + 1) * QW; g += 64) {
     const uint32_t w = pair[g + lane];
     const uint32_t c = (w & 0xffffu) + (w >> 16);
     uint32_t incl = c;
@@ -316,7 +319,7 @@ __global__ __launch_bounds__(256) void k_buckets_lds9(const uint8_t* __restrict_
   uint32_t off = 0;
   for (int w = 0; w < wave; w++) off += wsum[w];
   if (off)
-    for (uint32_t g = wave * 8192; g < (wave + 1) * 8192; g += 64) {
+    for (uint32_t g = wave * QW; g < (wave + 1) * QW; g += 64) {
       base[2 * (g + lane)] += off;
       base[2 * (g + lane) + 1] += off;
     }
