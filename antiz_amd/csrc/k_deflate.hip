@@ -784,11 +784,32 @@ __device__ __forceinline__ void pq_down(LDS uint32_t* heap, int heap_len, int k,
   heap[k] = v;
 }
 
+// Arguments of a non-inlined function are divergent to the compiler (any caller could pass
+// per-lane values), so a uniform argument used in control flow is re-asserted with readfirstlane:
+// the loops over it then run on SGPRs and scalar branches instead of exec-mask bookkeeping.
+template <typename T> __device__ __forceinline__ const CONSTANT T* uni_ptr(const CONSTANT T* p) {
+  return (const CONSTANT T*)(uintptr_t)uni((uint64_t)(uintptr_t)p);
+}
+template <typename T> __device__ __forceinline__ const GLOBAL T* uni_ptr(const GLOBAL T* p) {
+  return (const GLOBAL T*)(uintptr_t)uni((uint64_t)(uintptr_t)p);
+}
+
+struct TreeRes {
+  int max_code;
+  uint64_t d_opt, d_static;   // increments of opt_len / static_len (modulo 2^64, as zlib's ulg sums)
+};
+
 // build_tree + gen_bitlen (Z/trees.c:488-565, 617-699) from w.freq[0..elems).  Leaves' lengths land
-// in w.len, bl_count in w.bl_count; opt_len / static_len accumulate as in zlib.  Returns max_code.
-__device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, LDS uint8_t* lenv, int elems, int max_length, const CONSTANT uint8_t* xbits,
-                                       int xbase, const CONSTANT uint8_t* stlen, uint64_t& opt_len,
-                                       uint64_t& static_len, LDS uint64_t& cyc_heap, int lane) {
+// in lenv, bl_count in w.bl_count; returns max_code and the opt_len / static_len increments (in
+// registers: references to the caller's locals would put them in scratch memory).
+__device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc, LDS uint8_t* lenv, int elems, int max_length, const CONSTANT uint8_t* xbits,
+                                           int xbase, const CONSTANT uint8_t* stlen, LDS uint64_t& cyc_heap, int lane) {
+  elems = (int)uni((uint32_t)elems);
+  max_length = (int)uni((uint32_t)max_length);
+  xbase = (int)uni((uint32_t)xbase);
+  xbits = uni_ptr(xbits);
+  stlen = uni_ptr(stlen);
+  uint64_t opt_len = 0, static_len = 0;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   LDS uint32_t* const heap = w.heap;
   // leaves enter heap[1..] in increasing symbol order (Z/trees.c:631-638)
@@ -958,13 +979,14 @@ __device__ __noinline__ int build_tree(LDS TreeWork& w, LDS TreeScratch& sc, LDS
   }
   opt_len += wsum64(o);
   if (stlen) static_len += wsum64(st);
-  return max_code;
+  return TreeRes{max_code, opt_len, static_len};
 }
 
 // gen_codes (Z/trees.c:575-607), lane-parallel: the codes of one length are consecutive in
 // symbol order, so a ballot per length ranks the symbols.
 __device__ __noinline__ void gen_codes(const LDS TreeWork& w, int max_code, LDS uint16_t* codes, LDS uint8_t* lens,
                                        int lane) {
+  max_code = (int)uni((uint32_t)max_code);
   uint32_t nc = 0;   // lane b: next_code[b]
   {
     uint32_t code = 0;
@@ -1270,6 +1292,21 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
                                              int64_t block_start, uint64_t p, uint64_t S, uint32_t last_lit,
                                              uint32_t level, uint32_t lbs, int last, SweepOpts opt,
                                              uint64_t best_ident, bool full_needed, int lane) {
+  syms = uni_ptr(syms);
+  in = uni_ptr(in);
+  block_start = (int64_t)uni((uint64_t)block_start);
+  p = uni(p);
+  S = uni(S);
+  last_lit = uni(last_lit);
+  level = uni(level);
+  lbs = uni(lbs);
+  last = (int)uni((uint32_t)last);
+  opt.recomp_tresh = uni(opt.recomp_tresh);
+  opt.sizediff_tresh = uni(opt.sizediff_tresh);
+  opt.shortcut_len = uni(opt.shortcut_len);
+  opt.mismatch_tol = uni(opt.mismatch_tol);
+  best_ident = uni(best_ident);
+  full_needed = uni((uint32_t)full_needed) != 0;
   uint32_t hazard = 0;
   LDS uint32_t* const stage = (LDS uint32_t*)&sc;   // emission staging overlays the tree scratch
   const uint64_t c0 = clock64();
@@ -1280,14 +1317,20 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
   if (level > 0) {
     // literal/length tree
     for (int i = lane; i < NLC; i += 64) s.w.freq[i] = (uint16_t)(s.lfreq2[i >> 1] >> (16 * (i & 1)));
-    lmax = build_tree(s.w, sc, s.llen, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
-                      opt_len, static_len, b.cyc_heap, lane);
+    TreeRes r = build_tree(s.w, sc, s.llen, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
+                           b.cyc_heap, lane);
+    lmax = (int)uni((uint32_t)r.max_code);
+    opt_len += uni(r.d_opt);
+    static_len += uni(r.d_static);
     gen_codes(s.w, lmax, s.lcode, s.llen, lane);
     for (int i = lmax + 1 + lane; i < NLC + 2; i += 64) s.llen[i] = 0;
     // distance tree
     for (int i = lane; i < NDC; i += 64) s.w.freq[i] = (uint16_t)(s.dfreq2[i >> 1] >> (16 * (i & 1)));
-    dmax = build_tree(s.w, sc, s.dlen, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
-                      opt_len, static_len, b.cyc_heap, lane);
+    r = build_tree(s.w, sc, s.dlen, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
+                   b.cyc_heap, lane);
+    dmax = (int)uni((uint32_t)r.max_code);
+    opt_len += uni(r.d_opt);
+    static_len += uni(r.d_static);
     gen_codes(s.w, dmax, s.dcode, s.dlen, lane);
     for (int i = dmax + 1 + lane; i < NDC + 2; i += 64) s.dlen[i] = 0;
     // bit length tree
@@ -1297,7 +1340,9 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
     rle_tree(b, s, stage, s.dlen, dmax, false, lane);
     b.cyc_scan += STEP_CLOCK() - cs0;
     for (int i = lane; i < NBLC; i += 64) s.w.freq[i] = (uint16_t)s.bfreq[i];
-    int bmax = build_tree(s.w, sc, s.blen, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, opt_len, static_len, b.cyc_heap, lane);
+    r = build_tree(s.w, sc, s.blen, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, b.cyc_heap, lane);
+    const int bmax = (int)uni((uint32_t)r.max_code);
+    opt_len += uni(r.d_opt);
     gen_codes(s.w, bmax, s.bcode, s.blen, lane);
     for (int i = bmax + 1 + lane; i < NBLC + 2; i += 64) s.blen[i] = 0;
     for (max_blindex = NBLC - 1; max_blindex >= 3; max_blindex--)
