@@ -693,7 +693,12 @@ __device__ inline uint64_t wsum64(uint64_t v) {
 // independent accesses, all in flight together.
 __device__ inline void emit_bytes_from_stage(LDS BitOut& b, const LDS uint32_t* stage, uint32_t nb, int lane) {
   uint32_t eqa = 0, eqs = 0;
-  const uint64_t pos = b.pos, cap = b.cap, clen = b.clen, sc = b.shortcut;
+  // BitOut lives in LDS: its fields read back as VGPRs, so they are made uniform explicitly (the
+  // loops and branches on them are then scalar, the pointers usable as SGPR bases)
+  nb = uni(nb);
+  const uint64_t pos = uni(b.pos), cap = uni(b.cap), clen = uni(b.clen), sc = uni(b.shortcut);
+  GLOBAL uint8_t* const out = (GLOBAL uint8_t*)(uintptr_t)uni((uint64_t)(uintptr_t)b.out);
+  const GLOBAL uint8_t* const orig = (const GLOBAL uint8_t*)(uintptr_t)uni((uint64_t)(uintptr_t)b.orig);
   for (uint32_t w = (uint32_t)lane; 4 * w < nb; w += 64) {
     const uint32_t word = stage[w];
 #pragma unroll
@@ -701,9 +706,9 @@ __device__ inline void emit_bytes_from_stage(LDS BitOut& b, const LDS uint32_t* 
       const uint32_t k = 4 * w + j;
       const uint8_t x = (uint8_t)(word >> (8 * j));
       const uint64_t at = pos + k;
-      if (k < nb && at < cap) b.out[at] = x;
+      if (k < nb && at < cap) out[at] = x;
       if (k < nb && at < clen) {
-        const uint32_t e = b.orig[at] == x ? 1u : 0u;
+        const uint32_t e = orig[at] == x ? 1u : 0u;
         eqa += e;
         if (at < sc) eqs += e;
       }
@@ -718,26 +723,30 @@ __device__ inline void emit_bytes_from_stage(LDS BitOut& b, const LDS uint32_t* 
 // scalar emission (block headers, tree descriptions): bits accumulate in bb; whole bytes go out in
 // groups through the staging words.
 __device__ inline void put_bits(LDS BitOut& b, LDS uint32_t* stage, uint32_t v, uint32_t n, int lane) {
-  b.bb |= (uint64_t)v << b.bc;
-  b.bc += n;
-  if (b.bc >= 32) {
-    if (lane == 0) stage[0] = (uint32_t)b.bb;
+  const uint32_t bc = uni(b.bc) + n;
+  const uint64_t bb = uni(b.bb) | ((uint64_t)uni(v) << uni(b.bc));
+  if (bc >= 32) {
+    if (lane == 0) stage[0] = (uint32_t)bb;
     emit_bytes_from_stage(b, stage, 4, lane);
-    b.bb >>= 32;
-    b.bc -= 32;
+    b.bb = bb >> 32;
+    b.bc = bc - 32;
+  } else {
+    b.bb = bb;
+    b.bc = bc;
   }
 }
 __device__ inline void flush_bits_bytes(LDS BitOut& b, LDS uint32_t* stage, int lane) {  // whole bytes only
-  uint32_t nb = b.bc >> 3;
+  const uint32_t bc = uni(b.bc), nb = bc >> 3;
   if (!nb) return;
-  if (lane == 0) { stage[0] = (uint32_t)b.bb; stage[1] = (uint32_t)(b.bb >> 32); }
+  const uint64_t bb = uni(b.bb);
+  if (lane == 0) { stage[0] = (uint32_t)bb; stage[1] = (uint32_t)(bb >> 32); }
   emit_bytes_from_stage(b, stage, nb, lane);
-  b.bb = nb >= 8 ? 0 : (b.bb >> (8 * nb));
-  b.bc -= 8 * nb;
+  b.bb = nb >= 8 ? 0 : (bb >> (8 * nb));
+  b.bc = bc - 8 * nb;
 }
 __device__ inline void windup(LDS BitOut& b, LDS uint32_t* stage, int lane) {  // bi_windup
   flush_bits_bytes(b, stage, lane);
-  if (b.bc) {
+  if (uni(b.bc)) {
     if (lane == 0) stage[0] = (uint32_t)b.bb;
     emit_bytes_from_stage(b, stage, 1, lane);
     b.bb = 0; b.bc = 0;
@@ -1033,17 +1042,18 @@ __device__ __forceinline__ uint32_t dcode_base(uint32_t d) { return d < 2 ? d : 
 
 // Early-exit test after output progress: returns TR_* state to stop with, or ~0u to continue.
 __device__ inline uint32_t early_exit(const LDS BitOut& b, const SweepOpts& o, uint64_t best_ident, bool full_needed) {
-  if (b.overflow) return TR_OVERFLOW;
+  if (uni((uint32_t)b.overflow)) return TR_OVERFLOW;
   if (full_needed) return ~0u;
-  if (b.shortcut) {
-    uint64_t seen = b.pos < b.shortcut ? b.pos : b.shortcut;
-    uint64_t mism = seen - b.eq_sc;
+  const uint64_t pos = uni(b.pos), clen = uni(b.clen), sc = uni(b.shortcut);
+  if (sc) {
+    uint64_t seen = pos < sc ? pos : sc;
+    uint64_t mism = seen - uni(b.eq_sc);
     uint64_t thr = o.shortcut_len - o.recomp_tresh;   // uint64 wrap as in main.cpp:649
-    if (thr > b.shortcut || mism > b.shortcut - thr) return TR_SHORTCUT;
+    if (thr > sc || mism > sc - thr) return TR_SHORTCUT;
   }
-  if (b.pos > b.clen + o.sizediff_tresh) return TR_SIZEDIFF;
-  uint64_t seen = b.pos < b.clen ? b.pos : b.clen;
-  if (b.clen - (seen - b.eq_all) <= best_ident) return TR_CANT_BEAT;
+  if (pos > clen + o.sizediff_tresh) return TR_SIZEDIFF;
+  uint64_t seen = pos < clen ? pos : clen;
+  if (clen - (seen - uni(b.eq_all)) <= best_ident) return TR_CANT_BEAT;
   return ~0u;
 }
 
@@ -1094,9 +1104,10 @@ __device__ __forceinline__ void emit_lane_bits(LDS BitOut& b, LDS uint32_t* stag
   const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (total == 0) return;
   for (int i = lane; i < (int)STAGE_WORDS; i += 64) stage[i] = 0;
+  const uint32_t bc = uni(b.bc);
   if (lane == 0) { stage[0] = (uint32_t)b.bb; stage[1] = (uint32_t)(b.bb >> 32); }
-  stage_or(stage, b.bc + incl - nb, v, nb);
-  const uint32_t all = b.bc + total;
+  stage_or(stage, bc + incl - nb, v, nb);
+  const uint32_t all = bc + total;
   const uint32_t full = all >> 3;
   emit_bytes_from_stage(b, stage, full, lane);
   const uint32_t rem = all & 7;
@@ -1217,11 +1228,12 @@ __device__ bool compress_block(LDS BitOut& b, LDS TrialShared& s, LDS uint32_t* 
     if (total == 0) break;
     // stage words: word 0..1 seeded with the pending bits
     for (int i = lane; i < (int)STAGE_WORDS; i += 64) stage[i] = 0;
+    const uint32_t bc = uni(b.bc);
     if (lane == 0) { stage[0] = (uint32_t)b.bb; stage[1] = (uint32_t)(b.bb >> 32); }
-    const uint32_t off = b.bc + incl - nb;
+    const uint32_t off = bc + incl - nb;
     stage_or(stage, off, v0, n0);
     stage_or(stage, off + n0, v1, n1);
-    const uint32_t all = b.bc + total;
+    const uint32_t all = bc + total;
     const uint32_t full = all >> 3;
     emit_bytes_from_stage(b, stage, full, lane);
     const uint32_t rem = all & 7;
