@@ -34,6 +34,9 @@
 #define CONSTANT __attribute__((address_space(4)))
 #define GLOBAL __attribute__((address_space(1)))
 
+#ifndef ATZ_VISITED_CHECK
+#define ATZ_VISITED_CHECK 1   // fast levels: resolve slot-check failures by the visited nodes' insertion bits
+#endif
 // Per-step shader-clock counters in the parse loop (diagnostics; s_memtime also forces lgkmcnt waits).
 #ifndef ATZ_STEP_CLOCKS
 #define ATZ_STEP_CLOCKS 0
@@ -374,7 +377,11 @@ __global__ __launch_bounds__(256) void k_buckets_pk(const uint8_t* __restrict__ 
 // (NIL after the slide), which the parse checks.  nice_match is clamped to the lookahead, i.e.
 // to n - p near the end; bytes beyond the input can only extend candidates that already reach
 // n - p, which break at nice_match first.
-static constexpr uint32_t HOLE_SLOTS_M = 1024;   // == HOLE_SLOTS (fast-level hash slots; a collision only makes the hole check conservative)
+#ifndef ATZ_HOLE_SLOTS
+#define ATZ_HOLE_SLOTS 1024
+#endif
+static constexpr uint32_t HOLE_SLOTS_M = ATZ_HOLE_SLOTS;   // == HOLE_SLOTS (fast-level hash slots; a collision only makes the hole check conservative)
+static_assert(HOLE_SLOTS_M <= 2048 && (HOLE_SLOTS_M & (HOLE_SLOTS_M - 1)) == 0, "slot field is 11 bits of the match entry");
 
 // 16 bytes at byte offset x of a 4-byte aligned buffer: 5 aligned dword loads (independent, one
 // round trip) joined with v_alignbyte.  Reads up to 4 bytes past x + 16 (buffers carry slack).
@@ -1716,6 +1723,28 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
             const uint32_t wpos = x - ((ex >> 8) & 0x7fffu);
             exact = wpos > Sx && ins_get(wpos);
           }
+        } else if (!exact && ATZ_VISITED_CHECK && z.chain <= 8) {
+          // the walk spent its budget and a hole shares the slot: the entry is still exact when
+          // every node the walk visited (the bucket entries below x down to the lowest visited
+          // one, at most `chain` of them) was inserted -- deflate_fast's chain then starts with
+          // the same nodes and spends the same budget on them
+          const uint32_t lo = x - (ey >> 16);
+          const int32_t si = (int32_t)sidx[x];
+          bool ok = true, stop = false;
+          for (int32_t k = si - 1; ok && !stop && k > si - 1 - (int32_t)z.chain; k -= 4) {
+            uint32_t e4[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) e4[u] = k - u >= 0 ? bpos[k - u] : BUCKET_FIRST;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+              if (!ok || stop || k - u <= si - 1 - (int32_t)z.chain) break;
+              const uint32_t pos = e4[u] & ~BUCKET_FIRST;
+              if (k - u < 0 || pos < lo) { stop = true; break; }
+              ok = pos > Sx && ins_get(pos);
+              if (e4[u] & BUCKET_FIRST) stop = true;
+            }
+          }
+          exact = ok;
         }
         bad = !exact;
       }
