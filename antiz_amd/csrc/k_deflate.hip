@@ -378,7 +378,7 @@ __global__ __launch_bounds__(256) void k_buckets_pk(const uint8_t* __restrict__ 
 // to n - p near the end; bytes beyond the input can only extend candidates that already reach
 // n - p, which break at nice_match first.
 #ifndef ATZ_HOLE_SLOTS
-#define ATZ_HOLE_SLOTS 1024
+#define ATZ_HOLE_SLOTS 256   // C4 A/B (3 runs each): 1024 ~877, 512 ~878, 256 ~895, 128 ~869 MB/s (fast LDS 18.2 -> 15.1 KB)
 #endif
 static constexpr uint32_t HOLE_SLOTS_M = ATZ_HOLE_SLOTS;   // == HOLE_SLOTS (fast-level hash slots; a collision only makes the hole check conservative)
 static_assert(HOLE_SLOTS_M <= 2048 && (HOLE_SLOTS_M & (HOLE_SLOTS_M - 1)) == 0, "slot field is 11 bits of the match entry");
@@ -611,10 +611,8 @@ static constexpr uint32_t LOOKMIN = 262;
 static constexpr uint32_t BITMAP_BITS = 32768;
 static constexpr uint32_t HOLE_SLOTS = HOLE_SLOTS_M;   // fast mode: latest skipped position per hash slot
 
-struct TreeWork {      // one tree under construction (zlib's ct_data / heap / depth in LDS)
+struct TreeWork {      // one tree under construction (zlib's heap / bl_count in LDS; dad and freq in TreeScratch)
   uint32_t heap[HEAPN + 1];  // packed keys (freq:16 | depth:5 | node:10) in [1, heap_len]; node ids from heap_max
-  uint16_t dad[HEAPN];
-  uint16_t freq[NLC];        // leaf frequencies (forced leaves set to 1)
   uint16_t bl_count[16];
 };
 
@@ -622,8 +620,9 @@ struct TreeWork {      // one tree under construction (zlib's ct_data / heap / d
 // paused while a block is flushed; the ring is reloaded from HBM afterwards), which keeps the
 // trial kernels' LDS small enough for more waves per CU.
 struct TreeScratch {
-  uint16_t anc[2][HEAPN];
+  uint16_t anc[2][HEAPN];    // anc[1] holds zlib's dad[] while the heap runs (read once into anc[0])
   uint8_t dep[2][HEAPN];
+  uint16_t freq[NLC];        // leaf frequencies of the tree being built (forced leaves set to 1)
 };
 
 struct BitOut {
@@ -815,7 +814,7 @@ struct TreeRes {
   uint64_t d_opt, d_static;   // increments of opt_len / static_len (modulo 2^64, as zlib's ulg sums)
 };
 
-// build_tree + gen_bitlen (Z/trees.c:488-565, 617-699) from w.freq[0..elems).  Leaves' lengths land
+// build_tree + gen_bitlen (Z/trees.c:488-565, 617-699) from sc.freq[0..elems).  Leaves' lengths land
 // in lenv, bl_count in w.bl_count; returns max_code and the opt_len / static_len increments (in
 // registers: references to the caller's locals would put them in scratch memory).
 __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc, LDS uint8_t* lenv, int elems, int max_length, const CONSTANT uint8_t* xbits,
@@ -832,7 +831,7 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
   int heap_len = 0, max_code = -1;
   for (int g = 0; g < elems; g += 64) {
     const int n = g + lane;
-    const uint32_t f = n < elems ? w.freq[n] : 0u;
+    const uint32_t f = n < elems ? sc.freq[n] : 0u;
     const uint64_t m = __ballot(f != 0);
     if (f) heap[heap_len + 1 + __popcll(m & lt)] = tkey(f, 0, (uint32_t)n);
     else if (n < elems) lenv[n] = 0;
@@ -843,7 +842,7 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
   while (heap_len < 2) {
     const int node = max_code < 2 ? ++max_code : 0;
     ++heap_len;
-    if (lane == 0) { heap[heap_len] = tkey(1, 0, (uint32_t)node); w.freq[node] = 1; }
+    if (lane == 0) { heap[heap_len] = tkey(1, 0, (uint32_t)node); sc.freq[node] = 1; }
     opt_len--;
     if (stlen) static_len -= stlen[node];
   }
@@ -884,8 +883,8 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
       if (lane == 0) {
         heap[--heap_max] = kn & 1023u;
         heap[--heap_max] = km & 1023u;
-        w.dad[kn & 1023u] = (uint16_t)node;
-        w.dad[km & 1023u] = (uint16_t)node;
+        sc.anc[1][kn & 1023u] = (uint16_t)node;
+        sc.anc[1][km & 1023u] = (uint16_t)node;
       } else {
         heap_max -= 2;
       }
@@ -907,8 +906,8 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
     if (lane == 0) {
       heap[--heap_max] = kn & 1023u;
       heap[--heap_max] = km & 1023u;
-      w.dad[kn & 1023u] = (uint16_t)node;
-      w.dad[km & 1023u] = (uint16_t)node;
+      sc.anc[1][kn & 1023u] = (uint16_t)node;
+      sc.anc[1][km & 1023u] = (uint16_t)node;
     } else {
       heap_max -= 2;
     }
@@ -925,9 +924,9 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
   // five rounds), bits = min(depth, max_length); zlib counts the nodes it had to cap (overflow).
   const int nn = (int)node;   // node ids 0..nn-1 (leaves not in the tree are never read)
   for (int i = lane; i < nn; i += 64) {
-    const bool in_tree = i >= elems || (i <= max_code && w.freq[i] != 0);
+    const bool in_tree = i >= elems || (i <= max_code && sc.freq[i] != 0);
     const bool r = (uint32_t)i == root || !in_tree;   // leaves outside the tree: never followed
-    sc.anc[0][i] = r ? (uint16_t)root : w.dad[i];
+    sc.anc[0][i] = r ? (uint16_t)root : sc.anc[1][i];
     sc.dep[0][i] = r ? 0 : 1;
   }
   int cur = 0;
@@ -946,7 +945,7 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
     bool in_tree = false;
     uint32_t bits = 0;
     if (i < nn) {
-      in_tree = i >= elems || (i <= max_code && w.freq[i] != 0);   // internal node or leaf in the heap
+      in_tree = i >= elems || (i <= max_code && sc.freq[i] != 0);   // internal node or leaf in the heap
       bits = sc.dep[cur][i];
     }
     const bool capped = in_tree && (uint32_t)i != root && bits > (uint32_t)max_length;
@@ -985,7 +984,7 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
   // opt_len / static_len over the final lengths (= zlib's running sums + fix-up terms)
   uint64_t o = 0, st = 0;
   for (int n = lane; n < elems && n <= max_code; n += 64) {
-    const uint32_t f = w.freq[n];
+    const uint32_t f = sc.freq[n];
     if (f) {
       const uint32_t l = lenv[n];
       const uint32_t xb = (xbits && n >= xbase) ? xbits[n - xbase] : 0u;
@@ -1335,7 +1334,7 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
   int lmax = 0, dmax = 0, max_blindex = 0;
   if (level > 0) {
     // literal/length tree
-    for (int i = lane; i < NLC; i += 64) s.w.freq[i] = (uint16_t)(s.lfreq2[i >> 1] >> (16 * (i & 1)));
+    for (int i = lane; i < NLC; i += 64) sc.freq[i] = (uint16_t)(s.lfreq2[i >> 1] >> (16 * (i & 1)));
     TreeRes r = build_tree(s.w, sc, s.llen, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
                            b.cyc_heap, lane);
     lmax = (int)uni((uint32_t)r.max_code);
@@ -1344,7 +1343,7 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
     gen_codes(s.w, lmax, s.lcode, s.llen, lane);
     for (int i = lmax + 1 + lane; i < NLC + 2; i += 64) s.llen[i] = 0;
     // distance tree
-    for (int i = lane; i < NDC; i += 64) s.w.freq[i] = (uint16_t)(s.dfreq2[i >> 1] >> (16 * (i & 1)));
+    for (int i = lane; i < NDC; i += 64) sc.freq[i] = (uint16_t)(s.dfreq2[i >> 1] >> (16 * (i & 1)));
     r = build_tree(s.w, sc, s.dlen, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
                    b.cyc_heap, lane);
     dmax = (int)uni((uint32_t)r.max_code);
@@ -1358,7 +1357,7 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
     rle_tree(b, s, stage, s.llen, lmax, false, lane);
     rle_tree(b, s, stage, s.dlen, dmax, false, lane);
     b.cyc_scan += STEP_CLOCK() - cs0;
-    for (int i = lane; i < NBLC; i += 64) s.w.freq[i] = (uint16_t)s.bfreq[i];
+    for (int i = lane; i < NBLC; i += 64) sc.freq[i] = (uint16_t)s.bfreq[i];
     r = build_tree(s.w, sc, s.blen, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, b.cyc_heap, lane);
     const int bmax = (int)uni((uint32_t)r.max_code);
     opt_len += uni(r.d_opt);
