@@ -37,6 +37,9 @@
 #ifndef ATZ_VISITED_CHECK
 #define ATZ_VISITED_CHECK 1   // fast levels: resolve slot-check failures by the visited nodes' insertion bits
 #endif
+#ifndef ATZ_VISITED_MAX
+#define ATZ_VISITED_MAX 8     // ... for levels whose chain budget is at most this (level 3's 32: measured slower)
+#endif
 // Per-step shader-clock counters in the parse loop (diagnostics; s_memtime also forces lgkmcnt waits).
 #ifndef ATZ_STEP_CLOCKS
 #define ATZ_STEP_CLOCKS 0
@@ -1722,7 +1725,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
             const uint32_t wpos = x - ((ex >> 8) & 0x7fffu);
             exact = wpos > Sx && ins_get(wpos);
           }
-        } else if (!exact && ATZ_VISITED_CHECK && z.chain <= 8) {
+        } else if (!exact && ATZ_VISITED_CHECK && z.chain <= ATZ_VISITED_MAX) {
           // the walk spent its budget and a hole shares the slot: the entry is still exact when
           // every node the walk visited (the bucket entries below x down to the lowest visited
           // one, at most `chain` of them) was inserted -- deflate_fast's chain then starts with
