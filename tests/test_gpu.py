@@ -137,6 +137,33 @@ def test_deflate_random_vs_oracle(ctx):
     assert not bad, bad[:10]
 
 
+def test_fast_levels_holes_vs_oracle(ctx):
+    """deflate_fast (levels 1-3) on repetitive text: long matches leave many positions uninserted
+    ("holes") and chains exhaust their budget, which exercises the hole-slot check, the visited-node
+    insertion check (levels 1-2) and the exact fallback walk against the oracle, every memLevel."""
+    r = random.Random(1234)
+    words = [bytes(r.choice(b"abcdefgh") for _ in range(r.randrange(2, 7))) for _ in range(r.choice([5, 12, 40]))]
+    buf = bytearray()
+    items = []
+    for k in range(216):
+        vocab = words[:r.choice([3, 5, len(words)])]
+        n = r.randrange(200, 40000)
+        d = bytearray()
+        while len(d) < n:
+            d += r.choice(vocab) + (b" " if r.random() < 0.8 else b"\n")
+        d = bytes(d[:n])
+        items.append((len(buf), len(d), 1 + k % 3, 15 if k % 4 else r.randrange(9, 15), 1 + (k // 3) % 9))
+        buf += d
+    outs = ctx.deflate_batch(bytes(buf), items)
+    bad = []
+    for it, o in zip(items, outs):
+        want, _ = _libs.ora_deflate(bytes(buf[it[0]:it[0] + it[1]]), it[2], it[3], it[4])
+        if o != want:
+            first = next((i for i in range(min(len(o), len(want))) if o[i] != want[i]), min(len(o), len(want)))
+            bad.append((it[1:], len(o), len(want), first))
+    assert not bad, bad[:10]
+
+
 def test_zt_kat_precompress(atz):
     data, meta = G.zt_kat()
     with atz.Context() as c:
