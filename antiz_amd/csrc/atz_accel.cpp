@@ -390,7 +390,7 @@ static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, con
     HIPCHK(hipMemsetAsync(c->d_arena_used.p, 0, 8, c->st));
   }
   uint32_t n = (uint32_t)jobs.size();
-  // The 8 KiB-ring decoder needs an HBM copy of its output for matches beyond the ring: every job
+  // The small-ring decoder needs an HBM copy of its output for matches beyond the ring: every job
   // writes to a destination or an arena slot.  Jobs without output use the 32 KiB ring.
   bool small = !full_ring;
   for (const InfJob& jb : jobs) small = small && jb.out_off != NO_OUT;
@@ -645,7 +645,7 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       else add_file(ch.co + cd.i, ch.len - cd.i);
       add_byte(nx.b0);
       add_file(nx.co + 1, nx.len - 1);
-      // output into arena slots after the scan's (8 KiB-ring decoder); the bytes are not used
+      // output into arena slots after the scan's (small-ring decoder); the bytes are not used
       jb.in_len = out - jb.in_off; jb.out_off = ARENA_OUT; jb.out_cap = ARENA_SLOT;
       cj.push_back(jb);
       cj_chunk.push_back(j);
@@ -1900,7 +1900,7 @@ int atz_inflate_batch(atz_ctx_t* c, const uint8_t* buf, uint64_t len, const uint
   std::vector<InfJob> jobs(n);
   for (uint64_t k = 0; k < n; k++) {
     if (offs[k] + lens[k] > len) return ATZ_E_ARG;
-    // the scan's configuration: output into arena slots (8 KiB-ring decoder, 32 KiB-ring reruns)
+    // the scan's configuration: output into arena slots (small-ring decoder, 32 KiB-ring reruns)
     jobs[k].in_off = offs[k]; jobs[k].in_len = lens[k]; jobs[k].out_off = ARENA_OUT; jobs[k].out_cap = ARENA_SLOT;
   }
   std::vector<InfRes> res;

@@ -23,11 +23,13 @@ namespace atz {
 // the host runs it again with the 32 KiB ring.
 static constexpr uint32_t INF_RING_FULL = 32768;
 #ifndef INF_RING_SMALL_BYTES
-#define INF_RING_SMALL_BYTES 8192
+#define INF_RING_SMALL_BYTES 4096   // C4 k_inflate (A/B): 8 KiB x 4 waves 137 ms, 4 KiB x 5 126 ms, x 6 121 ms, x 8 127 ms
 #endif
 static constexpr uint32_t INF_RING_SMALL = INF_RING_SMALL_BYTES;
+static_assert(INF_RING_SMALL >= 4096 && (INF_RING_SMALL & (INF_RING_SMALL - 1)) == 0,
+              "small ring: power of two >= 4 KiB (a 2 KiB ring stalls the decoder)");
 #ifndef INF_SMALL_WAVES
-#define INF_SMALL_WAVES 4   // waves per SIMD the small-ring decoder is register-bounded for (C4 k_inflate: 3 -> 183 ms, 4 -> 154 ms)
+#define INF_SMALL_WAVES 6   // waves per SIMD the small-ring decoder is register-bounded for (8 KiB ring: 3 -> 183 ms, 4 -> 154 ms)
 #endif
 #ifndef ATZ_INF_CLOCKS
 #define ATZ_INF_CLOCKS 0                       // 1: per-job clocks and symbol counts in InfRes
