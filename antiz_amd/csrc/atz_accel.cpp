@@ -1015,7 +1015,7 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
     if (!cnt[k]) continue;
     kbeg(c, 4);
     if (k < NC)
-      hipLaunchKernelGGL(k_match_lds, dim3((uint32_t)cnt[k]), dim3(256), (uint32_t)(3 * cls[gmax[k]] + 64), c->st,
+      hipLaunchKernelGGL(k_match_lds, dim3((uint32_t)cnt[k]), dim3(MATCH_THREADS), (uint32_t)(3 * cls[gmax[k]] + 64), c->st,
                          x->d_infl.as<uint8_t>(), c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(),
                          c->d_mjobs.as<MatchJob>() + beg[k]);
     else

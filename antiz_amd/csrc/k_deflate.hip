@@ -500,7 +500,11 @@ __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl,
 // from the bucket arrays with all loads in flight at once.  A walk is then a chain of LDS reads
 // instead of dependent HBM round trips.  Host-side size classes keep positions < 32 Ki (16-bit).
 static constexpr uint32_t PREV_NIL = 0xffffu;
-__global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ infl, const uint32_t* __restrict__ chains,
+#ifndef ATZ_MATCH_THREADS
+#define ATZ_MATCH_THREADS 1024  // threads per k_match_lds block, all sharing the staged stream (C4: 256 ~913, 512 ~974, 1024 ~986 MB/s)
+#endif
+static constexpr uint32_t MATCH_THREADS = ATZ_MATCH_THREADS;
+__global__ __launch_bounds__(MATCH_THREADS) void k_match_lds(const uint8_t* __restrict__ infl, const uint32_t* __restrict__ chains,
                                                   uint2* __restrict__ R, const MatchJob* __restrict__ jobs) {
   extern __shared__ uint32_t dyn_lds[];
   const MatchJob jb = jobs[blockIdx.x];
@@ -513,17 +517,17 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ i
   const uint32_t nw = (uint32_t)(((want < n ? want : n) + 3) >> 2);
   LDS uint32_t* l32 = (LDS uint32_t*)dyn_lds;
   LDS uint16_t* prv = (LDS uint16_t*)(l32 + nw + 8);
-  for (uint32_t w = threadIdx.x; w < nw + 8; w += 256) l32[w] = w < nw ? g32[w] : 0u;
+  for (uint32_t w = threadIdx.x; w < nw + 8; w += MATCH_THREADS) l32[w] = w < nw ? g32[w] : 0u;
   const uint32_t nh = n >= 3 ? n - 2 : 0;
   const uint32_t P = (uint32_t)jb.p1 < nh ? (uint32_t)jb.p1 : nh;   // candidates and walk starts are < P
   if (4 * P >= nh) {
     // most positions wanted: one coalesced pass over the bucket array (entry i's predecessor is
     // entry i - 1 unless i opens its bucket), scattered into LDS -- no dependent gathers
-    for (uint32_t i0 = 0; i0 < nh; i0 += 2048) {
+    for (uint32_t i0 = 0; i0 < nh; i0 += 8 * MATCH_THREADS) {
       uint32_t a[8], b[8];
 #pragma unroll
       for (int u = 0; u < 8; u++) {
-        const uint32_t i = i0 + 256 * u + threadIdx.x;
+        const uint32_t i = i0 + MATCH_THREADS * u + threadIdx.x;
         a[u] = i < nh ? bpos[i] : BUCKET_FIRST | 0x7fffffffu;
         b[u] = (i < nh && i) ? bpos[i - 1] : 0u;
       }
@@ -534,15 +538,15 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ i
       }
     }
   } else {
-    for (uint32_t q0 = 0; q0 < P; q0 += 2048) {
+    for (uint32_t q0 = 0; q0 < P; q0 += 8 * MATCH_THREADS) {
       uint32_t ix[8], a[8], b[8];
 #pragma unroll
-      for (int u = 0; u < 8; u++) { const uint32_t q = q0 + 256 * u + threadIdx.x; ix[u] = q < P ? sidx[q] : 1u; }
+      for (int u = 0; u < 8; u++) { const uint32_t q = q0 + MATCH_THREADS * u + threadIdx.x; ix[u] = q < P ? sidx[q] : 1u; }
 #pragma unroll
       for (int u = 0; u < 8; u++) { a[u] = bpos[ix[u]]; b[u] = ix[u] ? bpos[ix[u] - 1] : 0u; }
 #pragma unroll
       for (int u = 0; u < 8; u++) {
-        const uint32_t q = q0 + 256 * u + threadIdx.x;
+        const uint32_t q = q0 + MATCH_THREADS * u + threadIdx.x;
         if (q < P) prv[q] = (a[u] & BUCKET_FIRST) ? (uint16_t)PREV_NIL : (uint16_t)(b[u] & ~BUCKET_FIRST);
       }
     }
@@ -554,7 +558,7 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ i
   const uint32_t B = c_cfg[jb.level][3], nice = c_cfg[jb.level][2], Bq = B >> 2;
   const uint32_t maxdist = (1u << jb.window) - 262;
   const uint32_t hbits = jb.memlevel + 7u, hmask = (1u << hbits) - 1u, hshift = (hbits + 2u) / 3u;
-  for (uint32_t p = (uint32_t)jb.p0 + threadIdx.x; p < (uint32_t)jb.p1; p += 256) {
+  for (uint32_t p = (uint32_t)jb.p0 + threadIdx.x; p < (uint32_t)jb.p1; p += MATCH_THREADS) {
     uint32_t bf = 2, df = 0, bq = 2, dq = 0, valid = 0, slot = 0, budget_out = 0;
     uint32_t reach = p;
     const uint32_t s0 = byte(p);
