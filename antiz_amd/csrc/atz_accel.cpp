@@ -1452,11 +1452,13 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
   }
   return 0;
 }
-static size_t sweep_pipes() {   // ATZ_PIPES=k (1..8), default 2 (measured on C4: 1 390, 2 417, 4 367 MB/s)
+// ATZ_PIPES=k (1..8), default 3.  C4 A/B after the 1024-thread match blocks (interleaved, 4 runs each):
+// 2 pipes ~988, 3 ~1022, 4 ~854 MB/s (earlier, with slower match walks, 2 was best)
+static size_t sweep_pipes() {
   static size_t v = 0;
   if (!v) {
     const char* e = std::getenv("ATZ_PIPES");
-    v = e ? (size_t)std::max(1, std::min(8, std::atoi(e))) : 2;
+    v = e ? (size_t)std::max(1, std::min(8, std::atoi(e))) : 3;
   }
   return v;
 }
