@@ -26,6 +26,8 @@
 #include <cstring>
 #include <string>
 #include <memory>
+#include <new>
+#include <stdexcept>
 #include <thread>
 #include <functional>
 #include <vector>
@@ -294,8 +296,12 @@ struct atz_ctx {
   std::vector<Rec> recs;
   std::vector<uint64_t> infl_off;   // per record offset in d_infl
   std::vector<uint32_t> adler;
-  const uint8_t* hfile = nullptr;
+  const uint8_t* hfile = nullptr;   // caller's host copy; valid only inside the call that set it
   uint64_t flen = 0;
+  // atz_scan -> atz_sweep hand-off: set by a successful atz_scan, cleared by every call that
+  // replaces recs / d_file (precompress, deflate, reconstruct, inflate_batch)
+  bool scan_valid = false;
+  std::vector<uint32_t> scan_trailer;   // per record: the stream's Adler-32 trailer (big-endian word)
   bool file_on_device = false;      // d_file holds the current file
   const uint8_t* dev_file = nullptr;
   atz_stats_t stats{};
@@ -779,10 +785,12 @@ static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F) {
   }
   c->stats.n_reinflated = jobs.size();
   for (size_t s = 0; s < n; s++) {
-    // Adler-32 of the inflated bytes = the verified trailer
+    // Adler-32 of the inflated bytes = the verified trailer (atz_sweep: saved by atz_scan, whose
+    // host buffer the caller need not keep alive)
     const uint64_t e = c->recs[s].offset + c->recs[s].comp_len;
-    c->adler[s] = ((uint32_t)c->hfile[e - 4] << 24) | ((uint32_t)c->hfile[e - 3] << 16) |
-                  ((uint32_t)c->hfile[e - 2] << 8) | c->hfile[e - 1];
+    c->adler[s] = c->hfile ? ((uint32_t)c->hfile[e - 4] << 24) | ((uint32_t)c->hfile[e - 3] << 16) |
+                                 ((uint32_t)c->hfile[e - 2] << 8) | c->hfile[e - 1]
+                           : c->scan_trailer[s];
   }
   HIPCHK(hipStreamSynchronize(c->st));
   kcollect(c);
@@ -795,6 +803,18 @@ static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F) {
 // sweep (8 bytes per position).  When a round would push the cache past its cap the cache is
 // dropped and the round's tables are rebuilt.
 static constexpr uint64_t CHAIN_CACHE_CAP = 48ull << 30;
+// ATZ_BUCKET_SORT=0: the older in-order bucket kernels for every job (A/B)
+static bool bucket_sort_on() {
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_BUCKET_SORT"); v = e ? std::atoi(e) : 1; }
+  return v != 0;
+}
+static bool bucket_verify() {   // ATZ_BUCKETS_VERIFY=1 (read per call): check k_buckets_sort against the others
+  const char* e = std::getenv("ATZ_BUCKETS_VERIFY");
+  return e && std::atoi(e) != 0;
+}
+static constexpr uint32_t BSORT_MAX_NPAD = ((160u * 1024u - BSORT_CNT_BYTES) / 6u) & ~63u;   // LDS limit
+static_assert(bsort_lds_bytes(BSORT_MAX_NPAD) <= 160u * 1024u && BSORT_MAX_NPAD < 65536u, "k_buckets_sort LDS class");
 // prefetch builds finished: fold their kernel times into the pipe's counters
 static int chains_prefetch_collect(Pipe* c) {
   if (!c->pev_pending) return 0;
@@ -826,6 +846,117 @@ static int chains_prefetch(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint
   c->pev_pending = true;
   return 0;
 }
+// The kernels of one set of bucket jobs, writing at chains + job.chain_off.
+static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<ChainJob> jobs, uint32_t* chains,
+                             bool use_sort) {
+  // streams whose sort fits in LDS: k_buckets_sort (every memLevel), one launch per size class
+  if (use_sort) {
+    static const uint32_t cls[] = {4096, 8192, 12288, 16384, 20480, BSORT_MAX_NPAD};
+    constexpr int NC = 6;
+    std::vector<ChainJob> byc[NC], rest;
+    for (const ChainJob& jb : jobs) {
+      const uint64_t npad = (jb.n + 63) & ~63ull;
+      int k = 0;
+      while (k < NC && npad > cls[k]) k++;
+      (k < NC ? byc[k] : rest).push_back(jb);
+    }
+    std::vector<ChainJob> all;
+    size_t beg[NC + 1] = {};
+    for (int k = 0; k < NC; k++) { beg[k] = all.size(); all.insert(all.end(), byc[k].begin(), byc[k].end()); }
+    beg[NC] = all.size();
+    if (!all.empty()) {
+      if (int r = upload(c, B.d_cjobs2, all.data(), all.size() * sizeof(ChainJob))) return r;
+      for (int k = 0; k < NC; k++) {
+        const size_t cnt = beg[k + 1] - beg[k];
+        if (!cnt) continue;
+        kbeg(c, 2);
+        hipLaunchKernelGGL(k_buckets_sort, dim3((uint32_t)cnt), dim3(BSORT_THREADS), bsort_lds_bytes(cls[k]), c->st,
+                           x->d_infl.as<uint8_t>(), B.d_cjobs2.as<ChainJob>() + beg[k], chains,
+                           (uint32_t)cnt);
+        kend(c);
+        KCHECK("k_buckets_sort");
+      }
+    }
+    for (const ChainJob& jb : all) c->stats.k_chains_alg_bytes += 9 * jb.n;
+    jobs.swap(rest);
+    if (jobs.empty()) return 0;
+  }
+  // hash tables of memLevel <= 8 and streams < 64 Ki positions: LDS kernels; memLevel 9: HBM scratch
+  static int pk8 = -1;   // ATZ_PK8=1: memLevel 8 on packed 16-bit counters (2 blocks per CU; measured
+                         // 838 vs 852 MB/s on C4: its builds are faster but slow the concurrent trials)
+  if (pk8 < 0) { const char* e = std::getenv("ATZ_PK8"); pk8 = e ? std::atoi(e) : 0; }
+  std::vector<ChainJob> tiny, small, mid, big, eight;
+  for (const ChainJob& jb : jobs) {
+    const uint32_t hs = 1u << (jb.memlevel + 7);
+    if (pk8 && hs == 32768 && jb.n < 65536) { eight.push_back(jb); continue; }
+    (jb.n >= 65536 || hs > 32768 ? big : hs <= 4096 ? tiny : hs <= 16384 ? small : mid).push_back(jb);
+  }
+  {
+    std::vector<ChainJob> all(tiny);
+    all.insert(all.end(), small.begin(), small.end());
+    all.insert(all.end(), mid.begin(), mid.end());
+    if (!all.empty()) {
+      if (int r = upload(c, B.d_cjobs2, all.data(), all.size() * sizeof(ChainJob))) return r;
+      const ChainJob* dj = B.d_cjobs2.as<ChainJob>();
+      auto launch = [&](auto kern, size_t off, size_t cnt, const char* nm) -> int {
+        if (!cnt) return 0;
+        kbeg(c, 2);
+        hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(), dj + off,
+                           chains, (uint32_t)cnt);
+        kend(c);
+        KCHECK(nm);
+        return 0;
+      };
+      if (int r = launch(k_buckets_lds<4096>, 0, tiny.size(), "k_buckets_lds<4096>")) return r;
+      if (int r = launch(k_buckets_lds<16384>, tiny.size(), small.size(), "k_buckets_lds<16384>")) return r;
+      if (int r = launch(k_buckets_lds<32768>, tiny.size() + small.size(), mid.size(), "k_buckets_lds<32768>")) return r;
+    }
+  }
+  std::vector<ChainJob> nine, rest;   // memLevel 9 with n < 64 Ki: packed LDS counters + HBM bases
+  for (const ChainJob& jb : big) ((jb.memlevel == 9 && jb.n < 65536) ? nine : rest).push_back(jb);
+  big.swap(rest);
+  if (!nine.empty() || !eight.empty()) {   // packed counters: memLevel 8 first, then 9
+    const size_t nbs = 4096;   // HBM scratch slots for the bucket bases, reused in launch order
+    if (int r = B.d_heads2.reserve(nbs * 65536 * 4)) return r;
+    std::vector<ChainJob> pk(eight);
+    pk.insert(pk.end(), nine.begin(), nine.end());
+    for (size_t k = 0; k < pk.size(); k++) pk[k].slot = (uint32_t)(k % nbs);
+    if (int r = upload(c, B.d_cjobs3, pk.data(), pk.size() * sizeof(ChainJob))) return r;
+    for (size_t b0 = 0; b0 < pk.size();) {
+      const bool is8 = b0 < eight.size();
+      const size_t end = is8 ? eight.size() : pk.size();
+      const size_t nb = std::min(nbs - b0 % nbs, end - b0);   // a launch never holds two jobs of one slot
+      kbeg(c, 2);
+      if (is8)
+        hipLaunchKernelGGL(k_buckets_pk<15>, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
+                           B.d_cjobs3.as<ChainJob>() + b0, chains, B.d_heads2.as<uint32_t>(),
+                           (uint32_t)nb);
+      else
+        hipLaunchKernelGGL(k_buckets_pk<16>, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
+                           B.d_cjobs3.as<ChainJob>() + b0, chains, B.d_heads2.as<uint32_t>(),
+                           (uint32_t)nb);
+      kend(c);
+      KCHECK("k_buckets_pk");
+      b0 += nb;
+    }
+  }
+  const size_t batch = 4096;   // scratch: 65536 x 8-byte words per job slot
+  if (!big.empty() && (int)B.d_heads.reserve(batch * 65536 * 8)) return ATZ_E_NOMEM;
+  for (size_t k = 0; k < big.size(); k++) big[k].slot = (uint32_t)(k % batch);
+  if (int r = upload(c, B.d_cjobs, big.data(), big.size() * sizeof(ChainJob))) return r;
+  for (size_t b0 = 0; b0 < big.size(); b0 += batch) {   // launches on one stream reuse the slots in order
+    size_t nb = std::min(batch, big.size() - b0);
+    kbeg(c, 2);
+    hipLaunchKernelGGL(k_buckets, dim3((uint32_t)nb), dim3(64), 0, c->st, x->d_infl.as<uint8_t>(),
+                       B.d_cjobs.as<ChainJob>() + b0, chains, B.d_heads.as<uint64_t>(),
+                       (uint32_t)nb);
+    kend(c);
+    KCHECK("k_buckets");
+  }
+  for (const ChainJob& jb : jobs) c->stats.k_chains_alg_bytes += 9 * jb.n;  // read I_s, write 8*I_s
+  return 0;
+}
+
 static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need, ChainBufs& B,
                             bool prefetch) {
   auto words = [&](uint32_t s) { return 2 * ((x->recs[s].infl_len + 63) & ~63ull); };
@@ -870,79 +1001,33 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     c->d_chains.p = np;
     c->d_chains.n = cap;
   }
-  // hash tables of memLevel <= 8 and streams < 64 Ki positions: LDS kernels; memLevel 9: HBM scratch
-  static int pk8 = -1;   // ATZ_PK8=1: memLevel 8 on packed 16-bit counters (2 blocks per CU; measured
-                         // 838 vs 852 MB/s on C4: its builds are faster but slow the concurrent trials)
-  if (pk8 < 0) { const char* e = std::getenv("ATZ_PK8"); pk8 = e ? std::atoi(e) : 0; }
-  std::vector<ChainJob> tiny, small, mid, big, eight;
-  for (const ChainJob& jb : jobs) {
-    const uint32_t hs = 1u << (jb.memlevel + 7);
-    if (pk8 && hs == 32768 && jb.n < 65536) { eight.push_back(jb); continue; }
-    (jb.n >= 65536 || hs > 32768 ? big : hs <= 4096 ? tiny : hs <= 16384 ? small : mid).push_back(jb);
-  }
-  {
-    std::vector<ChainJob> all(tiny);
-    all.insert(all.end(), small.begin(), small.end());
-    all.insert(all.end(), mid.begin(), mid.end());
-    if (!all.empty()) {
-      if (int r = upload(c, B.d_cjobs2, all.data(), all.size() * sizeof(ChainJob))) return r;
-      const ChainJob* dj = B.d_cjobs2.as<ChainJob>();
-      auto launch = [&](auto kern, size_t off, size_t cnt, const char* nm) -> int {
-        if (!cnt) return 0;
-        kbeg(c, 2);
-        hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(), dj + off,
-                           c->d_chains.as<uint32_t>(), (uint32_t)cnt);
-        kend(c);
-        KCHECK(nm);
-        return 0;
-      };
-      if (int r = launch(k_buckets_lds<4096>, 0, tiny.size(), "k_buckets_lds<4096>")) return r;
-      if (int r = launch(k_buckets_lds<16384>, tiny.size(), small.size(), "k_buckets_lds<16384>")) return r;
-      if (int r = launch(k_buckets_lds<32768>, tiny.size() + small.size(), mid.size(), "k_buckets_lds<32768>")) return r;
+  if (int r = build_bucket_jobs(x, c, B, jobs, c->d_chains.as<uint32_t>(), bucket_sort_on())) return r;
+  if (bucket_verify() && bucket_sort_on()) {
+    // diagnostics (ATZ_BUCKETS_VERIFY=1): the same jobs again on the in-order kernels, compared
+    uint64_t tot = 0;
+    std::vector<ChainJob> alt(jobs);
+    for (ChainJob& jb : alt) { jb.chain_off = tot; tot += 2 * ((jb.n + 63) & ~63ull); }
+    DBuf tmp;
+    if (int r = tmp.reserve(tot * 4 + 4096)) return r;
+    if (int r = build_bucket_jobs(x, c, B, alt, tmp.as<uint32_t>(), false)) return r;
+    std::vector<uint32_t> h1(tot), h2(tot);
+    for (size_t k = 0; k < jobs.size(); k++)
+      HIPCHK(hipMemcpyAsync(h1.data() + alt[k].chain_off, c->d_chains.as<uint32_t>() + jobs[k].chain_off,
+                            8 * ((jobs[k].n + 63) & ~63ull), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(h2.data(), tmp.p, tot * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    for (size_t k = 0; k < jobs.size(); k++) {
+      const uint64_t npad = (alt[k].n + 63) & ~63ull, nh = alt[k].n >= 3 ? alt[k].n - 2 : 0;
+      const uint32_t* a = h1.data() + alt[k].chain_off;
+      const uint32_t* b2 = h2.data() + alt[k].chain_off;
+      for (uint64_t i = 0; i < nh; i++)
+        if (a[i] != b2[i] || a[npad + i] != b2[npad + i]) {
+          std::fprintf(stderr, "atz: bucket mismatch: job %zu n %llu m %u at %llu\n", k, (unsigned long long)alt[k].n,
+                       alt[k].memlevel, (unsigned long long)i);
+          return ATZ_E_INTERNAL;
+        }
     }
   }
-  std::vector<ChainJob> nine, rest;   // memLevel 9 with n < 64 Ki: packed LDS counters + HBM bases
-  for (const ChainJob& jb : big) ((jb.memlevel == 9 && jb.n < 65536) ? nine : rest).push_back(jb);
-  big.swap(rest);
-  if (!nine.empty() || !eight.empty()) {   // packed counters: memLevel 8 first, then 9
-    const size_t nbs = 4096;   // HBM scratch slots for the bucket bases, reused in launch order
-    if (int r = B.d_heads2.reserve(nbs * 65536 * 4)) return r;
-    std::vector<ChainJob> pk(eight);
-    pk.insert(pk.end(), nine.begin(), nine.end());
-    for (size_t k = 0; k < pk.size(); k++) pk[k].slot = (uint32_t)(k % nbs);
-    if (int r = upload(c, B.d_cjobs3, pk.data(), pk.size() * sizeof(ChainJob))) return r;
-    for (size_t b0 = 0; b0 < pk.size();) {
-      const bool is8 = b0 < eight.size();
-      const size_t end = is8 ? eight.size() : pk.size();
-      const size_t nb = std::min(nbs - b0 % nbs, end - b0);   // a launch never holds two jobs of one slot
-      kbeg(c, 2);
-      if (is8)
-        hipLaunchKernelGGL(k_buckets_pk<15>, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
-                           B.d_cjobs3.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), B.d_heads2.as<uint32_t>(),
-                           (uint32_t)nb);
-      else
-        hipLaunchKernelGGL(k_buckets_pk<16>, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
-                           B.d_cjobs3.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), B.d_heads2.as<uint32_t>(),
-                           (uint32_t)nb);
-      kend(c);
-      KCHECK("k_buckets_pk");
-      b0 += nb;
-    }
-  }
-  const size_t batch = 4096;   // scratch: 65536 x 8-byte words per job slot
-  if (!big.empty() && (int)B.d_heads.reserve(batch * 65536 * 8)) return ATZ_E_NOMEM;
-  for (size_t k = 0; k < big.size(); k++) big[k].slot = (uint32_t)(k % batch);
-  if (int r = upload(c, B.d_cjobs, big.data(), big.size() * sizeof(ChainJob))) return r;
-  for (size_t b0 = 0; b0 < big.size(); b0 += batch) {   // launches on one stream reuse the slots in order
-    size_t nb = std::min(batch, big.size() - b0);
-    kbeg(c, 2);
-    hipLaunchKernelGGL(k_buckets, dim3((uint32_t)nb), dim3(64), 0, c->st, x->d_infl.as<uint8_t>(),
-                       B.d_cjobs.as<ChainJob>() + b0, c->d_chains.as<uint32_t>(), B.d_heads.as<uint64_t>(),
-                       (uint32_t)nb);
-    kend(c);
-    KCHECK("k_buckets");
-  }
-  for (const ChainJob& jb : jobs) c->stats.k_chains_alg_bytes += 9 * jb.n;  // read I_s, write 8*I_s
   return 0;
 }
 
@@ -1628,8 +1713,10 @@ static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::
 static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, uint64_t F, uint64_t* atz_len,
                            std::vector<StreamState>* ss_out) {
   auto t0 = std::chrono::steady_clock::now();
+  c->scan_valid = false;
   c->stats = atz_stats_t{};
   c->hfile = h; c->flen = F;
+  struct Drop { atz_ctx* c; ~Drop() { c->hfile = nullptr; } } drop{c};   // h is the caller's, valid for this call only
   c->stats.file_bytes = F;
   if (int r = scan_impl(c, h, d_file, F)) return r;
   auto t1 = std::chrono::steady_clock::now();
@@ -1650,6 +1737,7 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
 // one-shot deflates (reconstruct / atz_deflate): trials with mode "full output" on a temporary stream set
 static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, uint64_t>>& ins,
                         const std::vector<uint32_t>& params, std::vector<std::vector<uint8_t>>& outs) {
+  c->scan_valid = false;   // recs / infl_off / adler / chain_off are replaced below
   const size_t n = ins.size();
   outs.assign(n, {});
   if (!n) return 0;
@@ -1723,6 +1811,21 @@ static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, 
 }
 
 // ---------------------------------------------------------------------------------------------
+// No C++ exception crosses the C ABI (std::vector growth, new): allocation failures become
+// ATZ_E_NOMEM, anything else ATZ_E_INTERNAL.
+template <class F>
+static int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return ATZ_E_NOMEM;
+  } catch (const std::length_error&) {
+    return ATZ_E_NOMEM;
+  } catch (...) {
+    return ATZ_E_INTERNAL;
+  }
+}
+
 extern "C" {
 
 void atz_default_opts(atz_opts_t* o) {
@@ -1747,245 +1850,305 @@ const char* atz_strerror(int e) {
 void atz_free(void* p) { std::free(p); }
 
 int atz_open(atz_ctx_t** ctx, const atz_opts_t* opts) {
-  if (!ctx) return ATZ_E_ARG;
-  *ctx = nullptr;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ATZ_E_NODEV;
-  atz_ctx* c = new atz_ctx();
-  if (opts) c->o = *opts; else atz_default_opts(&c->o);
-  c->dev = c->o.device >= 0 ? c->o.device : 0;
-  if (c->o.device >= 0 && hipSetDevice(c->dev) != hipSuccess) { delete c; return ATZ_E_NODEV; }
-  if (c->o.device < 0) hipGetDevice(&c->dev);
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, c->dev) != hipSuccess) { delete c; return ATZ_E_NODEV; }
-  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
-    std::fprintf(stderr, "atz: device %d is %s, kernels are built for gfx950\n", c->dev, prop.gcnArchName);
-    delete c;
-    return ATZ_E_NODEV;
-  }
-  if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { delete c; return ATZ_E_HIP; }
-  DeflTables T;
-  make_tables(T);
-  if (atz_upload_defl_tables(&T) != hipSuccess) { delete c; return ATZ_E_NODEV; }
-  *ctx = c;
-  return ATZ_OK;
+  return guarded([&]() -> int {
+    if (!ctx) return ATZ_E_ARG;
+    *ctx = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ATZ_E_NODEV;
+    atz_ctx* c = new atz_ctx();
+    if (opts) c->o = *opts; else atz_default_opts(&c->o);
+    c->dev = c->o.device >= 0 ? c->o.device : 0;
+    if (c->o.device >= 0 && hipSetDevice(c->dev) != hipSuccess) { delete c; return ATZ_E_NODEV; }
+    if (c->o.device < 0) hipGetDevice(&c->dev);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->dev) != hipSuccess) { delete c; return ATZ_E_NODEV; }
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+      std::fprintf(stderr, "atz: device %d is %s, kernels are built for gfx950\n", c->dev, prop.gcnArchName);
+      delete c;
+      return ATZ_E_NODEV;
+    }
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { delete c; return ATZ_E_HIP; }
+    DeflTables T;
+    make_tables(T);
+    if (atz_upload_defl_tables(&T) != hipSuccess) { delete c; return ATZ_E_NODEV; }
+    *ctx = c;
+    return ATZ_OK;
+  });
 }
 
 void atz_close(atz_ctx_t* c) {
   if (!c) return;
-  hipStreamSynchronize(c->st);
-  hipStreamDestroy(c->st);
-  delete c;   // every DBuf member frees its device memory
+  try {
+    hipStreamSynchronize(c->st);
+    hipStreamDestroy(c->st);
+    delete c;   // every DBuf member frees its device memory
+  } catch (...) {
+  }
 }
 
 int atz_scan(atz_ctx_t* c, const uint8_t* file, uint64_t len, atz_cand_t** out, uint64_t* n) {
-  (void)hipGetLastError();
-  if (!c || (!file && len) || !out || !n) return ATZ_E_ARG;
-  if (int r = upload(c, c->d_file, file, len)) return r;
-  c->hfile = file; c->flen = len;
-  c->stats = atz_stats_t{};
-  if (int r = scan_impl(c, file, c->d_file.as<uint8_t>(), len)) return r;
-  *n = c->recs.size();
-  *out = (atz_cand_t*)std::malloc((c->recs.size() + 1) * sizeof(atz_cand_t));
-  for (size_t s = 0; s < c->recs.size(); s++) {
-    (*out)[s].offset = c->recs[s].offset; (*out)[s].comp_len = c->recs[s].comp_len;
-    (*out)[s].infl_len = c->recs[s].infl_len; (*out)[s].type = c->recs[s].type; (*out)[s].flags = c->recs[s].flags;
-  }
-  return ATZ_OK;
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || (!file && len) || !out || !n) return ATZ_E_ARG;
+    c->scan_valid = false;
+    if (int r = upload(c, c->d_file, file, len)) return r;
+    c->hfile = file; c->flen = len;
+    c->stats = atz_stats_t{};
+    const int rs = scan_impl(c, file, c->d_file.as<uint8_t>(), len);
+    c->hfile = nullptr;   // the caller's buffer is not used after this call returns
+    if (rs) return rs;
+    // atz_sweep needs each stream's Adler-32 trailer: keep it, so `file` may be freed in between
+    c->scan_trailer.assign(c->recs.size(), 0);
+    for (size_t s = 0; s < c->recs.size(); s++) {
+      const Rec& r = c->recs[s];
+      if (r.comp_len < 4 || r.offset + r.comp_len > len) continue;   // atz_sweep reports ATZ_E_REF_UB
+      const uint8_t* e = file + r.offset + r.comp_len;
+      c->scan_trailer[s] = ((uint32_t)e[-4] << 24) | ((uint32_t)e[-3] << 16) | ((uint32_t)e[-2] << 8) | e[-1];
+    }
+    *n = c->recs.size();
+    *out = (atz_cand_t*)std::malloc((c->recs.size() + 1) * sizeof(atz_cand_t));
+    if (!*out) return ATZ_E_NOMEM;
+    for (size_t s = 0; s < c->recs.size(); s++) {
+      (*out)[s].offset = c->recs[s].offset; (*out)[s].comp_len = c->recs[s].comp_len;
+      (*out)[s].infl_len = c->recs[s].infl_len; (*out)[s].type = c->recs[s].type; (*out)[s].flags = c->recs[s].flags;
+    }
+    c->scan_valid = true;
+    return ATZ_OK;
+  });
 }
 
 int atz_sweep(atz_ctx_t* c, const atz_cand_t* cands, uint64_t n, atz_result_t* res, uint64_t** diff_off,
               uint8_t** diff_val, uint64_t* n_diffs) {
-  (void)hipGetLastError();
-  if (!c || !res || n != c->recs.size()) return ATZ_E_ARG;
-  (void)cands;
-  if (int r = inflate_records(c, c->d_file.as<uint8_t>(), c->flen)) return r;
-  std::vector<StreamState> ss;
-  if (int r = sweep_impl(c, c->d_file.as<uint8_t>(), ss)) return r;
-  uint64_t nd = 0;
-  for (auto& s : ss) if (s.recomp) nd += s.rawdiff.size();
-  uint64_t* dof = (uint64_t*)std::malloc((nd + 1) * 8);
-  uint8_t* dva = (uint8_t*)std::malloc(nd + 1);
-  uint64_t k = 0;
-  for (size_t s = 0; s < n; s++) {
-    const StreamState& st = ss[s];
-    atz_result_t& r = res[s];
-    r.clevel = st.c; r.window = st.w; r.memlevel = st.m; r.recomp = st.recomp;
-    r.n_trials = st.trials; r.ident = st.ident; r.first_diff = st.first_diff;
-    r.diff_index = k;
-    r.n_diff = st.recomp ? st.rawdiff.size() : 0;
-    if (st.recomp)
-      for (size_t q = 0; q < st.rawdiff.size(); q++, k++) {
-        dof[k] = q == 0 ? 0 : (uint64_t)st.rawdiff[q] - st.rawdiff[q - 1];
-        dva[k] = st.diffval[q];
-      }
-  }
-  *diff_off = dof; *diff_val = dva; *n_diffs = nd;
-  return ATZ_OK;
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    // only on the records of this context's last atz_scan (nothing in between replaced them)
+    if (!c || !res || !c->scan_valid || n != c->recs.size()) return ATZ_E_ARG;
+    (void)cands;
+    c->scan_valid = false;   // inflate_records / the sweep overwrite the scan's device state
+    c->hfile = nullptr;
+    if (int r = inflate_records(c, c->d_file.as<uint8_t>(), c->flen)) return r;
+    std::vector<StreamState> ss;
+    if (int r = sweep_impl(c, c->d_file.as<uint8_t>(), ss)) return r;
+    uint64_t nd = 0;
+    for (auto& s : ss) if (s.recomp) nd += s.rawdiff.size();
+    uint64_t* dof = (uint64_t*)std::malloc((nd + 1) * 8);
+    uint8_t* dva = (uint8_t*)std::malloc(nd + 1);
+    uint64_t k = 0;
+    for (size_t s = 0; s < n; s++) {
+      const StreamState& st = ss[s];
+      atz_result_t& r = res[s];
+      r.clevel = st.c; r.window = st.w; r.memlevel = st.m; r.recomp = st.recomp;
+      r.n_trials = st.trials; r.ident = st.ident; r.first_diff = st.first_diff;
+      r.diff_index = k;
+      r.n_diff = st.recomp ? st.rawdiff.size() : 0;
+      if (st.recomp)
+        for (size_t q = 0; q < st.rawdiff.size(); q++, k++) {
+          dof[k] = q == 0 ? 0 : (uint64_t)st.rawdiff[q] - st.rawdiff[q - 1];
+          dva[k] = st.diffval[q];
+        }
+    }
+    *diff_off = dof; *diff_val = dva; *n_diffs = nd;
+    return ATZ_OK;
+  });
 }
 
 int atz_precompress(atz_ctx_t* c, const uint8_t* file, uint64_t len, uint8_t** atz, uint64_t* atz_len,
                     atz_stats_t* stats) {
-  (void)hipGetLastError();
-  if (!c || (!file && len) || !atz || !atz_len) return ATZ_E_ARG;
-  if (int r = upload(c, c->d_file, file, len)) return r;
-  uint64_t al = 0;
-  if (int r = precompress_dev(c, c->d_file.as<uint8_t>(), file, len, &al, nullptr)) return r;
-  uint8_t* h = (uint8_t*)std::malloc(al + 1);
-  if (!h) return ATZ_E_NOMEM;
-  HIPCHK(hipMemcpy(h, c->d_atz.p, al, hipMemcpyDeviceToHost));
-  *atz = h; *atz_len = al;
-  if (stats) *stats = c->stats;
-  return ATZ_OK;
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || (!file && len) || !atz || !atz_len) return ATZ_E_ARG;
+    if (int r = upload(c, c->d_file, file, len)) return r;
+    uint64_t al = 0;
+    if (int r = precompress_dev(c, c->d_file.as<uint8_t>(), file, len, &al, nullptr)) return r;
+    uint8_t* h = (uint8_t*)std::malloc(al + 1);
+    if (!h) return ATZ_E_NOMEM;
+    HIPCHK(hipMemcpy(h, c->d_atz.p, al, hipMemcpyDeviceToHost));
+    *atz = h; *atz_len = al;
+    if (stats) *stats = c->stats;
+    return ATZ_OK;
+  });
 }
 
 int atz_precompress_device(atz_ctx_t* c, const uint8_t* d_file, const uint8_t* h_file, uint64_t len,
                            const uint8_t** d_atz, uint64_t* atz_len, atz_stats_t* stats) {
-  (void)hipGetLastError();
-  if (!c || !d_file || !h_file || !d_atz || !atz_len) return ATZ_E_ARG;
-  uint64_t al = 0;
-  if (int r = precompress_dev(c, d_file, h_file, len, &al, nullptr)) return r;
-  *d_atz = c->d_atz.as<uint8_t>();
-  *atz_len = al;
-  if (stats) *stats = c->stats;
-  return ATZ_OK;
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || !d_file || !h_file || !d_atz || !atz_len) return ATZ_E_ARG;
+    uint64_t al = 0;
+    if (int r = precompress_dev(c, d_file, h_file, len, &al, nullptr)) return r;
+    *d_atz = c->d_atz.as<uint8_t>();
+    *atz_len = al;
+    if (stats) *stats = c->stats;
+    return ATZ_OK;
+  });
 }
 
 uint64_t atz_deflate_bound(uint64_t n, int window, int memlevel) { return bound(n, window, memlevel); }
 
 int atz_deflate(atz_ctx_t* c, const uint8_t* in, uint64_t in_len, int clevel, int window, int memlevel,
                 uint8_t* out, uint64_t out_cap, uint64_t* out_len) {
-  (void)hipGetLastError();
-  if (!c || (!in && in_len) || !out_len || clevel < 0 || clevel > 9 || window < 8 || window > 15 ||
-      memlevel < 1 || memlevel > 9)
-    return ATZ_E_ARG;
-  if (window == 8) window = 9;
-  std::vector<std::vector<uint8_t>> outs;
-  if (int r = deflate_many(c, {{in, in_len}}, {((uint32_t)clevel << 16) | ((uint32_t)window << 8) | (uint32_t)memlevel}, outs))
-    return r;
-  *out_len = outs[0].size();
-  if (outs[0].size() > out_cap) return ATZ_E_ARG;
-  if (out && !outs[0].empty()) std::memcpy(out, outs[0].data(), outs[0].size());
-  return ATZ_OK;
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || (!in && in_len) || !out_len || clevel < 0 || clevel > 9 || window < 8 || window > 15 ||
+        memlevel < 1 || memlevel > 9)
+      return ATZ_E_ARG;
+    if (window == 8) window = 9;
+    std::vector<std::vector<uint8_t>> outs;
+    if (int r = deflate_many(c, {{in, in_len}}, {((uint32_t)clevel << 16) | ((uint32_t)window << 8) | (uint32_t)memlevel}, outs))
+      return r;
+    *out_len = outs[0].size();
+    if (outs[0].size() > out_cap) return ATZ_E_ARG;
+    if (out && !outs[0].empty()) std::memcpy(out, outs[0].data(), outs[0].size());
+    return ATZ_OK;
+  });
 }
 
 int atz_deflate_batch(atz_ctx_t* c, const uint8_t* buf, uint64_t len, const uint64_t* offs, const uint64_t* lens,
                       const uint32_t* params, uint64_t n, uint8_t* out, const uint64_t* out_offs,
                       const uint64_t* out_caps, uint64_t* out_lens) {
-  (void)hipGetLastError();
-  if (!c || (!buf && len) || !out_lens) return ATZ_E_ARG;
-  std::vector<std::pair<const uint8_t*, uint64_t>> ins(n);
-  std::vector<uint32_t> ps(n);
-  for (uint64_t k = 0; k < n; k++) {
-    if (offs[k] + lens[k] > len) return ATZ_E_ARG;
-    int cl = (int)(params[k] >> 16), w = (int)((params[k] >> 8) & 0xff), m = (int)(params[k] & 0xff);
-    if (cl < 0 || cl > 9 || w < 8 || w > 15 || m < 1 || m > 9) return ATZ_E_ARG;
-    if (w == 8) w = 9;
-    ins[k] = {buf + offs[k], lens[k]};
-    ps[k] = ((uint32_t)cl << 16) | ((uint32_t)w << 8) | (uint32_t)m;
-  }
-  std::vector<std::vector<uint8_t>> outs;
-  if (int r = deflate_many(c, ins, ps, outs)) return r;
-  for (uint64_t k = 0; k < n; k++) {
-    out_lens[k] = outs[k].size();
-    if (outs[k].size() > out_caps[k]) return ATZ_E_ARG;
-    if (!outs[k].empty()) std::memcpy(out + out_offs[k], outs[k].data(), outs[k].size());
-  }
-  return ATZ_OK;
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || (!buf && len) || !out_lens) return ATZ_E_ARG;
+    std::vector<std::pair<const uint8_t*, uint64_t>> ins(n);
+    std::vector<uint32_t> ps(n);
+    for (uint64_t k = 0; k < n; k++) {
+      if (offs[k] + lens[k] > len) return ATZ_E_ARG;
+      int cl = (int)(params[k] >> 16), w = (int)((params[k] >> 8) & 0xff), m = (int)(params[k] & 0xff);
+      if (cl < 0 || cl > 9 || w < 8 || w > 15 || m < 1 || m > 9) return ATZ_E_ARG;
+      if (w == 8) w = 9;
+      ins[k] = {buf + offs[k], lens[k]};
+      ps[k] = ((uint32_t)cl << 16) | ((uint32_t)w << 8) | (uint32_t)m;
+    }
+    std::vector<std::vector<uint8_t>> outs;
+    if (int r = deflate_many(c, ins, ps, outs)) return r;
+    for (uint64_t k = 0; k < n; k++) {
+      out_lens[k] = outs[k].size();
+      if (outs[k].size() > out_caps[k]) return ATZ_E_ARG;
+      if (!outs[k].empty()) std::memcpy(out + out_offs[k], outs[k].data(), outs[k].size());
+    }
+    return ATZ_OK;
+  });
 }
 
 int atz_inflate_batch(atz_ctx_t* c, const uint8_t* buf, uint64_t len, const uint64_t* offs, const uint64_t* lens,
                       uint64_t n, uint32_t* status, uint64_t* consumed, uint64_t* produced) {
-  (void)hipGetLastError();
-  if (!c || (!buf && len)) return ATZ_E_ARG;
-  if (int r = upload(c, c->d_tmp, buf, len)) return r;
-  std::vector<InfJob> jobs(n);
-  for (uint64_t k = 0; k < n; k++) {
-    if (offs[k] + lens[k] > len) return ATZ_E_ARG;
-    // the scan's configuration: output into arena slots (small-ring decoder, 32 KiB-ring reruns)
-    jobs[k].in_off = offs[k]; jobs[k].in_len = lens[k]; jobs[k].out_off = ARENA_OUT; jobs[k].out_cap = ARENA_SLOT;
-  }
-  std::vector<InfRes> res;
-  const uint64_t arena_cap = std::min<uint64_t>(64ull << 30, std::max<uint64_t>(256ull << 20, n * ARENA_SLOT));
-  if (int r = run_inflate_jobs(c, c->d_tmp.as<uint8_t>(), nullptr, jobs, res, arena_cap)) return r;
-  for (uint64_t k = 0; k < n; k++) { status[k] = res[k].status; consumed[k] = res[k].consumed; produced[k] = res[k].produced; }
-  return ATZ_OK;
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || (!buf && len)) return ATZ_E_ARG;
+    c->scan_valid = false;   // the arena holds the last scan's kept outputs
+    if (int r = upload(c, c->d_tmp, buf, len)) return r;
+    std::vector<InfJob> jobs(n);
+    for (uint64_t k = 0; k < n; k++) {
+      if (offs[k] + lens[k] > len) return ATZ_E_ARG;
+      // the scan's configuration: output into arena slots (small-ring decoder, 32 KiB-ring reruns)
+      jobs[k].in_off = offs[k]; jobs[k].in_len = lens[k]; jobs[k].out_off = ARENA_OUT; jobs[k].out_cap = ARENA_SLOT;
+    }
+    std::vector<InfRes> res;
+    const uint64_t arena_cap = std::min<uint64_t>(64ull << 30, std::max<uint64_t>(256ull << 20, n * ARENA_SLOT));
+    if (int r = run_inflate_jobs(c, c->d_tmp.as<uint8_t>(), nullptr, jobs, res, arena_cap)) return r;
+    for (uint64_t k = 0; k < n; k++) { status[k] = res[k].status; consumed[k] = res[k].consumed; produced[k] = res[k].produced; }
+    return ATZ_OK;
+  });
 }
 
 static uint64_t rd8(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
 
 int atz_reconstruct(atz_ctx_t* c, const uint8_t* atz, uint64_t n, uint8_t** out, uint64_t* out_len) {
-  (void)hipGetLastError();
-  if (!c || !atz || !out || !out_len) return ATZ_E_ARG;
-  if (n < 28 || std::memcmp(atz, "ATZ\1", 4) != 0) return ATZ_E_FORMAT;   // main.cpp:1018-1021
-  if (rd8(atz + 4) != n) return ATZ_E_FORMAT;                              // main.cpp:1022-1025
-  const uint64_t origlen = rd8(atz + 12), nstrms = rd8(atz + 20);
-  std::vector<uint8_t> o;
-  if (nstrms == 0) {
-    if (28 + origlen > n) return ATZ_E_FORMAT;
-    o.assign(atz + 28, atz + 28 + origlen);
-  } else {
-    struct D { uint64_t off, cl, il, nd, fd, dpos, ipos; uint8_t c, w, m; };
-    std::vector<D> d(nstrms);
-    uint64_t lastos = 28;                                                  // main.cpp:1031-1063
-    for (uint64_t j = 0; j < nstrms; j++) {
-      if (lastos + 35 > n) return ATZ_E_FORMAT;
-      d[j].off = rd8(atz + lastos); d[j].cl = rd8(atz + lastos + 8); d[j].il = rd8(atz + lastos + 16);
-      d[j].c = atz[lastos + 24]; d[j].w = atz[lastos + 25]; d[j].m = atz[lastos + 26];
-      d[j].nd = rd8(atz + lastos + 27);
-      if (d[j].nd) {
-        d[j].fd = rd8(atz + lastos + 35); d[j].dpos = lastos + 43; d[j].ipos = 43 + d[j].nd * 9 + lastos;
-        lastos = lastos + 43 + d[j].nd * 9 + d[j].il;
-      } else {
-        d[j].fd = 0; d[j].dpos = 0; d[j].ipos = 35 + lastos;
-        lastos = lastos + 35 + d[j].il;
-      }
-      if (lastos > n) return ATZ_E_FORMAT;
-      if (d[j].c > 9 || d[j].w < 8 || d[j].w > 15 || d[j].m < 1 || d[j].m > 9) return ATZ_E_REF_ABORT;
-    }
-    std::vector<std::pair<const uint8_t*, uint64_t>> ins;
-    std::vector<uint32_t> params;
-    for (auto& x : d) {
-      ins.push_back({atz + x.ipos, x.il});
-      int w = x.w == 8 ? 9 : x.w;
-      params.push_back(((uint32_t)x.c << 16) | ((uint32_t)w << 8) | x.m);
-    }
-    std::vector<std::vector<uint8_t>> defl;
-    if (int r = deflate_many(c, ins, params, defl)) return r;
-    uint64_t residue = lastos, gapsum = 0, lo = 0, ll = 0;
-    for (uint64_t j = 0; j < nstrms; j++) {
-      if (lo + ll != d[j].off) {
-        uint64_t g = d[j].off - (lo + ll);
-        if (residue + gapsum + g > n) return ATZ_E_FORMAT;
-        o.insert(o.end(), atz + residue + gapsum, atz + residue + gapsum + g);
-        gapsum += g;
-      }
-      std::vector<uint8_t>& cb = defl[j];
-      if (cb.size() > d[j].cl + 65535) return ATZ_E_REF_ABORT;            // deflate() != Z_STREAM_END
-      cb.resize(std::max<uint64_t>(cb.size(), d[j].cl), 0);
-      if (d[j].nd) {
-        uint64_t sum = 0;
-        for (uint64_t i = 0; i < d[j].nd; i++) {
-          uint64_t delta = rd8(atz + d[j].dpos + 8 * i);
-          uint64_t at = d[j].fd + delta + sum;
-          if (at < cb.size()) cb[at] = atz[d[j].dpos + 8 * d[j].nd + i];
-          sum += delta;
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || !atz || !out || !out_len) return ATZ_E_ARG;
+    c->scan_valid = false;
+    if (n < 28 || std::memcmp(atz, "ATZ\1", 4) != 0) return ATZ_E_FORMAT;   // main.cpp:1018-1021
+    if (rd8(atz + 4) != n) return ATZ_E_FORMAT;                              // main.cpp:1022-1025
+    const uint64_t origlen = rd8(atz + 12), nstrms = rd8(atz + 20);
+    // Every size field below comes from the file.  The reference trusts them (a huge count or
+    // length makes its new[] throw and the process abort); here each is bounded by the bytes that
+    // are actually left, with subtraction-only checks (no sum can wrap), before anything is sized
+    // from it.
+    std::vector<uint8_t> o;
+    if (nstrms == 0) {
+      if (origlen > n - 28) return ATZ_E_FORMAT;
+      o.assign(atz + 28, atz + 28 + origlen);
+    } else {
+      if (nstrms > (n - 28) / 35) return ATZ_E_FORMAT;                     // each descriptor is >= 35 bytes
+      struct D { uint64_t off, cl, il, nd, fd, dpos, ipos; uint8_t c, w, m; };
+      std::vector<D> d(nstrms);
+      uint64_t lastos = 28;                                                  // main.cpp:1031-1063
+      for (uint64_t j = 0; j < nstrms; j++) {
+        if (n - lastos < 35) return ATZ_E_FORMAT;
+        D& x = d[j];
+        x.off = rd8(atz + lastos); x.cl = rd8(atz + lastos + 8); x.il = rd8(atz + lastos + 16);
+        x.c = atz[lastos + 24]; x.w = atz[lastos + 25]; x.m = atz[lastos + 26];
+        x.nd = rd8(atz + lastos + 27);
+        if (x.nd) {
+          if (n - lastos < 43) return ATZ_E_FORMAT;
+          const uint64_t room = n - lastos - 43;
+          if (x.nd > room / 9) return ATZ_E_FORMAT;
+          if (x.il > room - x.nd * 9) return ATZ_E_FORMAT;
+          x.fd = rd8(atz + lastos + 35); x.dpos = lastos + 43; x.ipos = lastos + 43 + x.nd * 9;
+          lastos = x.ipos + x.il;
+        } else {
+          if (x.il > n - lastos - 35) return ATZ_E_FORMAT;
+          x.fd = 0; x.dpos = 0; x.ipos = lastos + 35;
+          lastos = x.ipos + x.il;
         }
+        if (x.c > 9 || x.w < 8 || x.w > 15 || x.m < 1 || x.m > 9) return ATZ_E_REF_ABORT;
       }
-      o.insert(o.end(), cb.begin(), cb.begin() + d[j].cl);
-      lo = d[j].off; ll = d[j].cl;
+      // streams in file order, inside the original (the writer emits them so; a crafted file
+      // with overlapping or out-of-range streams is rejected before any buffer is sized)
+      uint64_t end = 0;
+      for (uint64_t j = 0; j < nstrms; j++) {
+        if (d[j].off < end || d[j].off > origlen || d[j].cl > origlen - d[j].off) return ATZ_E_FORMAT;
+        end = d[j].off + d[j].cl;
+      }
+      std::vector<std::pair<const uint8_t*, uint64_t>> ins;
+      std::vector<uint32_t> params;
+      for (auto& x : d) {
+        ins.push_back({atz + x.ipos, x.il});
+        int w = x.w == 8 ? 9 : x.w;
+        params.push_back(((uint32_t)x.c << 16) | ((uint32_t)w << 8) | x.m);
+      }
+      std::vector<std::vector<uint8_t>> defl;
+      if (int r = deflate_many(c, ins, params, defl)) return r;
+      const uint64_t residue = lastos;
+      uint64_t gapsum = 0, lo = 0, ll = 0;
+      auto take = [&](uint64_t g) -> bool {   // g residue bytes: inside the file?
+        return residue + gapsum <= n && g <= n - (residue + gapsum);
+      };
+      for (uint64_t j = 0; j < nstrms; j++) {
+        if (lo + ll != d[j].off) {
+          const uint64_t g = d[j].off - (lo + ll);   // > 0: offsets checked ascending above
+          if (!take(g)) return ATZ_E_FORMAT;
+          o.insert(o.end(), atz + residue + gapsum, atz + residue + gapsum + g);
+          gapsum += g;
+        }
+        std::vector<uint8_t>& cb = defl[j];
+        if (cb.size() > d[j].cl + 65535) return ATZ_E_REF_ABORT;            // deflate() != Z_STREAM_END
+        cb.resize(std::max<uint64_t>(cb.size(), d[j].cl), 0);
+        if (d[j].nd) {
+          uint64_t sum = 0;
+          for (uint64_t i = 0; i < d[j].nd; i++) {
+            uint64_t delta = rd8(atz + d[j].dpos + 8 * i);
+            uint64_t at = d[j].fd + delta + sum;
+            if (at < cb.size()) cb[at] = atz[d[j].dpos + 8 * d[j].nd + i];
+            sum += delta;
+          }
+        }
+        o.insert(o.end(), cb.begin(), cb.begin() + d[j].cl);
+        lo = d[j].off; ll = d[j].cl;
+      }
+      if (lo + ll < origlen) {
+        const uint64_t t = origlen - (lo + ll);
+        if (!take(t)) return ATZ_E_FORMAT;
+        o.insert(o.end(), atz + residue + gapsum, atz + residue + gapsum + t);
+      }
     }
-    if (lo + ll < origlen) {
-      uint64_t t = origlen - (lo + ll);
-      if (residue + gapsum + t > n) return ATZ_E_FORMAT;
-      o.insert(o.end(), atz + residue + gapsum, atz + residue + gapsum + t);
-    }
-  }
-  uint8_t* h = (uint8_t*)std::malloc(o.size() + 1);
-  if (!h) return ATZ_E_NOMEM;
-  if (!o.empty()) std::memcpy(h, o.data(), o.size());
-  *out = h; *out_len = o.size();
-  return ATZ_OK;
+    uint8_t* h = (uint8_t*)std::malloc(o.size() + 1);
+    if (!h) return ATZ_E_NOMEM;
+    if (!o.empty()) std::memcpy(h, o.data(), o.size());
+    *out = h; *out_len = o.size();
+    return ATZ_OK;
+  });
 }
 
 }  // extern "C"

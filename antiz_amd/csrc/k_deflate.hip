@@ -367,6 +367,118 @@ __global__ __launch_bounds__(256) void k_buckets_pk(const uint8_t* __restrict__ 
   }
 }
 
+// k_buckets_sort: the same bucket arrays by a stable LSD radix sort of the positions by hash, all of
+// it in LDS and on every wave of the block (the kernels above assign positions in order on one
+// wave, which left a 128 KiB-LDS block's CU mostly idle).  Positions are sorted as u16 by their
+// hash (H[p], kept in LDS): one pass per <= 8-bit digit (hash_bits = memLevel + 7: one pass for
+// memLevel 1, two above), each pass a stable counting sort -- every wave owns a contiguous tile of
+// the input order and counts its digits per batch of 64 (lanes sharing a digit found with one
+// ballot per digit bit), an exclusive scan over (digit, wave) gives each wave's output ranges in
+// digit-major, wave-minor order, and the waves scatter their tiles in order.  A final sweep over
+// the sorted order writes bpos (first entry of a hash flagged BUCKET_FIRST) and sidx.  The result
+// is the unique (hash, position) order, so it is identical to the other kernels' output.
+// LDS: 6 bytes per position + 2 bytes per (digit, wave); streams of < 64 Ki positions.
+static constexpr uint32_t BSORT_THREADS = 1024, BSORT_W = BSORT_THREADS / 64;
+static constexpr uint32_t BSORT_CNT_BYTES = 256 * BSORT_W * 2;
+__host__ __device__ constexpr uint32_t bsort_lds_bytes(uint32_t npad) { return 6 * npad + BSORT_CNT_BYTES; }
+// lanes of the wave (among `valid` ones) whose `bits`-bit digit equals this lane's
+__device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, uint32_t bits) {
+  uint64_t m = __ballot(valid);
+  for (uint32_t k = 0; k < bits; k++) {
+    const bool b = (d >> k) & 1u;
+    const uint64_t bal = __ballot(b);
+    m &= b ? bal : ~bal;
+  }
+  return m;
+}
+__global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* __restrict__ infl,
+                                                              const ChainJob* __restrict__ jobs,
+                                                              uint32_t* __restrict__ chains, uint32_t njobs) {
+  extern __shared__ uint32_t dyn_lds[];
+  __shared__ uint32_t wtot[BSORT_W];
+  const uint32_t j = blockIdx.x;
+  if (j >= njobs) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const ChainJob jb = jobs[j];
+  const uint8_t* in = infl + jb.infl_off;
+  const uint32_t n = (uint32_t)jb.n;
+  const uint32_t npad = (n + 63) & ~63u;
+  uint32_t* sidx = chains + jb.chain_off;
+  uint32_t* bpos = sidx + npad;
+  const uint32_t hbits = jb.memlevel + 7, hmask = (1u << hbits) - 1, hshift = (hbits + 2) / 3;
+  const uint32_t nh = n >= 3 ? n - 2 : 0;
+  LDS uint16_t* H = (LDS uint16_t*)dyn_lds;   // hash of position p
+  LDS uint16_t* A = H + npad;                 // positions after the low-digit pass
+  LDS uint16_t* Bo = A + npad;                // positions in (hash, position) order
+  LDS uint16_t* cnt = Bo + npad;              // [digit * BSORT_W + wave]: count, then output offset
+  for (uint32_t p = tid; p < nh; p += BSORT_THREADS)
+    H[p] = (uint16_t)((((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask);
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint32_t T = ((nh + BSORT_W - 1) / BSORT_W + 63) & ~63u;   // input tile of a wave
+  const uint32_t t0 = (uint32_t)wave * T < nh ? (uint32_t)wave * T : nh;
+  const uint32_t t1 = t0 + T < nh ? t0 + T : nh;
+  // one stable counting-sort pass: digit (H[p] >> shift) & (2^bits - 1) of p = src ? src[i] : i
+  auto pass = [&](const LDS uint16_t* src, LDS uint16_t* dst, uint32_t shift, uint32_t bits) {
+    const uint32_t dmask = (1u << bits) - 1;
+    __syncthreads();   // H / the previous pass's dst written, its scatter done with cnt
+    for (uint32_t i = tid; i < 256 * BSORT_W; i += BSORT_THREADS) cnt[i] = 0;
+    __syncthreads();
+    for (uint32_t i0 = t0; i0 < t1; i0 += 64) {
+      const uint32_t i = i0 + (uint32_t)lane;
+      const bool valid = i < t1;
+      const uint32_t p = valid ? (src ? (uint32_t)src[i] : i) : 0u;
+      const uint32_t d = valid ? ((uint32_t)H[p] >> shift) & dmask : 0u;
+      const uint64_t pm = digit_peers(d, valid, bits);
+      if (valid && (pm & lt) == 0) cnt[d * BSORT_W + wave] += (uint16_t)__popcll(pm);
+    }
+    __syncthreads();
+    // exclusive scan of the 256 x BSORT_W counts (4 per thread, then across the block)
+    const uint32_t b4 = 4u * (uint32_t)tid;
+    uint32_t c4[4], s = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) { c4[u] = cnt[b4 + u]; s += c4[u]; }
+    uint32_t incl = s;
+    for (int dd = 1; dd < 64; dd <<= 1) {
+      const uint32_t t = __shfl_up(incl, dd, 64);
+      if (lane >= dd) incl += t;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < wave; w++) off += wtot[w];
+    uint32_t e = off + incl - s;
+#pragma unroll
+    for (int u = 0; u < 4; u++) { cnt[b4 + u] = (uint16_t)e; e += c4[u]; }
+    __syncthreads();
+    for (uint32_t i0 = t0; i0 < t1; i0 += 64) {
+      const uint32_t i = i0 + (uint32_t)lane;
+      const bool valid = i < t1;
+      const uint32_t p = valid ? (src ? (uint32_t)src[i] : i) : 0u;
+      const uint32_t d = valid ? ((uint32_t)H[p] >> shift) & dmask : 0u;
+      const uint64_t pm = digit_peers(d, valid, bits);
+      const uint32_t base = valid ? (uint32_t)cnt[d * BSORT_W + wave] : 0u;
+      if (valid) {
+        dst[base + (uint32_t)__popcll(pm & lt)] = (uint16_t)p;
+        if ((pm & lt) == 0) cnt[d * BSORT_W + wave] = (uint16_t)(base + (uint32_t)__popcll(pm));
+      }
+    }
+  };
+  static_assert(256 * BSORT_W == 4 * BSORT_THREADS, "the scan takes 4 counters per thread");
+  if (hbits <= 8) {
+    pass(nullptr, Bo, 0, hbits);
+  } else {
+    pass(nullptr, A, 0, hbits - 8);
+    pass(A, Bo, hbits - 8, 8);
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < nh; i += BSORT_THREADS) {
+    const uint32_t p = Bo[i];
+    const bool first = i == 0 || H[Bo[i - 1]] != H[p];
+    bpos[i] = p | (first ? BUCKET_FIRST : 0u);
+    sidx[p] = i;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_match: longest_match (Z/deflate.c:1148-1289) for every position of a trial, lanes = positions.
 //

@@ -26,8 +26,10 @@ static constexpr uint32_t INF_RING_FULL = 32768;
 #define INF_RING_SMALL_BYTES 4096   // C4 k_inflate (A/B): 8 KiB x 4 waves 137 ms, 4 KiB x 5 126 ms, x 6 121 ms, x 8 127 ms
 #endif
 static constexpr uint32_t INF_RING_SMALL = INF_RING_SMALL_BYTES;
-static_assert(INF_RING_SMALL >= 4096 && (INF_RING_SMALL & (INF_RING_SMALL - 1)) == 0,
-              "small ring: power of two >= 4 KiB (a 2 KiB ring stalls the decoder)");
+// >= 2 KiB: a far source (dist > RING) ends >= RING - 258 bytes back, which must lie below the
+// unflushed tail (< RING/2 + 258 + 64 bytes), i.e. RING/2 >= 580
+static_assert(INF_RING_SMALL >= 2048 && (INF_RING_SMALL & (INF_RING_SMALL - 1)) == 0,
+              "small ring: a power of two >= 2 KiB");
 #ifndef INF_SMALL_WAVES
 #define INF_SMALL_WAVES 6   // waves per SIMD the small-ring decoder is register-bounded for (8 KiB ring: 3 -> 183 ms, 4 -> 154 ms)
 #endif
@@ -622,7 +624,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
         uint64_t done = 0;
         while (done < take) {
           uint64_t step = take - done;
-          if (step > 4096) step = 4096;
+          if (step > FLUSH_AT) step = FLUSH_AT;   // after a flush (which empties the ring) a step always fits
           const uint64_t room = RING - (prod - flushed);
           if (step > room) { flush(false); continue; }
           for (uint64_t k = lane; k < step; k += 64) ring[(prod + k) & RMASK] = src[done + k];

@@ -35,8 +35,11 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n_streams, seed):
-    """Time the real reference binary on a bounded sample of the workload (1 thread)."""
+def cpu_baseline(n_streams, seed, ctx):
+    """Time the real reference binary on a bounded sample of the workload (1 thread), and check that
+    the library's .atz of the same sample is byte-identical to the reference's (parity at the bench
+    configuration: same generator, seed and options, 3 sweep pipes)."""
+    import hashlib
     from antiz_amd import datagen
     ref = os.path.join(ROOT, "oracle", "_ref", "uncomp")
     if not os.path.exists(ref):
@@ -53,6 +56,10 @@ def cpu_baseline(n_streams, seed):
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         dt = time.perf_counter() - t0
         ok = r.returncode == 0
+        ref_sha = None
+        if ok:
+            with open(p + ".atz", "rb") as f:
+                ref_sha = hashlib.sha256(f.read()).hexdigest()
     finally:
         for fn in (p, p + ".atz"):
             if os.path.exists(fn):
@@ -60,7 +67,12 @@ def cpu_baseline(n_streams, seed):
         os.rmdir(d)
     if not ok:
         return None
+    atz, _ = ctx.precompress(data)
+    same = hashlib.sha256(atz).hexdigest() == ref_sha
+    if not same:
+        log("PARITY FAILURE: the library's .atz of the cpu_baseline sample differs from the reference's")
     return {"value": round(len(data) / 1e6 / dt, 4), "unit": "MB/s", "cores": 1, "kind": "reference",
+            "atz_identical_to_reference": same, "atz_sha256": ref_sha[:16],
             "sample": "%d-stream prefix config of the same generator (%.1f MB, seed %d), oracle/_ref/uncomp --notest, "
                       "%.1f s wall" % (n_streams, len(data) / 1e6, seed, dt)}
 
@@ -172,7 +184,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.cpu_sample_streams, seed)
+        cpu = cpu_baseline(args.cpu_sample_streams, seed, ctx)
 
     if rank == 0:
         out = {

@@ -97,7 +97,10 @@ void atz_default_opts(atz_opts_t *opts);
 /* Phase 1: the reference's chunked scan.  *out (atz_free) receives *n records in scan order. */
 int atz_scan(atz_ctx_t *ctx, const uint8_t *file, uint64_t len, atz_cand_t **out, uint64_t *n);
 
-/* Phase 3 on the streams of the LAST atz_scan of this context (cands must be that array).
+/* Phase 3 on the streams of the LAST atz_scan of this context (cands must be that array).  Returns
+ * ATZ_E_ARG unless atz_scan was the previous call on ctx (any other call replaces its records); the
+ * scanned host buffer need not stay alive (atz_scan keeps what the sweep needs: the file on the
+ * device, each stream's Adler-32 trailer).  One atz_sweep per atz_scan.
  * res[n] is caller-allocated.  *diff_off / *diff_val (atz_free) hold n_diffs delta-encoded entries. */
 int atz_sweep(atz_ctx_t *ctx, const atz_cand_t *cands, uint64_t n, atz_result_t *res,
               uint64_t **diff_off, uint8_t **diff_val, uint64_t *n_diffs);

@@ -210,7 +210,7 @@ def test_roundtrip_large_mixed(atz):
 
 
 def test_far_history_and_ring_retry(atz):
-    """The 8 KiB-ring decoder: matches beyond the ring read the job's HBM output; a stream longer than
+    """The 4 KiB-ring decoder: matches beyond the ring read the job's HBM output; a stream longer than
     its 64 KiB arena slot loses that copy and is rerun on the 32 KiB ring.  Streams with long-distance
     matches (a repeated 20 KiB block) of 30 KiB .. 400 KiB output, at every window, must give the
     oracle's .atz bytes."""
@@ -238,3 +238,105 @@ def test_far_history_and_ring_retry(atz):
         got = c.inflate_batch(data, list(zip(offs, lens)))
         for (rc2, cons, prod), l in zip(got, lens):
             assert rc2 == 0 and cons == l
+
+
+def test_bucket_sort_matches_inorder_kernels(atz):
+    """k_buckets_sort (LDS radix sort of the positions by hash) against the in-order bucket kernels,
+    array for array (ATZ_BUCKETS_VERIFY=1 rebuilds every job both ways and fails on any difference),
+    over every memLevel and stream sizes from empty to past the sort's LDS limit; the deflates must
+    still equal the oracle's."""
+    from antiz_amd import datagen
+    rng = np.random.default_rng(5)
+    r = random.Random(5)
+    buf = bytearray()
+    items = []
+    sizes = [0, 1, 2, 3, 4, 63, 64, 65, 1000, 4094, 4096, 4097, 8191, 12289, 16384, 20481, 25900, 25999, 30000, 70000]
+    for k, n in enumerate(sizes * 2):
+        kind = k % 3
+        if kind == 0:
+            d = datagen.text(rng, n)
+        elif kind == 1:
+            d = bytes(r.choice(b"ab") for _ in range(n))
+        else:
+            d = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        for m in range(1, 10):
+            items.append((len(buf), len(d), 1 + (k + m) % 9, 15, m))
+        buf += d
+    os.environ["ATZ_BUCKETS_VERIFY"] = "1"
+    try:
+        with atz.Context() as c:
+            outs = c.deflate_batch(bytes(buf), items)
+    finally:
+        del os.environ["ATZ_BUCKETS_VERIFY"]
+    bad = []
+    for it, o in zip(items, outs):
+        want, _ = _libs.ora_deflate(bytes(buf[it[0]:it[0] + it[1]]), it[2], it[3], it[4])
+        if o != want:
+            bad.append(it[1:])
+    assert not bad, bad[:10]
+
+
+def test_bench_config_slice_matches_oracle(atz):
+    """Parity at the configuration bench.py times: the first 1 600 streams of the C4 workload itself
+    (same generator and seed; > 768 streams, so the sweep runs on all 3 pipes with multi-trial
+    speculative rounds), default options.  The .atz bytes, the stream table and every stream's
+    chosen parameters, ident and recomp decision must equal the oracle's."""
+    from antiz_amd import datagen
+    data = datagen.gen_c4(seed=4, n_streams=1600, workers=4)
+    rc, ref, st_ref = _libs.ora_precompress(data)
+    assert rc == 0
+    with atz.Context() as c:
+        recs = c.scan(data)
+        assert [r[:4] for r in recs] == [(s["offset"], s["type"], s["comp_len"], s["infl_len"]) for s in st_ref["streams"]]
+        res, _ = c.sweep()
+        got = [(r["clevel"], r["window"], r["memlevel"], r["ident"], r["recomp"]) for r in res]
+        exp = [(s["clevel"], s["window"], s["memlevel"], s["ident"], s["recomp"]) for s in st_ref["streams"]]
+        assert got == exp
+        out, st = c.precompress(data)
+        assert st["n_streams"] > 1500 and st["n_recomp"] == st["n_streams"]
+        assert sha(out) == sha(ref)
+
+
+def test_reconstruct_rejects_crafted_atz(atz):
+    """Size fields of an ATZ1 file are untrusted: counts and lengths that overflow, overlap or point
+    past the file must give ATZ_E_FORMAT (the reference would abort or read out of bounds), never a
+    crash or a huge allocation."""
+    import struct
+    data = open(os.path.join(GOLD, "zt", "input.bin"), "rb").read()[:3000]
+    s, _ = _libs.ora_deflate(_libs.text(random.Random(3), 5000), 6, 15, 8)
+    data = data + s + b"tail"
+    with atz.Context() as c:
+        good, _ = c.precompress(data)
+        assert c.reconstruct(good) == data
+        n = len(good)
+
+        def fix(b):
+            b = bytearray(b)
+            b[4:12] = struct.pack("<Q", len(b))
+            return bytes(b)
+        bad = []
+        b = bytearray(good); b[20:28] = struct.pack("<Q", 1 << 62); bad.append(bytes(b))              # stream count
+        b = bytearray(good); b[28 + 16:28 + 24] = struct.pack("<Q", (1 << 64) - 30); bad.append(bytes(b))   # infl_len wraps
+        b = bytearray(good); b[28 + 27:28 + 35] = struct.pack("<Q", 1 << 61); bad.append(bytes(b))    # diff count
+        b = bytearray(good); b[28 + 8:28 + 16] = struct.pack("<Q", 1 << 63); bad.append(bytes(b))     # comp_len
+        b = bytearray(good); b[28:36] = struct.pack("<Q", (1 << 64) - 1); bad.append(bytes(b))       # offset
+        bad.append(fix(good[:n // 2]))                                                               # truncated
+        for k, x in enumerate(bad):
+            with pytest.raises(atz.AtzError):
+                c.reconstruct(x)
+
+
+def test_sweep_requires_its_scan(atz):
+    """atz_sweep works only on the records of the context's previous call, atz_scan; any other call
+    in between (here a deflate) replaces them, and the sweep is refused instead of reading stale
+    state."""
+    from antiz_amd import datagen
+    data = datagen.gen_c2(seed=9, n=20)
+    with atz.Context() as c:
+        c.scan(bytes(data))              # a temporary: the scanned buffer may be released after the scan
+        c.deflate(b"hello hello hello", 6, 15, 8)
+        with pytest.raises(atz.AtzError):
+            c.sweep()
+        recs = c.scan(data)
+        res, _ = c.sweep()
+        assert len(res) == len(recs) == 20
