@@ -29,6 +29,8 @@
 #include <new>
 #include <stdexcept>
 #include <thread>
+#include <condition_variable>
+#include <mutex>
 #include <functional>
 #include <vector>
 
@@ -144,6 +146,7 @@ struct StreamState {
   bool recomp = false;
 };
 
+
 uint32_t pk(int c, int w, int m) { return ((uint32_t)c << 16) | ((uint32_t)w << 8) | (uint32_t)m; }
 
 void prange(std::vector<uint32_t>& l, int cmin, int cmax, int wmin, int wmax, int mmin, int mmax) {
@@ -237,6 +240,11 @@ int header_type_host(unsigned b0, unsigned b1) {
   return -1;
 }
 
+// Stream bytes are addressed by absolute device addresses (infl_off / StreamDev.infl_off /
+// ChainJob.infl_off / MatchJob.infl_off), so every kernel takes a null inflated-buffer base: the
+// records of one file may live in several allocations (one per scan piece).
+const uint8_t* const INFL_BASE = nullptr;
+
 }  // namespace
 
 struct KTimer {   // HIP events bracketing kernel launches on the library stream
@@ -269,6 +277,11 @@ struct Pipe {
   KTimer pkt;
   uint64_t chain_used = 0, chain_cap = 0;
   std::vector<uint32_t> streams;   // the streams whose chain tables this pipe owns
+  // streams handed to this pipe (scan pieces arrive while it sweeps); closed after the last piece
+  std::mutex in_mu;
+  std::condition_variable in_cv;
+  std::vector<uint32_t> inbox;
+  bool in_closed = false;
   int id = 0;
   // diagnostics (ATZ_TIMING): host phase times, per trial kind x level counters
   double t_list = 0, t_chains = 0, t_trials = 0, t_apply = 0;
@@ -308,6 +321,8 @@ struct atz_ctx {
   // chains cache: per record and memlevel
   std::vector<std::array<uint64_t, 10>> chain_off;   // offset in the owning pipe's d_chains
   std::vector<std::unique_ptr<Pipe>> pipes;
+  std::vector<std::unique_ptr<DBuf>> slabs;   // inflated records, one allocation per scan piece
+  size_t pipes_running = 1;
 };
 
 // kind: 0 trial, 1 inflate, 2 chains, 3 other, 4 match tables
@@ -486,15 +501,36 @@ static void chunk_bytes(const uint8_t* f, const Chunk& ch, std::vector<uint8_t>&
     tm_ = std::chrono::steady_clock::now();                                                \
   } while (0)
 
-static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64_t F) {
-  auto t0 = std::chrono::steady_clock::now();
-  auto tm_ = t0;
-  c->recs.clear();
+// Phase 1 is split into a plan (chunk layout, header list, candidates) and pieces: contiguous chunk
+// ranges whose candidates are inflated and replayed in file order.  The replay state (a pending
+// stream at a chunk end) carries from one piece into the next, so any split gives the reference's
+// sequential result; precompress_dev hands each piece's records to the sweep while the next piece
+// is scanned.
+struct ScanCand { uint32_t chunk; int32_t type; uint64_t i; };
+// pending stream: its bytes are chunk j0 from i0 plus the napp following chunk buffers (size
+// bytes); they are materialized only for a second refill (rare)
+struct ScanPend { uint64_t off; int type; int state; uint32_t j0, napp; uint64_t i0, size; uint64_t in, out; long spec_chunk; int refills; };
+struct ScanState {
+  std::vector<Chunk> chunks;
+  std::vector<ScanCand> cands;
+  std::vector<size_t> cbeg;      // chunk j's candidates: cands[cbeg[j] .. cbeg[j + 1])
+  std::vector<InfRes> cres;      // per candidate
+  std::vector<long> pend0;       // per chunk: pending candidate of the selection from i = 0 (-1: none)
+  std::vector<InfRes> cont0;     // per chunk: speculative first continuation of that candidate
+  bool need_more = false;
+  ScanPend pd{};
+  uint64_t arena_cap = 0;
+  uint64_t max_records() const { return cands.size() + chunks.size() + 1; }
+};
+
+static int scan_plan(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64_t F, ScanState& S) {
+  auto tm_ = std::chrono::steady_clock::now();
   const uint64_t cs = c->o.chunksize;
   if (cs < 2) return ATZ_E_REF_UB;      // main.cpp:410-415 never reaches eof with chunksize 1
   if (F == 0) return ATZ_E_REF_UB;      // main.cpp:406 reads rBuffer[-1]
   // ---- chunk layout exactly as searchInfile reads the file (main.cpp:405-415) ----
-  std::vector<Chunk> chunks;
+  std::vector<Chunk>& chunks = S.chunks;
+  chunks.clear();
   {
     uint64_t g = F < cs ? F : cs;
     chunks.push_back({0, g, h[0], true});
@@ -546,91 +582,102 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
   }
   TMARK("scan: layout+ordered pairs");
   // ---- candidates per chunk: i >= 1 are file pairs, i == 0 uses buffer[0] ----
-  // Cand.job: index into fjobs (file-backed, output kept in an arena slot) or VJOB | index into
-  // vjobs (materialized buffers: chunk starts whose buffer[0] is not the file byte)
-  static constexpr uint64_t VJOB = 1ull << 63;
-  struct Cand { uint32_t chunk; int32_t type; uint64_t i; uint64_t job; };
-  std::vector<Cand> cands;
-  std::vector<InfJob> fjobs, vjobs;
-  std::vector<uint8_t> virt;
-  cands.reserve(pairs.size() + chunks.size());
-  fjobs.reserve(pairs.size() + chunks.size());
+  S.cands.clear();
+  S.cands.reserve(pairs.size() + chunks.size());
+  S.cbeg.assign(chunks.size() + 1, 0);
   {
     size_t pi = 0;
     for (uint32_t j = 0; j < chunks.size(); j++) {
+      S.cbeg[j] = S.cands.size();
       const Chunk& ch = chunks[j];
       if (ch.len < 2) continue;
-      int t0 = header_type_host(ch.b0, h[ch.co + 1]);
-      if (t0 >= 0) {
-        InfJob jb;
-        jb.in_len = ch.len;
-        if (ch.b0_file) {
-          jb.in_off = ch.co; jb.out_off = ARENA_OUT; jb.out_cap = ARENA_SLOT;
-          cands.push_back({j, t0, 0, fjobs.size()});
-          fjobs.push_back(jb);
-        } else {
-          jb.in_off = virt.size(); jb.out_off = NO_OUT; jb.out_cap = 0;
-          std::vector<uint8_t> v;
-          chunk_bytes(h, ch, v);
-          virt.insert(virt.end(), v.begin(), v.end());
-          virt.resize((virt.size() + 3) & ~(size_t)3);
-          cands.push_back({j, t0, 0, VJOB | vjobs.size()});
-          vjobs.push_back(jb);
-        }
-      }
+      const int t0 = header_type_host(ch.b0, h[ch.co + 1]);
+      if (t0 >= 0) S.cands.push_back({j, t0, 0});
       const uint64_t lo = ch.co + 1, hi = ch.co + ch.len - 2;   // file pairs scanned as i = 1 .. len-2
-      const uint64_t end = ch.co + ch.len;
       while (pi < pairs.size() && (pairs[pi] >> 5) < lo) pi++;
-      for (; pi < pairs.size() && (pairs[pi] >> 5) <= hi; pi++) {
-        const uint64_t p = pairs[pi] >> 5;
-        cands.push_back({j, (int32_t)(pairs[pi] & 31), p - ch.co, fjobs.size()});
-        fjobs.push_back({p, end - p, ARENA_OUT, ARENA_SLOT});
-      }
+      for (; pi < pairs.size() && (pairs[pi] >> 5) <= hi; pi++)
+        S.cands.push_back({j, (int32_t)(pairs[pi] & 31), (pairs[pi] >> 5) - ch.co});
     }
+    S.cbeg[chunks.size()] = S.cands.size();
   }
-  TMARK("scan: candidate jobs");
-  std::vector<InfRes> fr, vr;
+  S.cres.assign(S.cands.size(), InfRes{});
+  S.pend0.assign(chunks.size(), -1);
+  S.cont0.assign(chunks.size(), InfRes{});
+  S.need_more = false;
+  S.pd = ScanPend{};
   // a slot (ARENA_SLOT) is claimed at a candidate's first flush (4 KiB of output): room for a slot
   // per ~64 input bytes, capped -- slots are only written as far as the output goes
-  const uint64_t arena_cap = std::min<uint64_t>(64ull << 30, std::max<uint64_t>(1ull << 30, 16 * F));
+  S.arena_cap = std::min<uint64_t>(64ull << 30, std::max<uint64_t>(1ull << 30, 16 * F));
+  c->stats.n_candidates = S.cands.size();
+  TMARK("scan: candidates");
+  return 0;
+}
+
+// greedy selection in chunk j from position i0 (main.cpp:218-241); records go to *out.  Returns
+// the pending candidate index or -1.
+static long scan_select(const ScanState& S, uint32_t j, uint64_t i0, std::vector<Rec>* out) {
+  const Chunk& ch = S.chunks[j];
+  uint64_t i = i0;
+  for (size_t k = S.cbeg[j]; k < S.cbeg[j + 1]; k++) {
+    const ScanCand& cd = S.cands[k];
+    if (cd.i < i) continue;
+    const InfRes& r = S.cres[k];
+    if (r.consumed <= 16) continue;
+    if (r.status == INF_END) {
+      if (out) out->push_back({cd.i + ch.co, r.consumed, r.produced, cd.type, 0, r.arena_off});
+      i = cd.i + r.consumed;
+    } else if (r.consumed == ch.len - cd.i) {
+      return (long)k;
+    }
+  }
+  return -1;
+}
+
+// Chunks [ja, jb): candidate inflates (their outputs kept in the arena, which is reset: earlier
+// pieces' records were gathered out of it already), speculative first continuations, then the
+// sequential replay (main.cpp:205-246 over searchInfile's chunk sequence), appending to c->recs.
+static int scan_piece(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, ScanState& S, uint32_t ja, uint32_t jb) {
+  auto tm_ = std::chrono::steady_clock::now();
+  const std::vector<Chunk>& chunks = S.chunks;
+  const size_t k0 = S.cbeg[ja], k1 = S.cbeg[jb];
   {
-    if (int r = run_inflate_jobs(c, d_file, nullptr, fjobs, fr, arena_cap)) return r;
+    // file-backed jobs (output kept in an arena slot), and materialized buffers for chunk starts
+    // whose buffer[0] is not the file byte
+    std::vector<InfJob> fjobs, vjobs;
+    std::vector<size_t> fk, vk;
+    std::vector<uint8_t> virt;
+    fjobs.reserve(k1 - k0);
+    fk.reserve(k1 - k0);
+    for (size_t k = k0; k < k1; k++) {
+      const ScanCand& cd = S.cands[k];
+      const Chunk& ch = chunks[cd.chunk];
+      if (cd.i == 0 && !ch.b0_file) {
+        InfJob jb2;
+        jb2.in_off = virt.size(); jb2.in_len = ch.len; jb2.out_off = NO_OUT; jb2.out_cap = 0;
+        std::vector<uint8_t> v;
+        chunk_bytes(h, ch, v);
+        virt.insert(virt.end(), v.begin(), v.end());
+        virt.resize((virt.size() + 3) & ~(size_t)3);
+        vjobs.push_back(jb2);
+        vk.push_back(k);
+      } else {
+        fjobs.push_back({ch.co + cd.i, ch.len - cd.i, ARENA_OUT, ARENA_SLOT});
+        fk.push_back(k);
+      }
+    }
+    std::vector<InfRes> fr, vr;
+    if (int r = run_inflate_jobs(c, d_file, nullptr, fjobs, fr, S.arena_cap)) return r;
     if (!vjobs.empty()) {
       if (int r = upload(c, c->d_virt, virt.data(), virt.size())) return r;
       if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, vjobs, vr)) return r;
     }
+    for (size_t q = 0; q < fk.size(); q++) S.cres[fk[q]] = fr[q];
+    for (size_t q = 0; q < vk.size(); q++) S.cres[vk[q]] = vr[q];
   }
-  auto result = [&](const Cand& cd) -> const InfRes& { return (cd.job & VJOB) ? vr[cd.job & ~VJOB] : fr[cd.job]; };
-  c->stats.n_candidates = cands.size();
   TMARK("scan: candidate inflate");
-  // ---- per-chunk candidate index ranges ----
-  std::vector<size_t> cbeg(chunks.size() + 1, cands.size());
-  for (size_t k = cands.size(); k-- > 0;) cbeg[cands[k].chunk] = k;
-  for (size_t j = chunks.size(); j-- > 0;) if (cbeg[j] > cbeg[j + 1]) cbeg[j] = cbeg[j + 1];
-  // greedy selection from position i0 (main.cpp:218-241). Returns pending candidate index or -1.
-  auto select = [&](uint32_t j, uint64_t i0, std::vector<Rec>* out) -> long {
-    const Chunk& ch = chunks[j];
-    uint64_t i = i0;
-    for (size_t k = cbeg[j]; k < cbeg[j + 1]; k++) {
-      const Cand& cd = cands[k];
-      if (cd.i < i) continue;
-      const InfRes& r = result(cd);
-      if (r.consumed <= 16) continue;
-      if (r.status == INF_END) {
-        if (out) out->push_back({cd.i + ch.co, r.consumed, r.produced, cd.type, 0, r.arena_off});
-        i = cd.i + r.consumed;
-      } else if (r.consumed == ch.len - cd.i) {
-        return (long)k;
-      }
-    }
-    return -1;
-  };
-  // speculative first continuations: pending candidate of chunk j (selection from 0) + buffer j+1
-  std::vector<long> pend0(chunks.size(), -1);
-  std::vector<InfRes> cont0(chunks.size());
   {
-    // continuation inputs (pending bytes of chunk j + the whole buffer of chunk j+1) assembled in
-    // HBM by k_gather from file ranges and the chunks' buffer[0] bytes
+    // speculative first continuations: pending candidate of chunk j (selection from 0) + buffer
+    // j+1, assembled in HBM by k_gather from file ranges and the chunks' buffer[0] bytes
     std::vector<Seg> segs;
     std::vector<uint8_t> meta;
     uint64_t out = 0;
@@ -638,22 +685,22 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
     auto add_byte = [&](uint8_t b) { segs.push_back({0, 0, meta.size(), out, 1}); meta.push_back(b); out += 1; };
     std::vector<InfJob> cj;
     std::vector<uint32_t> cj_chunk;
-    for (uint32_t j = 0; j + 1 < chunks.size(); j++) {
-      long k = select(j, 0, nullptr);
-      pend0[j] = k;
+    for (uint32_t j = ja; j < jb && j + 1 < chunks.size(); j++) {
+      const long k = scan_select(S, j, 0, nullptr);
+      S.pend0[j] = k;
       if (k < 0) continue;
-      const Cand& cd = cands[k];
+      const ScanCand& cd = S.cands[k];
       const Chunk& ch = chunks[j];
       const Chunk& nx = chunks[j + 1];
-      InfJob jb;
-      jb.in_off = out;
+      InfJob jb2;
+      jb2.in_off = out;
       if (cd.i == 0) { add_byte(ch.b0); add_file(ch.co + 1, ch.len - 1); }
       else add_file(ch.co + cd.i, ch.len - cd.i);
       add_byte(nx.b0);
       add_file(nx.co + 1, nx.len - 1);
       // output into arena slots after the scan's (small-ring decoder); the bytes are not used
-      jb.in_len = out - jb.in_off; jb.out_off = ARENA_OUT; jb.out_cap = ARENA_SLOT;
-      cj.push_back(jb);
+      jb2.in_len = out - jb2.in_off; jb2.out_off = ARENA_OUT; jb2.out_cap = ARENA_SLOT;
+      cj.push_back(jb2);
       cj_chunk.push_back(j);
       out = (out + 3) & ~3ull;
     }
@@ -669,34 +716,34 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
       kend(c);
       KCHECK("k_gather");
       std::vector<InfRes> cr;
-      if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, cj, cr, arena_cap, false, false)) return r;
-      for (size_t q = 0; q < cj.size(); q++) cont0[cj_chunk[q]] = cr[q];
+      if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, cj, cr, S.arena_cap, false, false)) return r;
+      for (size_t q = 0; q < cj.size(); q++) S.cont0[cj_chunk[q]] = cr[q];
     }
-    c->stats.n_continuations = cj.size();
+    c->stats.n_continuations += cj.size();
   }
   TMARK("scan: continuations");
-  // ---- sequential replay (main.cpp:205-246 over searchInfile's chunk sequence) ----
-  bool need_more = false;
-  // pending stream: its bytes are chunk j0 from i0 plus the napp following chunk buffers (size
-  // bytes); they are materialized only for a second refill (rare)
-  struct Pend { uint64_t off; int type; int state; uint32_t j0, napp; uint64_t i0, size; uint64_t in, out; long spec_chunk; int refills; } pd{};
-  auto materialize = [&](const Pend& q, std::vector<uint8_t>& v) {
+  // ---- sequential replay ----
+  ScanPend& pd = S.pd;
+  auto materialize = [&](const ScanPend& q, std::vector<uint8_t>& v) {
     v.clear();
     const Chunk& c0 = chunks[q.j0];
     if (q.i0 == 0) chunk_bytes(h, c0, v);
     else v.assign(h + c0.co + q.i0, h + c0.co + c0.len);
     for (uint32_t k = 1; k <= q.napp; k++) chunk_bytes(h, chunks[q.j0 + k], v);
   };
-  for (uint32_t j = 0; j < chunks.size(); j++) {
+  // c->recs never reallocates while the sweep reads it (capacity = S.max_records())
+  auto room = [&]() { return c->recs.capacity() - c->recs.size() >= (S.cbeg[jb] - S.cbeg[ja]) + (jb - ja); };
+  if (!room()) return ATZ_E_INTERNAL;
+  for (uint32_t j = ja; j < jb; j++) {
     const Chunk& ch = chunks[j];
     uint64_t i = 0;
-    if (need_more) {
+    if (S.need_more) {
       uint64_t avail;
       int st;
       if (pd.state == INF_NEED) {
         InfRes rr;
         if (pd.refills == 0 && pd.spec_chunk == (long)j - 1) {
-          rr = cont0[j - 1];
+          rr = S.cont0[j - 1];
         } else {
           std::vector<uint8_t> v;
           materialize(pd, v);
@@ -718,73 +765,91 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
         c->recs.push_back({pd.off, pd.in, pd.out, pd.type, 1});
         i = ch.len - avail;
       }
-      need_more = avail == 0;
+      S.need_more = avail == 0;
     }
-    if (!need_more) {
-      long k = select(j, i, &c->recs);
+    if (!S.need_more) {
+      const long k = scan_select(S, j, i, &c->recs);
       if (k >= 0) {
-        const Cand& cd = cands[k];
-        need_more = true;
-        pd.off = cd.i + ch.co; pd.type = cd.type; pd.state = (int)result(cd).status;
-        pd.in = result(cd).consumed; pd.out = result(cd).produced;
+        const ScanCand& cd = S.cands[k];
+        S.need_more = true;
+        pd.off = cd.i + ch.co; pd.type = cd.type; pd.state = (int)S.cres[k].status;
+        pd.in = S.cres[k].consumed; pd.out = S.cres[k].produced;
         pd.j0 = j; pd.i0 = cd.i; pd.napp = 0;
         pd.size = cd.i == 0 ? ch.len : ch.len - cd.i;
-        pd.spec_chunk = (i == 0 && pend0[j] == k) ? (long)j : -2;
+        pd.spec_chunk = (i == 0 && S.pend0[j] == k) ? (long)j : -2;
         pd.refills = 0;
       }
     }
   }
   TMARK("scan: replay");
+  return 0;
+}
+
+// Every record, one piece.  (atz_scan; precompress_dev scans piece by piece while the sweep runs)
+static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64_t F) {
+  auto t0 = std::chrono::steady_clock::now();
+  c->recs.clear();
+  ScanState S;
+  if (int r = scan_plan(c, h, d_file, F, S)) return r;
+  c->recs.reserve(S.max_records());
+  if (int r = scan_piece(c, h, d_file, S, 0, (uint32_t)S.chunks.size())) return r;
   c->stats.scan_ms = ms_since(t0);
   return 0;
 }
 
-// final inflate of every record from the FILE bytes (Phase 3's doInflate, main.cpp:431-453)
-static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F) {
-  const size_t n = c->recs.size();
-  c->infl_off.resize(n);
-  c->adler.resize(n);
+// Inflated bytes of records [r0, r1) (Phase 3's doInflate, main.cpp:431-453) into `slab`:
+// c->infl_off[s] receives the absolute device address of stream s's bytes (the kernels take a null
+// base), so the records of different pieces may live in different allocations.
+static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F, size_t r0, size_t r1, DBuf& slab) {
+  if (c->infl_off.size() < r1) c->infl_off.resize(r1);
+  if (c->adler.size() < r1) c->adler.resize(r1);
   uint64_t tot = 0;
+  std::vector<uint64_t> loc(r1 - r0);
+  for (size_t s = r0; s < r1; s++) {
+    const Rec& r = c->recs[s];
+    if (r.offset + r.comp_len > F) return ATZ_E_REF_UB;   // reads past EOF (uninitialised rBuffer)
+    loc[s - r0] = tot;
+    tot += (r.infl_len + 255) & ~255ull;
+  }
+  if (int r = slab.reserve(tot + 65536)) return r;
+  const uint64_t base = (uint64_t)(uintptr_t)slab.p;
   // Streams whose scan decode kept its full output in the arena are copied; the others are
   // inflated again from the file with their exact length (doInflate, main.cpp:461-486) -- the
   // same bytes from the same offset, so both give the same result.
   std::vector<InfJob> jobs;
   std::vector<size_t> job_rec;
   std::vector<Seg> segs;
-  for (size_t s = 0; s < n; s++) {
+  for (size_t s = r0; s < r1; s++) {
     const Rec& r = c->recs[s];
-    if (r.offset + r.comp_len > F) return ATZ_E_REF_UB;   // reads past EOF (uninitialised rBuffer)
-    c->infl_off[s] = tot;
+    c->infl_off[s] = base + loc[s - r0];
     if (r.arena_off != ~0ull) {
-      segs.push_back({0, 0, r.arena_off, tot, r.infl_len});
+      segs.push_back({0, 0, r.arena_off, loc[s - r0], r.infl_len});
     } else {
       InfJob jb;
-      jb.in_off = r.offset; jb.in_len = r.comp_len; jb.out_off = tot; jb.out_cap = r.infl_len;
+      jb.in_off = r.offset; jb.in_len = r.comp_len; jb.out_off = loc[s - r0]; jb.out_cap = r.infl_len;
       jobs.push_back(jb);
       job_rec.push_back(s);
     }
-    tot += (r.infl_len + 255) & ~255ull;
   }
-  if (int r = c->d_infl.reserve(tot + 65536)) return r;
   if (!segs.empty()) {
     if (int r = upload(c, c->d_segs, segs.data(), segs.size() * sizeof(Seg))) return r;
     const uint32_t nseg = (uint32_t)segs.size();
     const uint32_t blocks = std::min<uint32_t>((nseg + 3) / 4, 65535u);
     kbeg(c, 3);
     hipLaunchKernelGGL(k_gather, dim3(blocks), dim3(256), 0, c->st, c->d_arena.as<uint8_t>(), nullptr, nullptr,
-                       c->d_infl.as<uint8_t>(), c->d_segs.as<Seg>(), nseg);
+                       slab.as<uint8_t>(), c->d_segs.as<Seg>(), nseg);
     kend(c);
     KCHECK("k_gather");
   }
   std::vector<InfRes> res;
-  if (int r = run_inflate_jobs(c, d_file, c->d_infl.as<uint8_t>(), jobs, res)) return r;
+  if (int r = run_inflate_jobs(c, d_file, slab.as<uint8_t>(), jobs, res)) return r;
   for (size_t q = 0; q < jobs.size(); q++) {
     const size_t s = job_rec[q];
     if (res[q].status != INF_END) return ATZ_E_REF_ABORT;          // main.cpp:450-452
     if (res[q].produced != c->recs[s].infl_len || res[q].consumed != c->recs[s].comp_len) return ATZ_E_REF_UB;
   }
-  c->stats.n_reinflated = jobs.size();
-  for (size_t s = 0; s < n; s++) {
+  c->stats.n_reinflated += jobs.size();
+  for (size_t s = r0; s < r1; s++) {
     // Adler-32 of the inflated bytes = the verified trailer (atz_sweep: saved by atz_scan, whose
     // host buffer the caller need not keep alive)
     const uint64_t e = c->recs[s].offset + c->recs[s].comp_len;
@@ -871,7 +936,7 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
         if (!cnt) continue;
         kbeg(c, 2);
         hipLaunchKernelGGL(k_buckets_sort, dim3((uint32_t)cnt), dim3(BSORT_THREADS), bsort_lds_bytes(cls[k]), c->st,
-                           x->d_infl.as<uint8_t>(), B.d_cjobs2.as<ChainJob>() + beg[k], chains,
+                           INFL_BASE, B.d_cjobs2.as<ChainJob>() + beg[k], chains,
                            (uint32_t)cnt);
         kend(c);
         KCHECK("k_buckets_sort");
@@ -901,7 +966,7 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
       auto launch = [&](auto kern, size_t off, size_t cnt, const char* nm) -> int {
         if (!cnt) return 0;
         kbeg(c, 2);
-        hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(), dj + off,
+        hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(256), 0, c->st, INFL_BASE, dj + off,
                            chains, (uint32_t)cnt);
         kend(c);
         KCHECK(nm);
@@ -928,11 +993,11 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
       const size_t nb = std::min(nbs - b0 % nbs, end - b0);   // a launch never holds two jobs of one slot
       kbeg(c, 2);
       if (is8)
-        hipLaunchKernelGGL(k_buckets_pk<15>, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
+        hipLaunchKernelGGL(k_buckets_pk<15>, dim3((uint32_t)nb), dim3(256), 0, c->st, INFL_BASE,
                            B.d_cjobs3.as<ChainJob>() + b0, chains, B.d_heads2.as<uint32_t>(),
                            (uint32_t)nb);
       else
-        hipLaunchKernelGGL(k_buckets_pk<16>, dim3((uint32_t)nb), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
+        hipLaunchKernelGGL(k_buckets_pk<16>, dim3((uint32_t)nb), dim3(256), 0, c->st, INFL_BASE,
                            B.d_cjobs3.as<ChainJob>() + b0, chains, B.d_heads2.as<uint32_t>(),
                            (uint32_t)nb);
       kend(c);
@@ -947,7 +1012,7 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
   for (size_t b0 = 0; b0 < big.size(); b0 += batch) {   // launches on one stream reuse the slots in order
     size_t nb = std::min(batch, big.size() - b0);
     kbeg(c, 2);
-    hipLaunchKernelGGL(k_buckets, dim3((uint32_t)nb), dim3(64), 0, c->st, x->d_infl.as<uint8_t>(),
+    hipLaunchKernelGGL(k_buckets, dim3((uint32_t)nb), dim3(64), 0, c->st, INFL_BASE,
                        B.d_cjobs.as<ChainJob>() + b0, chains, B.d_heads.as<uint64_t>(),
                        (uint32_t)nb);
     kend(c);
@@ -1101,10 +1166,10 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
     kbeg(c, 4);
     if (k < NC)
       hipLaunchKernelGGL(k_match_lds, dim3((uint32_t)cnt[k]), dim3(MATCH_THREADS), (uint32_t)(3 * cls[gmax[k]] + 64), c->st,
-                         x->d_infl.as<uint8_t>(), c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(),
+                         INFL_BASE, c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(),
                          c->d_mjobs.as<MatchJob>() + beg[k]);
     else
-      hipLaunchKernelGGL(k_match, dim3((uint32_t)cnt[k]), dim3(256), 0, c->st, x->d_infl.as<uint8_t>(),
+      hipLaunchKernelGGL(k_match, dim3((uint32_t)cnt[k]), dim3(256), 0, c->st, INFL_BASE,
                          c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(), c->d_mjobs.as<MatchJob>() + beg[k]);
     kend(c);
     KCHECK("k_match");
@@ -1198,7 +1263,7 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
   auto launch = [&](int k, const Trial* h, size_t cnt, size_t base) -> int {
     HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + base, h, cnt * sizeof(Trial), hipMemcpyHostToDevice, c->st));
     SweepArgs A;
-    A.file = d_cmp; A.infl = x->d_infl.as<uint8_t>(); A.chains = c->d_chains.as<uint32_t>();
+    A.file = d_cmp; A.infl = INFL_BASE; A.chains = c->d_chains.as<uint32_t>();
     A.R = c->d_R.as<uint2>();
     A.streams = x->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
     A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
@@ -1302,11 +1367,25 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
   return 0;
 }
 
+// ATZ_ROUND_GB=g: match tables + output scratch of one round, over all pipes (default 24 GB)
+static uint64_t round_budget_bytes() {
+  static int64_t v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_ROUND_GB"); v = (int64_t)((e ? std::max(1.0, std::atof(e)) : 24.0) * (1ull << 30)); }
+  return (uint64_t)v;
+}
 // The sweep of the streams c->streams on pipe c (per-kind x level counters: count, cycles
 // total/tree/emit/heap/fallback, parsed bytes, symbols, scan/send cycles, parse window phases).
 static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss, size_t target) {
   auto t0 = std::chrono::steady_clock::now();
-  std::vector<uint32_t> active = c->streams;
+  std::vector<uint32_t> active;
+  // new streams join at round boundaries; an idle pipe waits for the next scan piece
+  auto take_inbox = [&]() -> bool {   // false: nothing left to do
+    std::unique_lock<std::mutex> lk(c->in_mu);
+    if (active.empty()) c->in_cv.wait(lk, [&] { return !c->inbox.empty() || c->in_closed; });
+    for (uint32_t s : c->inbox) { active.push_back(s); c->streams.push_back(s); }
+    c->inbox.clear();
+    return !active.empty();
+  };
   SweepOpts so{x->o.recomp_tresh, x->o.sizediff_tresh, x->o.shortcut_len, x->o.mismatch_tol};
   uint64_t rounds = 0, ntr = 0, nsc = 0, nhz = 0, nspec = 0;
   std::vector<Trial> tr[3];
@@ -1317,7 +1396,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
   // reference's sequential one; the speculation only changes how much work runs per launch.
   static size_t chunk = ~(size_t)0;   // ATZ_CHUNK=n: at most n streams per round (the rest wait their turn)
   if (chunk == ~(size_t)0) { const char* e = std::getenv("ATZ_CHUNK"); chunk = e ? (size_t)std::atoll(e) : 0; }
-  while (!active.empty()) {
+  while (take_inbox()) {
     rounds++;
     std::vector<uint32_t> waiting;
     if (chunk && active.size() > chunk) {
@@ -1333,12 +1412,21 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     std::vector<std::pair<int, uint32_t>> mine;
     std::vector<uint32_t> mbeg(active.size() + 1);
     mine.reserve(active.size() * K);
-    uint64_t out_tot = 0, sym_tot = 0;
+    uint64_t out_tot = 0, sym_tot = 0, round_bytes = 0;
+    const uint64_t round_budget = round_budget_bytes() / x->pipes_running;
     for (size_t a = 0; a < active.size(); a++) {
       mbeg[a] = (uint32_t)mine.size();
       const uint32_t s = active[a];
       StreamState& st = ss[s];
-      for (uint32_t j = 0; j < K && st.idx + j < st.list->size(); j++) {
+      const uint32_t Ks = K;
+      // scratch of a round (match tables, outputs, symbols) is bounded: streams past the budget
+      // wait for the next round, where they go first
+      if (a > 0 && round_bytes > round_budget) {
+        waiting.insert(waiting.begin(), active.begin() + a, active.end());
+        active.resize(a);
+        break;
+      }
+      for (uint32_t j = 0; j < Ks && st.idx + j < st.list->size(); j++) {
         uint32_t p = (*st.list)[st.idx + j];
         int cl = (int)(p >> 16), w = (int)((p >> 8) & 0xff), m = (int)(p & 0xff);
         Trial t{};
@@ -1348,12 +1436,14 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
         t.sym_off = sym_tot; sym_tot += (1ull << (m + 6)) + 64;
+        round_bytes += 8 * (x->recs[s].infl_len + 320) + t.out_cap + 4 * ((1ull << (m + 6)) + 64);
         int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
         if (kind) need.push_back({s, m});
         mine.push_back({kind, (uint32_t)tr[kind].size()});
         tr[kind].push_back(t);
       }
     }
+    mbeg.resize(active.size() + 1);
     mbeg[active.size()] = (uint32_t)mine.size();
     auto ta = std::chrono::steady_clock::now();
     size_t nbuild = 0;
@@ -1529,7 +1619,13 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
     std::unique_ptr<Pipe> p(new Pipe());
     p->id = (int)c->pipes.size();
     if (hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
-    if (hipStreamCreateWithFlags(&p->pst, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
+    // the second stream only for the (off by default) prefetch / split-kind modes: an idle stream
+    // still holds one of the process's GPU_MAX_HW_QUEUES (4) hardware queues, and a pipe whose
+    // stream shares a queue with another pipe's is serialised behind it
+    static int pst = -1;   // ATZ_PST=1: create it anyway (A/B of the hardware-queue mapping)
+    if (pst < 0) { const char* e = std::getenv("ATZ_PST"); pst = e ? std::atoi(e) : 1; }
+    if ((pst || chain_prefetch_on() || split_kinds()) &&
+        hipStreamCreateWithFlags(&p->pst, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
     if (hipEventCreateWithFlags(&p->pev, hipEventDisableTiming) != hipSuccess) return ATZ_E_HIP;
     if (hipEventCreateWithFlags(&p->fev0, hipEventDisableTiming) != hipSuccess) return ATZ_E_HIP;
     if (hipEventCreateWithFlags(&p->fev1, hipEventDisableTiming) != hipSuccess) return ATZ_E_HIP;
@@ -1547,49 +1643,108 @@ static size_t sweep_pipes() {
   }
   return v;
 }
-static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
-  auto t0 = std::chrono::steady_clock::now();
-  const size_t n = c->recs.size();
-  ss.assign(n, StreamState());
-  c->chain_off.assign(n, {});
-  for (auto& a : c->chain_off) a.fill(~0ull);
-  for (size_t s = 0; s < n; s++) ss[s].list = &trial_list(c->recs[s].type, false);
-  // device stream table
-  std::vector<StreamDev> sd(n);
-  for (size_t s = 0; s < n; s++) {
-    sd[s].orig_off = c->recs[s].offset; sd[s].infl_off = c->infl_off[s];
-    sd[s].comp_len = c->recs[s].comp_len; sd[s].infl_len = c->recs[s].infl_len;
+// The sweep runs while the scan is still producing records: sweep_begin starts one host thread
+// per pipe, sweep_publish hands a range of ready records (inflated, Adler-32 known) to the pipes,
+// sweep_finish closes the inboxes, joins the threads and folds their counters.  Host tables are
+// sized for the scan's upper bound on records up front, so nothing the pipes read reallocates.
+struct SweepRun {
+  const uint8_t* d_file = nullptr;
+  std::vector<StreamState>* ss = nullptr;
+  size_t np = 0, published = 0;
+  std::vector<StreamDev> sd;      // host staging of the device stream table
+  std::vector<std::thread> th;
+  std::vector<int> rc;
+  std::chrono::steady_clock::time_point t0;
+  bool running = false;
+};
+
+static void sweep_close(atz_ctx* c, SweepRun& R) {
+  for (size_t g = 0; g < R.np; g++) {
+    Pipe* p = c->pipes[g].get();
+    std::lock_guard<std::mutex> lk(p->in_mu);
+    p->in_closed = true;
+    p->in_cv.notify_all();
   }
-  if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;
-  if (int r = upload(c, c->d_streams, sd.data(), n * sizeof(StreamDev))) return r;
-  HIPCHK(hipStreamSynchronize(c->st));
-  const size_t np = std::max<size_t>(1, std::min(sweep_pipes(), (n + 255) / 256));
-  if (int r = ensure_pipes(c, np)) return r;
-  for (size_t g = 0; g < np; g++) {
+  for (auto& t : R.th) t.join();
+  R.th.clear();
+  R.running = false;
+}
+
+static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState>& ss, size_t n_max, SweepRun& R) {
+  R.t0 = std::chrono::steady_clock::now();
+  R.d_file = d_file;
+  R.ss = &ss;
+  R.published = 0;
+  ss.assign(n_max, StreamState());
+  c->chain_off.assign(n_max, {});
+  for (auto& a : c->chain_off) a.fill(~0ull);
+  if (c->infl_off.size() < n_max) c->infl_off.resize(n_max);
+  if (c->adler.size() < n_max) c->adler.resize(n_max);
+  R.sd.assign(n_max, StreamDev{});
+  if (int r = c->d_adler.reserve(n_max * 4 + 4096)) return r;
+  if (int r = c->d_streams.reserve(n_max * sizeof(StreamDev) + 4096)) return r;
+  R.np = std::max<size_t>(1, std::min(sweep_pipes(), (n_max + 255) / 256));
+  c->pipes_running = R.np;
+  if (int r = ensure_pipes(c, R.np)) return r;
+  for (size_t g = 0; g < R.np; g++) {
     Pipe* p = c->pipes[g].get();
     p->streams.clear();
-    for (size_t s = g; s < n; s += np) p->streams.push_back((uint32_t)s);
+    p->inbox.clear();
+    p->in_closed = false;
     p->stats = atz_stats_t{};
     p->chain_used = 0;
-    p->chain_cap = CHAIN_CACHE_CAP / np;
+    p->chain_cap = CHAIN_CACHE_CAP / R.np;
     p->t_list = p->t_chains = p->t_trials = p->t_apply = 0;
     std::memset(p->kind, 0, sizeof(p->kind));
   }
   static size_t target = 0;   // trials per round and pipe (ATZ_TARGET: tuning)
   if (!target) { const char* e = std::getenv("ATZ_TARGET"); target = e ? (size_t)std::max(256, std::atoi(e)) : 4096; }   // C4: 16384 758, 8192 774, 4096 787 MB/s
-  std::vector<int> rc(np, 0);
-  if (np == 1) {
-    rc[0] = sweep_pipe(c, c->pipes[0].get(), d_file, ss, target);
-  } else {
-    std::vector<std::thread> th;
-    for (size_t g = 0; g < np; g++)
-      th.emplace_back([&, g]() {
-        if (hipSetDevice(c->dev) != hipSuccess) { rc[g] = ATZ_E_HIP; return; }
-        rc[g] = sweep_pipe(c, c->pipes[g].get(), d_file, ss, target);
-      });
-    for (auto& t : th) t.join();
+  R.rc.assign(R.np, 0);
+  R.running = true;
+  for (size_t g = 0; g < R.np; g++)
+    R.th.emplace_back([c, &R, &ss, g]() {
+      if (hipSetDevice(c->dev) != hipSuccess) { R.rc[g] = ATZ_E_HIP; return; }
+      R.rc[g] = sweep_pipe(c, c->pipes[g].get(), R.d_file, ss, target);
+      if (R.rc[g]) {   // a failed pipe keeps draining nothing: drop what reaches it
+        Pipe* p = c->pipes[g].get();
+        std::lock_guard<std::mutex> lk(p->in_mu);
+        p->inbox.clear();
+      }
+    });
+  return 0;
+}
+
+// records [r0, r1) are inflated (infl_off, adler set): device table entries, then the pipes
+static int sweep_publish(atz_ctx* c, SweepRun& R, size_t r0, size_t r1) {
+  if (r1 <= r0) return 0;
+  if (r1 > R.sd.size()) return ATZ_E_INTERNAL;
+  for (size_t s = r0; s < r1; s++) {
+    StreamDev& d = R.sd[s];
+    d.orig_off = c->recs[s].offset; d.infl_off = c->infl_off[s];
+    d.comp_len = c->recs[s].comp_len; d.infl_len = c->recs[s].infl_len;
+    (*R.ss)[s].list = &trial_list(c->recs[s].type, false);
   }
-  for (size_t g = 0; g < np; g++) if (rc[g]) return rc[g];
+  HIPCHK(hipMemcpyAsync(c->d_adler.as<uint32_t>() + r0, c->adler.data() + r0, (r1 - r0) * 4, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipMemcpyAsync(c->d_streams.as<StreamDev>() + r0, R.sd.data() + r0, (r1 - r0) * sizeof(StreamDev),
+                        hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));   // the pipes' streams read these tables
+  for (size_t g = 0; g < R.np; g++) {
+    Pipe* p = c->pipes[g].get();
+    std::lock_guard<std::mutex> lk(p->in_mu);
+    // interleaved over the pipes by global index: every pipe gets the same mix of classes and sizes
+    for (size_t s = r0 + (g + R.np - r0 % R.np) % R.np; s < r1; s += R.np) p->inbox.push_back((uint32_t)s);
+    p->in_cv.notify_all();
+  }
+  R.published = r1;
+  return 0;
+}
+
+static int sweep_finish(atz_ctx* c, SweepRun& R) {
+  sweep_close(c, R);
+  const size_t np = R.np, n = R.published;
+  std::vector<StreamState>& ss = *R.ss;
+  for (size_t g = 0; g < np; g++) if (R.rc[g]) return R.rc[g];
+  ss.resize(n);
   // fold the pipes' counters into the context's
   uint64_t kind[3][10][14] = {};
   double tch = 0, ttr = 0, tap = 0;
@@ -1613,7 +1768,7 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
   }
   if (timing_on())
     std::fprintf(stderr, "atz: sweep host: chains %.1f ms (incl. kernels), trials %.1f ms (incl. kernels), apply %.1f ms, total %.1f ms\n",
-                 tch, ttr, tap, ms_since(t0));
+                 tch, ttr, tap, ms_since(R.t0));
   if (timing_on())
     for (int k = 0; k < 3; k++)
       for (int l = 0; l < 10; l++) {
@@ -1631,8 +1786,25 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
     const uint64_t C = c->recs[s].comp_len;
     st.recomp = (C - st.ident) <= c->o.recomp_tresh && st.ident > 0;
   }
-  c->stats.sweep_ms = ms_since(t0);
+  c->stats.sweep_ms = ms_since(R.t0);
   return 0;
+}
+
+// joins the pipe threads on every exit path of a caller that started them
+struct SweepGuard {
+  atz_ctx* c;
+  SweepRun& R;
+  ~SweepGuard() { if (R.running) sweep_close(c, R); }
+};
+
+// the sweep of every record of the context (atz_sweep)
+static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
+  const size_t n = c->recs.size();
+  SweepRun R;
+  SweepGuard guard{c, R};
+  if (int r = sweep_begin(c, d_file, ss, n, R)) return r;
+  if (int r = sweep_publish(c, R, 0, n)) return r;
+  return sweep_finish(c, R);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1700,7 +1872,7 @@ static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::
   uint32_t blocks = std::min<uint32_t>((nseg + 3) / 4, 65535u);
   kbeg(c, 3);
   hipLaunchKernelGGL(k_gather, dim3(blocks ? blocks : 1), dim3(256), 0, c->st, c->d_meta.as<uint8_t>(),
-                     c->d_infl.as<uint8_t>(), d_file, c->d_atz.as<uint8_t>(), c->d_segs.as<Seg>(), nseg);
+                     INFL_BASE, d_file, c->d_atz.as<uint8_t>(), c->d_segs.as<Seg>(), nseg);
   kend(c);
   KCHECK("k_gather");
   HIPCHK(hipStreamSynchronize(c->st));
@@ -1708,6 +1880,14 @@ static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::
   *atz_len = out;
   c->stats.write_ms = ms_since(t0);
   return 0;
+}
+
+// ATZ_PIECES=k: the scan runs in k chunk ranges, each handed to the sweep as soon as its records
+// are inflated, so the sweep of the first pieces overlaps the scan of the rest (1: scan, then sweep)
+static uint32_t scan_pieces() {
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_PIECES"); v = e ? std::max(1, std::atoi(e)) : 1; }
+  return (uint32_t)v;
 }
 
 static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, uint64_t F, uint64_t* atz_len,
@@ -1718,15 +1898,36 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
   c->hfile = h; c->flen = F;
   struct Drop { atz_ctx* c; ~Drop() { c->hfile = nullptr; } } drop{c};   // h is the caller's, valid for this call only
   c->stats.file_bytes = F;
-  if (int r = scan_impl(c, h, d_file, F)) return r;
-  auto t1 = std::chrono::steady_clock::now();
-  if (int r = inflate_records(c, d_file, F)) return r;
-  c->stats.scan_ms += ms_since(t1);
+  c->recs.clear();
+  ScanState S;
+  if (int r = scan_plan(c, h, d_file, F, S)) return r;
+  const size_t n_max = S.max_records();
+  c->recs.reserve(n_max);
   std::vector<StreamState> ss;
-  if (int r = sweep_impl(c, d_file, ss)) return r;
+  SweepRun R;
+  SweepGuard guard{c, R};
+  if (int r = sweep_begin(c, d_file, ss, n_max, R)) return r;
+  const uint32_t nch = (uint32_t)S.chunks.size();
+  const uint32_t P = std::max<uint32_t>(1, std::min(scan_pieces(), nch));
+  while (c->slabs.size() < P) c->slabs.emplace_back(new DBuf());
+  double scan_busy = ms_since(t0);
+  for (uint32_t p = 0; p < P; p++) {
+    auto tp = std::chrono::steady_clock::now();
+    const uint32_t ja = (uint32_t)((uint64_t)nch * p / P), jb = (uint32_t)((uint64_t)nch * (p + 1) / P);
+    const size_t r0 = c->recs.size();
+    if (int r = scan_piece(c, h, d_file, S, ja, jb)) return r;
+    const size_t r1 = c->recs.size();
+    if (int r = inflate_records(c, d_file, F, r0, r1, *c->slabs[p])) return r;
+    if (int r = sweep_publish(c, R, r0, r1)) return r;
+    scan_busy += ms_since(tp);
+  }
+  c->stats.scan_ms = scan_busy;   // the scan thread's own time (the sweep runs beside it)
+  if (int r = sweep_finish(c, R)) return r;
+  c->infl_off.resize(c->recs.size());
+  c->adler.resize(c->recs.size());
   if (int r = write_impl(c, d_file, F, ss, atz_len)) return r;
   c->stats.n_streams = c->recs.size();
-  for (auto& s : ss) c->stats.n_recomp += s.recomp;
+  for (auto& s2 : ss) c->stats.n_recomp += s2.recomp;
   c->stats.atz_bytes = *atz_len;
   c->stats.total_ms = ms_since(t0);
   if (ss_out) ss_out->swap(ss);
@@ -1749,7 +1950,8 @@ static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, 
   if (int r = upload(c, c->d_infl, hb.data(), hb.size(), 65536)) return r;
   // fake record table for chain building
   c->recs.assign(n, Rec{});
-  c->infl_off = off;
+  c->infl_off.resize(n);
+  for (size_t s = 0; s < n; s++) c->infl_off[s] = (uint64_t)(uintptr_t)c->d_infl.p + off[s];
   c->adler.resize(n);
   for (size_t s = 0; s < n; s++) {
     c->recs[s].infl_len = ins[s].second;
@@ -1772,7 +1974,7 @@ static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, 
   HIPCHK(hipStreamSynchronize(p->st));
   std::vector<StreamDev> sd(n);
   for (size_t s = 0; s < n; s++) {
-    sd[s].orig_off = 0; sd[s].infl_off = off[s]; sd[s].comp_len = 0; sd[s].infl_len = ins[s].second;
+    sd[s].orig_off = 0; sd[s].infl_off = c->infl_off[s]; sd[s].comp_len = 0; sd[s].infl_len = ins[s].second;
   }
   if (int r = upload(c, c->d_streams, sd.data(), n * sizeof(StreamDev))) return r;
   if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;
@@ -1926,7 +2128,8 @@ int atz_sweep(atz_ctx_t* c, const atz_cand_t* cands, uint64_t n, atz_result_t* r
     (void)cands;
     c->scan_valid = false;   // inflate_records / the sweep overwrite the scan's device state
     c->hfile = nullptr;
-    if (int r = inflate_records(c, c->d_file.as<uint8_t>(), c->flen)) return r;
+    if (c->slabs.empty()) c->slabs.emplace_back(new DBuf());
+    if (int r = inflate_records(c, c->d_file.as<uint8_t>(), c->flen, 0, c->recs.size(), *c->slabs[0])) return r;
     std::vector<StreamState> ss;
     if (int r = sweep_impl(c, c->d_file.as<uint8_t>(), ss)) return r;
     uint64_t nd = 0;
