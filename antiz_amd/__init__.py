@@ -51,7 +51,8 @@ class Stats(C.Structure):
 
 EXPORTS = ["atz_open", "atz_close", "atz_strerror", "atz_free", "atz_default_opts", "atz_scan", "atz_sweep",
            "atz_precompress", "atz_precompress_device", "atz_reconstruct", "atz_deflate", "atz_deflate_batch",
-           "atz_inflate_batch", "atz_deflate_bound"]
+           "atz_inflate_batch", "atz_deflate_bound", "atz_shard_scan", "atz_shard_sweep", "atz_shard_piece",
+           "atz_shard_assemble"]
 
 _lib = None
 
@@ -89,6 +90,14 @@ def lib():
                                         C.POINTER(u64)]
         L.atz_deflate_bound.restype = u64
         L.atz_deflate_bound.argtypes = [u64, C.c_int, C.c_int]
+        L.atz_shard_scan.argtypes = [C.c_void_p, C.c_void_p, C.c_char_p, u64, C.c_int, C.c_int, C.POINTER(u8p),
+                                     C.POINTER(u64)]
+        L.atz_shard_sweep.argtypes = [C.c_void_p, C.c_void_p, C.c_char_p, u64, C.POINTER(C.c_char_p),
+                                      C.POINTER(u64), C.c_int, C.POINTER(u64), C.POINTER(u8p), C.POINTER(u64),
+                                      C.POINTER(u64), C.POINTER(Stats)]
+        L.atz_shard_piece.argtypes = [C.c_void_p, C.c_void_p]
+        L.atz_shard_assemble.argtypes = [C.c_void_p, C.c_void_p, u64, C.c_char_p, u64, u64, u64, C.c_void_p, u64,
+                                         C.POINTER(u64)]
         _lib = L
     return _lib
 
@@ -138,6 +147,41 @@ class Context:
         _check(L.atz_precompress_device(self.h, C.c_void_p(d_ptr), host_data, len(host_data), C.byref(dp),
                                         C.byref(n), C.byref(st)))
         return dp.value, n.value, st.as_dict()
+
+    # ---- one file over several GPUs (antiz_amd.shard drives these with torch.distributed) ----
+    def shard_scan(self, d_ptr, host_data, rank, world):
+        L = lib()
+        p = u8p()
+        n = u64(0)
+        _check(L.atz_shard_scan(self.h, C.c_void_p(d_ptr), host_data, len(host_data), rank, world, C.byref(p),
+                                C.byref(n)))
+        out = C.string_at(p, n.value)
+        L.atz_free(p)
+        return out
+
+    def shard_sweep(self, d_ptr, host_data, blobs):
+        """-> (piece_len, recomp flags (bytes, one per record of this rank), n_recomp, stats)"""
+        L = lib()
+        k = len(blobs)
+        bp = (C.c_char_p * k)(*blobs)
+        bl = (u64 * k)(*[len(b) for b in blobs])
+        pl, nf, nr = u64(0), u64(0), u64(0)
+        fp = u8p()
+        st = Stats()
+        _check(L.atz_shard_sweep(self.h, C.c_void_p(d_ptr), host_data, len(host_data), bp, bl, k, C.byref(pl),
+                                 C.byref(fp), C.byref(nf), C.byref(nr), C.byref(st)))
+        flags = C.string_at(fp, nf.value)
+        L.atz_free(fp)
+        return pl.value, flags, nr.value, st.as_dict()
+
+    def shard_piece(self, d_dst):
+        _check(lib().atz_shard_piece(self.h, C.c_void_p(d_dst)))
+
+    def shard_assemble(self, d_ptr, file_len, flags, n_recomp, pieces_len, d_atz, cap):
+        n = u64(0)
+        _check(lib().atz_shard_assemble(self.h, C.c_void_p(d_ptr), file_len, flags, len(flags), n_recomp,
+                                        pieces_len, C.c_void_p(d_atz), cap, C.byref(n)))
+        return n.value
 
     def reconstruct(self, atz):
         L = lib()

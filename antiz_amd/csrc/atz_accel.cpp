@@ -323,6 +323,17 @@ struct atz_ctx {
   std::vector<std::unique_ptr<Pipe>> pipes;
   std::vector<std::unique_ptr<DBuf>> slabs;   // inflated records, one allocation per scan piece
   size_t pipes_running = 1;
+  // multi-GPU precompress of one file (atz_shard_*): this rank's state between the calls
+  struct Shard {
+    std::shared_ptr<struct ScanState> S;
+    int rank = -1, world = 0;
+    uint32_t ja = 0, jb = 0;
+    uint64_t F = 0;
+    std::vector<std::pair<uint64_t, uint64_t>> all;   // every record of the file: (offset, comp_len)
+    uint64_t piece_len = 0;
+    int stage = 0;   // 1 scanned, 2 swept (piece in d_atz)
+    std::chrono::steady_clock::time_point t0;
+  } shard;
 };
 
 // kind: 0 trial, 1 inflate, 2 chains, 3 other, 4 match tables
@@ -634,9 +645,8 @@ static long scan_select(const ScanState& S, uint32_t j, uint64_t i0, std::vector
 }
 
 // Chunks [ja, jb): candidate inflates (their outputs kept in the arena, which is reset: earlier
-// pieces' records were gathered out of it already), speculative first continuations, then the
-// sequential replay (main.cpp:205-246 over searchInfile's chunk sequence), appending to c->recs.
-static int scan_piece(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, ScanState& S, uint32_t ja, uint32_t jb) {
+// pieces' records were gathered out of it already) and speculative first continuations.
+static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, ScanState& S, uint32_t ja, uint32_t jb) {
   auto tm_ = std::chrono::steady_clock::now();
   const std::vector<Chunk>& chunks = S.chunks;
   const size_t k0 = S.cbeg[ja], k1 = S.cbeg[jb];
@@ -722,7 +732,14 @@ static int scan_piece(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, ScanS
     c->stats.n_continuations += cj.size();
   }
   TMARK("scan: continuations");
-  // ---- sequential replay ----
+  return 0;
+}
+
+// The sequential replay of chunks [ja, jb) (main.cpp:205-246 over searchInfile's chunk sequence),
+// appending to c->recs; needs the candidate results and first continuations of those chunks.
+static int scan_replay(atz_ctx* c, const uint8_t* h, ScanState& S, uint32_t ja, uint32_t jb) {
+  auto tm_ = std::chrono::steady_clock::now();
+  const std::vector<Chunk>& chunks = S.chunks;
   ScanPend& pd = S.pd;
   auto materialize = [&](const ScanPend& q, std::vector<uint8_t>& v) {
     v.clear();
@@ -783,6 +800,11 @@ static int scan_piece(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, ScanS
   }
   TMARK("scan: replay");
   return 0;
+}
+
+static int scan_piece(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, ScanState& S, uint32_t ja, uint32_t jb) {
+  if (int r = scan_inflate(c, h, d_file, S, ja, jb)) return r;
+  return scan_replay(c, h, S, ja, jb);
 }
 
 // Every record, one piece.  (atz_scan; precompress_dev scans piece by piece while the sweep runs)
@@ -1811,28 +1833,12 @@ static int sweep_impl(atz_ctx* c, const uint8_t* d_file, std::vector<StreamState
 // Phase 4: ATZ1 assembled in HBM
 static void put8(std::vector<uint8_t>& m, uint64_t v) { uint8_t b[8]; std::memcpy(b, &v, 8); m.insert(m.end(), b, b + 8); }
 
-static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::vector<StreamState>& ss,
-                      uint64_t* atz_len) {
-  auto t0 = std::chrono::steady_clock::now();
-  std::vector<uint8_t> meta;
-  std::vector<Seg> segs;
-  uint64_t out = 0;
-  auto emit_meta = [&](const std::vector<uint8_t>& bytes) {
-    Seg g{0, 0, meta.size(), out, bytes.size()};
-    meta.insert(meta.end(), bytes.begin(), bytes.end());
-    segs.push_back(g);
-    out += bytes.size();
-  };
-  const size_t n = c->recs.size();
-  uint64_t nrec = 0;
-  for (size_t s = 0; s < n; s++) nrec += ss[s].recomp;
-  {
-    std::vector<uint8_t> h = {'A', 'T', 'Z', 1};
-    put8(h, 0); put8(h, F); put8(h, nrec);
-    emit_meta(h);
-  }
-  meta.reserve(meta.size() + nrec * 43 + 64);
-  segs.reserve(3 * n + 8);
+// Stream descriptors + inflated payloads of the recompressed streams, in record order
+// (writeStreamdesc, main.cpp:805-831): metadata bytes into `meta`, copy segments into `segs`.
+static void atz_descriptors(atz_ctx* c, const std::vector<StreamState>& ss, std::vector<uint8_t>& meta,
+                            std::vector<Seg>& segs, uint64_t& out) {
+  const size_t n = ss.size();
+  segs.reserve(segs.size() + 2 * n + 8);
   for (size_t s = 0; s < n; s++) {
     const StreamState& st = ss[s];
     if (!st.recomp) continue;
@@ -1849,34 +1855,73 @@ static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::
     }
     segs.push_back({0, 0, m0, out, meta.size() - m0});
     out += meta.size() - m0;
-    segs.push_back({1, 0, c->infl_off[s], out, r.infl_len});
+    segs.push_back({1, 0, c->infl_off[s], out, r.infl_len});   // absolute address (INFL_BASE)
     out += r.infl_len;
   }
+}
+
+// The residue (main.cpp:784-796): every file byte outside the recompressed streams, in order.
+// rec[k] = (offset, comp_len) of every record of the file, recomp[k] its decision.
+static int atz_residue(const std::vector<std::pair<uint64_t, uint64_t>>& rec, const uint8_t* recomp, uint64_t F,
+                       std::vector<Seg>& segs, uint64_t& out) {
   uint64_t lastos = 0, lastlen = 0;
-  for (size_t s = 0; s < n; s++) {
-    const Rec& r = c->recs[s];
-    if (lastos + lastlen != r.offset) {
-      if (r.offset < lastos + lastlen) return ATZ_E_REF_UB;   // copyto() with a wrapped length
-      segs.push_back({2, 0, lastos + lastlen, out, r.offset - (lastos + lastlen)});
-      out += r.offset - (lastos + lastlen);
+  for (size_t s = 0; s < rec.size(); s++) {
+    const uint64_t off = rec[s].first, len = rec[s].second;
+    if (lastos + lastlen != off) {
+      if (off < lastos + lastlen) return ATZ_E_REF_UB;   // copyto() with a wrapped length
+      segs.push_back({2, 0, lastos + lastlen, out, off - (lastos + lastlen)});
+      out += off - (lastos + lastlen);
     }
-    if (!ss[s].recomp) { segs.push_back({2, 0, r.offset, out, r.comp_len}); out += r.comp_len; }
-    lastos = r.offset; lastlen = r.comp_len;
+    if (!recomp[s]) { segs.push_back({2, 0, off, out, len}); out += len; }
+    lastos = off; lastlen = len;
   }
   if (lastos + lastlen < F) { segs.push_back({2, 0, lastos + lastlen, out, F - (lastos + lastlen)}); out += F - (lastos + lastlen); }
-  std::memcpy(meta.data() + 4, &out, 8);   // back-patched length (main.cpp:797-800)
+  return 0;
+}
+
+// k_gather of the segments into dst (device): metadata, resident payloads, file ranges
+static int gather_segments(atz_ctx* c, const uint8_t* d_file, const std::vector<uint8_t>& meta,
+                           const std::vector<Seg>& segs, uint8_t* dst) {
   if (int r = upload(c, c->d_meta, meta.data(), meta.size())) return r;
   if (int r = upload(c, c->d_segs, segs.data(), segs.size() * sizeof(Seg))) return r;
-  if (int r = c->d_atz.reserve(out + 4096)) return r;
-  uint32_t nseg = (uint32_t)segs.size();
-  uint32_t blocks = std::min<uint32_t>((nseg + 3) / 4, 65535u);
+  const uint32_t nseg = (uint32_t)segs.size();
+  const uint32_t blocks = std::min<uint32_t>((nseg + 3) / 4, 65535u);
   kbeg(c, 3);
   hipLaunchKernelGGL(k_gather, dim3(blocks ? blocks : 1), dim3(256), 0, c->st, c->d_meta.as<uint8_t>(),
-                     INFL_BASE, d_file, c->d_atz.as<uint8_t>(), c->d_segs.as<Seg>(), nseg);
+                     INFL_BASE, d_file, dst, c->d_segs.as<Seg>(), nseg);
   kend(c);
   KCHECK("k_gather");
   HIPCHK(hipStreamSynchronize(c->st));
   kcollect(c);
+  return 0;
+}
+
+static void atz_header(std::vector<uint8_t>& meta, uint64_t F, uint64_t nrec) {
+  const uint8_t h[4] = {'A', 'T', 'Z', 1};
+  meta.insert(meta.end(), h, h + 4);
+  put8(meta, 0); put8(meta, F); put8(meta, nrec);   // length back-patched (main.cpp:776, 797-800)
+}
+
+static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::vector<StreamState>& ss,
+                      uint64_t* atz_len) {
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint8_t> meta;
+  std::vector<Seg> segs;
+  const size_t n = c->recs.size();
+  uint64_t nrec = 0;
+  for (size_t s = 0; s < n; s++) nrec += ss[s].recomp;
+  atz_header(meta, F, nrec);
+  segs.push_back({0, 0, 0, 0, meta.size()});
+  uint64_t out = meta.size();
+  meta.reserve(meta.size() + nrec * 43 + 64);
+  atz_descriptors(c, ss, meta, segs, out);
+  std::vector<std::pair<uint64_t, uint64_t>> rec(n);
+  std::vector<uint8_t> rc(n);
+  for (size_t s = 0; s < n; s++) { rec[s] = {c->recs[s].offset, c->recs[s].comp_len}; rc[s] = ss[s].recomp; }
+  if (int r = atz_residue(rec, rc.data(), F, segs, out)) return r;
+  std::memcpy(meta.data() + 4, &out, 8);   // back-patched length (main.cpp:797-800)
+  if (int r = c->d_atz.reserve(out + 4096)) return r;
+  if (int r = gather_segments(c, d_file, meta, segs, c->d_atz.as<uint8_t>())) return r;
   *atz_len = out;
   c->stats.write_ms = ms_since(t0);
   return 0;
@@ -1893,7 +1938,7 @@ static uint32_t scan_pieces() {
 static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, uint64_t F, uint64_t* atz_len,
                            std::vector<StreamState>* ss_out) {
   auto t0 = std::chrono::steady_clock::now();
-  c->scan_valid = false;
+  c->scan_valid = false; c->shard.stage = 0;
   c->stats = atz_stats_t{};
   c->hfile = h; c->flen = F;
   struct Drop { atz_ctx* c; ~Drop() { c->hfile = nullptr; } } drop{c};   // h is the caller's, valid for this call only
@@ -1938,7 +1983,7 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
 // one-shot deflates (reconstruct / atz_deflate): trials with mode "full output" on a temporary stream set
 static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, uint64_t>>& ins,
                         const std::vector<uint32_t>& params, std::vector<std::vector<uint8_t>>& outs) {
-  c->scan_valid = false;   // recs / infl_off / adler / chain_off are replaced below
+  c->scan_valid = false; c->shard.stage = 0;   // recs / infl_off / adler / chain_off are replaced below
   const size_t n = ins.size();
   outs.assign(n, {});
   if (!n) return 0;
@@ -2009,6 +2054,156 @@ static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, 
       HIPCHK(hipMemcpy(o.data(), p->d_out.as<uint8_t>() + tr[k][q].out_off, o.size(), hipMemcpyDeviceToHost));
     }
   }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Multi-GPU precompress of one file: one process, context and GPU per rank, each
+// holding the whole file in HBM.  Rank r inflates the scan candidates of its contiguous chunk range
+// [nch*r/world, nch*(r+1)/world) (atz_shard_scan); the ranks all-gather those results, and each
+// replays the whole file's greedy selection from them (the same record list on every rank: the
+// replay is cheap host work, the inflates were the cost), then sweeps and writes the ATZ1
+// descriptors of the records its chunk range produced (atz_shard_sweep).  Rank 0 gathers the pieces
+// (RCCL over xGMI, by the caller) and adds the header and the residue (atz_shard_assemble).  The
+// result is byte-identical to a one-GPU precompress of the file.
+static constexpr uint64_t SHARD_MAGIC = 0x315348535a5441ull;   // "ATZSHS1"
+static constexpr size_t SHARD_HDR = 7;                          // words
+
+static void shard_range(uint32_t nch, int rank, int world, uint32_t& ja, uint32_t& jb) {
+  ja = (uint32_t)((uint64_t)nch * (uint64_t)rank / (uint64_t)world);
+  jb = (uint32_t)((uint64_t)nch * (uint64_t)(rank + 1) / (uint64_t)world);
+}
+
+static int shard_scan_impl(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, uint64_t F, int rank, int world,
+                           std::vector<uint64_t>& blob) {
+  atz_ctx::Shard& sh = c->shard;
+  sh = atz_ctx::Shard{};
+  sh.t0 = std::chrono::steady_clock::now();
+  c->scan_valid = false; c->shard.stage = 0;
+  c->stats = atz_stats_t{};
+  c->stats.file_bytes = F;
+  c->recs.clear();
+  sh.S = std::make_shared<ScanState>();
+  ScanState& S = *sh.S;
+  if (int r = scan_plan(c, h, d_file, F, S)) return r;
+  const uint32_t nch = (uint32_t)S.chunks.size();
+  shard_range(nch, rank, world, sh.ja, sh.jb);
+  if (int r = scan_inflate(c, h, d_file, S, sh.ja, sh.jb)) return r;
+  const size_t k0 = S.cbeg[sh.ja], k1 = S.cbeg[sh.jb];
+  blob.assign(SHARD_HDR, 0);
+  blob[0] = SHARD_MAGIC; blob[1] = (uint64_t)world; blob[2] = (uint64_t)rank; blob[3] = sh.ja; blob[4] = sh.jb;
+  blob[5] = k1 - k0; blob[6] = F;
+  blob.reserve(SHARD_HDR + 3 * (k1 - k0) + 4 * (sh.jb - sh.ja));
+  for (size_t k = k0; k < k1; k++) {
+    blob.push_back(S.cres[k].status); blob.push_back(S.cres[k].consumed); blob.push_back(S.cres[k].produced);
+  }
+  for (uint32_t j = sh.ja; j < sh.jb; j++) {
+    blob.push_back((uint64_t)(int64_t)S.pend0[j]);
+    blob.push_back(S.cont0[j].status); blob.push_back(S.cont0[j].consumed); blob.push_back(S.cont0[j].produced);
+  }
+  sh.rank = rank; sh.world = world; sh.F = F;
+  sh.stage = 1;
+  c->stats.scan_ms = ms_since(sh.t0);
+  return 0;
+}
+
+static int shard_sweep_impl(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, uint64_t F,
+                            const uint8_t* const* blobs, const uint64_t* blob_lens, int world,
+                            std::vector<uint8_t>& flags, uint64_t* n_recomp) {
+  atz_ctx::Shard& sh = c->shard;
+  if (sh.stage != 1 || world != sh.world || F != sh.F || !blobs || !blob_lens) return ATZ_E_ARG;
+  sh.stage = 0;
+  auto t1 = std::chrono::steady_clock::now();
+  ScanState& S = *sh.S;
+  const uint32_t nch = (uint32_t)S.chunks.size();
+  // the other ranks' candidate results and continuations (their arena outputs are theirs: the
+  // records this rank keeps come from its own candidates, or are inflated again from the file)
+  for (int q = 0; q < world; q++) {
+    if (q == sh.rank) continue;
+    if (!blobs[q] || blob_lens[q] % 8 || blob_lens[q] < SHARD_HDR * 8) return ATZ_E_ARG;
+    const size_t nw = blob_lens[q] / 8;
+    std::vector<uint64_t> b(nw);
+    std::memcpy(b.data(), blobs[q], nw * 8);
+    uint32_t ja, jb;
+    shard_range(nch, q, world, ja, jb);
+    const size_t k0 = S.cbeg[ja], k1 = S.cbeg[jb];
+    if (b[0] != SHARD_MAGIC || b[1] != (uint64_t)world || b[2] != (uint64_t)q || b[3] != ja || b[4] != jb ||
+        b[5] != k1 - k0 || b[6] != F || nw != SHARD_HDR + 3 * (k1 - k0) + 4 * (size_t)(jb - ja))
+      return ATZ_E_ARG;
+    const uint64_t* p = b.data() + SHARD_HDR;
+    for (size_t k = k0; k < k1; k++, p += 3) {
+      InfRes r{};
+      r.status = (uint32_t)p[0]; r.consumed = p[1]; r.produced = p[2]; r.arena_off = ARENA_NONE;
+      S.cres[k] = r;
+    }
+    for (uint32_t j = ja; j < jb; j++, p += 4) {
+      S.pend0[j] = (long)(int64_t)p[0];
+      InfRes r{};
+      r.status = (uint32_t)p[1]; r.consumed = p[2]; r.produced = p[3]; r.arena_off = ARENA_NONE;
+      S.cont0[j] = r;
+    }
+  }
+  // the whole file's replay; this rank keeps the records its chunk range produced
+  c->recs.clear();
+  c->recs.reserve(S.max_records());
+  c->hfile = h; c->flen = F;
+  struct Drop { atz_ctx* c; ~Drop() { c->hfile = nullptr; } } drop{c};
+  if (int r = scan_replay(c, h, S, 0, sh.ja)) return r;
+  const size_t r0 = c->recs.size();
+  if (int r = scan_replay(c, h, S, sh.ja, sh.jb)) return r;
+  const size_t r1 = c->recs.size();
+  if (int r = scan_replay(c, h, S, sh.jb, nch)) return r;
+  sh.all.resize(c->recs.size());
+  for (size_t s = 0; s < c->recs.size(); s++) sh.all[s] = {c->recs[s].offset, c->recs[s].comp_len};
+  c->recs.erase(c->recs.begin() + r1, c->recs.end());
+  c->recs.erase(c->recs.begin(), c->recs.begin() + r0);
+  const size_t n = c->recs.size();
+  if (c->slabs.empty()) c->slabs.emplace_back(new DBuf());
+  if (int r = inflate_records(c, d_file, F, 0, n, *c->slabs[0])) return r;
+  c->stats.scan_ms += ms_since(t1);
+  std::vector<StreamState> ss;
+  if (int r = sweep_impl(c, d_file, ss)) return r;
+  // this rank's piece: descriptors + payloads of its recompressed streams
+  auto t2 = std::chrono::steady_clock::now();
+  std::vector<uint8_t> meta;
+  std::vector<Seg> segs;
+  uint64_t out = 0;
+  atz_descriptors(c, ss, meta, segs, out);
+  if (int r = c->d_atz.reserve(out + 4096)) return r;
+  if (!segs.empty())
+    if (int r = gather_segments(c, d_file, meta, segs, c->d_atz.as<uint8_t>())) return r;
+  sh.piece_len = out;
+  flags.resize(n);
+  uint64_t nr = 0;
+  for (size_t s = 0; s < n; s++) { flags[s] = ss[s].recomp; nr += ss[s].recomp; }
+  *n_recomp = nr;
+  c->stats.n_streams = n;
+  c->stats.n_recomp = nr;
+  c->stats.atz_bytes = out;
+  c->stats.write_ms = ms_since(t2);
+  c->stats.total_ms = ms_since(sh.t0);
+  sh.stage = 2;
+  return 0;
+}
+
+static int shard_assemble_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const uint8_t* flags, uint64_t n_flags,
+                               uint64_t n_recomp, uint64_t pieces_len, uint8_t* d_atz, uint64_t cap, uint64_t* atz_len) {
+  atz_ctx::Shard& sh = c->shard;
+  if (sh.stage != 2 || sh.rank != 0 || F != sh.F || n_flags != sh.all.size() || (!flags && n_flags) || !d_atz)
+    return ATZ_E_ARG;
+  uint64_t nr = 0;
+  for (uint64_t s = 0; s < n_flags; s++) nr += flags[s] != 0;
+  if (nr != n_recomp) return ATZ_E_ARG;
+  std::vector<uint8_t> meta;
+  std::vector<Seg> segs;
+  atz_header(meta, F, n_recomp);
+  segs.push_back({0, 0, 0, 0, meta.size()});
+  uint64_t out = meta.size() + pieces_len;   // the pieces are already in place
+  if (int r = atz_residue(sh.all, flags, F, segs, out)) return r;
+  if (out > cap) return ATZ_E_ARG;
+  std::memcpy(meta.data() + 4, &out, 8);
+  if (int r = gather_segments(c, d_file, meta, segs, d_atz)) return r;
+  *atz_len = out;
   return 0;
 }
 
@@ -2092,7 +2287,7 @@ int atz_scan(atz_ctx_t* c, const uint8_t* file, uint64_t len, atz_cand_t** out, 
   return guarded([&]() -> int {
     (void)hipGetLastError();
     if (!c || (!file && len) || !out || !n) return ATZ_E_ARG;
-    c->scan_valid = false;
+    c->scan_valid = false; c->shard.stage = 0;
     if (int r = upload(c, c->d_file, file, len)) return r;
     c->hfile = file; c->flen = len;
     c->stats = atz_stats_t{};
@@ -2126,7 +2321,7 @@ int atz_sweep(atz_ctx_t* c, const atz_cand_t* cands, uint64_t n, atz_result_t* r
     // only on the records of this context's last atz_scan (nothing in between replaced them)
     if (!c || !res || !c->scan_valid || n != c->recs.size()) return ATZ_E_ARG;
     (void)cands;
-    c->scan_valid = false;   // inflate_records / the sweep overwrite the scan's device state
+    c->scan_valid = false; c->shard.stage = 0;   // inflate_records / the sweep overwrite the scan's device state
     c->hfile = nullptr;
     if (c->slabs.empty()) c->slabs.emplace_back(new DBuf());
     if (int r = inflate_records(c, c->d_file.as<uint8_t>(), c->flen, 0, c->recs.size(), *c->slabs[0])) return r;
@@ -2238,7 +2433,7 @@ int atz_inflate_batch(atz_ctx_t* c, const uint8_t* buf, uint64_t len, const uint
   return guarded([&]() -> int {
     (void)hipGetLastError();
     if (!c || (!buf && len)) return ATZ_E_ARG;
-    c->scan_valid = false;   // the arena holds the last scan's kept outputs
+    c->scan_valid = false; c->shard.stage = 0;   // the arena holds the last scan's kept outputs
     if (int r = upload(c, c->d_tmp, buf, len)) return r;
     std::vector<InfJob> jobs(n);
     for (uint64_t k = 0; k < n; k++) {
@@ -2254,13 +2449,70 @@ int atz_inflate_batch(atz_ctx_t* c, const uint8_t* buf, uint64_t len, const uint
   });
 }
 
+int atz_shard_scan(atz_ctx_t* c, const uint8_t* d_file, const uint8_t* h_file, uint64_t len, int rank, int world,
+                   uint8_t** blob, uint64_t* blob_len) {
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || !d_file || !h_file || !blob || !blob_len || world < 1 || rank < 0 || rank >= world) return ATZ_E_ARG;
+    std::vector<uint64_t> b;
+    if (int r = shard_scan_impl(c, d_file, h_file, len, rank, world, b)) { c->shard.stage = 0; return r; }
+    uint8_t* p = (uint8_t*)std::malloc(b.size() * 8 + 1);
+    if (!p) return ATZ_E_NOMEM;
+    std::memcpy(p, b.data(), b.size() * 8);
+    *blob = p; *blob_len = b.size() * 8;
+    return ATZ_OK;
+  });
+}
+
+int atz_shard_sweep(atz_ctx_t* c, const uint8_t* d_file, const uint8_t* h_file, uint64_t len,
+                    const uint8_t* const* blobs, const uint64_t* blob_lens, int world, uint64_t* piece_len,
+                    uint8_t** recomp_flags, uint64_t* n_flags, uint64_t* n_recomp, atz_stats_t* stats) {
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || !d_file || !h_file || !piece_len || !recomp_flags || !n_flags || !n_recomp) return ATZ_E_ARG;
+    std::vector<uint8_t> f;
+    if (int r = shard_sweep_impl(c, d_file, h_file, len, blobs, blob_lens, world, f, n_recomp)) {
+      c->shard.stage = 0;
+      return r;
+    }
+    uint8_t* p = (uint8_t*)std::malloc(f.size() + 1);
+    if (!p) return ATZ_E_NOMEM;
+    if (!f.empty()) std::memcpy(p, f.data(), f.size());
+    *recomp_flags = p; *n_flags = f.size();
+    *piece_len = c->shard.piece_len;
+    if (stats) *stats = c->stats;
+    return ATZ_OK;
+  });
+}
+
+int atz_shard_piece(atz_ctx_t* c, uint8_t* d_dst) {
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || c->shard.stage != 2 || (!d_dst && c->shard.piece_len)) return ATZ_E_ARG;
+    if (c->shard.piece_len)
+      HIPCHK(hipMemcpyAsync(d_dst, c->d_atz.p, c->shard.piece_len, hipMemcpyDeviceToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return ATZ_OK;
+  });
+}
+
+int atz_shard_assemble(atz_ctx_t* c, const uint8_t* d_file, uint64_t len, const uint8_t* recomp_flags,
+                       uint64_t n_flags, uint64_t n_recomp, uint64_t pieces_len, uint8_t* d_atz, uint64_t cap,
+                       uint64_t* atz_len) {
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || !d_file || !atz_len) return ATZ_E_ARG;
+    return shard_assemble_impl(c, d_file, len, recomp_flags, n_flags, n_recomp, pieces_len, d_atz, cap, atz_len);
+  });
+}
+
 static uint64_t rd8(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
 
 int atz_reconstruct(atz_ctx_t* c, const uint8_t* atz, uint64_t n, uint8_t** out, uint64_t* out_len) {
   return guarded([&]() -> int {
     (void)hipGetLastError();
     if (!c || !atz || !out || !out_len) return ATZ_E_ARG;
-    c->scan_valid = false;
+    c->scan_valid = false; c->shard.stage = 0;
     if (n < 28 || std::memcmp(atz, "ATZ\1", 4) != 0) return ATZ_E_FORMAT;   // main.cpp:1018-1021
     if (rd8(atz + 4) != n) return ATZ_E_FORMAT;                              // main.cpp:1022-1025
     const uint64_t origlen = rd8(atz + 12), nstrms = rd8(atz + 20);

@@ -1,0 +1,105 @@
+"""One file precompressed by several GPUs: one process and libatz_accel context per GPU,
+launched by torch.distributed (backend "nccl" = RCCL over xGMI; "gloo" for CPU-side tests).
+
+The reference is single-threaded (main.cpp has no threads); this is the build's own multi-GPU layer
+over the C ABI's atz_shard_* calls (include/atz_accel.h).  The data path has two exchanges:
+  1. all-gather of the scan-candidate results of every rank's chunk range (a few MB): each rank then
+     replays the reference's greedy chunk scan (main.cpp:205-246) for the whole file;
+  2. gather of the ATZ1 pieces (descriptors + inflated payloads of each rank's recompressed streams,
+     main.cpp:805-831) to rank 0, one point-to-point transfer per rank, received in place at its
+     offset in rank 0's output buffer; rank 0 then writes the header and the residue (main.cpp:764-801).
+The ATZ1 bytes equal the one-GPU result.
+"""
+import torch
+import torch.distributed as dist
+
+HEADER = 28   # "ATZ\x01" + file length + original length + stream count (main.cpp:770-776)
+
+
+def _device(group=None):
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+
+
+def allgather_bytes(b, group=None):
+    """Every rank's byte string, in rank order (variable sizes: lengths first, then padded payloads)."""
+    dev = _device(group)
+    world = dist.get_world_size(group)
+    n = torch.tensor([len(b)], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    m = max(max(ns), 1)
+    t = torch.zeros(m, dtype=torch.uint8, device=dev)
+    if b:
+        t[:len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    outs = [torch.empty(m, dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.all_gather(outs, t, group=group)
+    return [o[:k].cpu().numpy().tobytes() for o, k in zip(outs, ns)]
+
+
+def allgather_ints(vals, group=None):
+    """[[v0, v1, ...] of rank 0, of rank 1, ...] for a fixed-length list of ints per rank."""
+    dev = _device(group)
+    world = dist.get_world_size(group)
+    t = torch.tensor(vals, dtype=torch.int64, device=dev)
+    ts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(ts, t, group=group)
+    return [[int(x) for x in u.cpu().tolist()] for u in ts]
+
+
+def gather_pieces(ctx, piece_lens, out, out_device="cuda", group=None):
+    """Rank r's piece lands at out[HEADER + sum(piece_lens[:r])] on rank 0 (out: rank 0's output buffer;
+    pieces are staged through the host when the backend is gloo).  Zero-length pieces are not sent."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dev = _device(group)
+    offs = [HEADER]
+    for L in piece_lens[:-1]:
+        offs.append(offs[-1] + L)
+    if rank == 0:
+        if piece_lens[0]:
+            ctx.shard_piece(out.data_ptr() + offs[0])
+        ops, stage = [], []
+        for q in range(1, world):
+            if not piece_lens[q]:
+                continue
+            if out.device == dev:
+                buf = out[offs[q]:offs[q] + piece_lens[q]]
+            else:   # gloo: receive on the host, then copy into place
+                buf = torch.empty(piece_lens[q], dtype=torch.uint8, device=dev)
+                stage.append((q, buf))
+            ops.append(dist.P2POp(dist.irecv, buf, q, group=group))
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+        for q, buf in stage:
+            out[offs[q]:offs[q] + piece_lens[q]].copy_(buf)
+    elif piece_lens[rank]:
+        piece = torch.empty(piece_lens[rank], dtype=torch.uint8, device=out_device)
+        ctx.shard_piece(piece.data_ptr())
+        if piece.device != dev:
+            piece = piece.to(dev)
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, piece, 0, group=group)]):
+            w.wait()
+
+
+def precompress_sharded(ctx, d_file, data, group=None, out_device="cuda"):
+    """Precompress `data` (host bytes; d_file: the same bytes resident on this rank's GPU, a uint8 tensor
+    with >= 4096 bytes of slack) over every rank of `group`.  Returns (atz tensor, atz_len, stats) on
+    rank 0 (ATZ1 bytes = atz[:atz_len], on out_device) and (None, 0, stats) elsewhere."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dptr = d_file.data_ptr()
+    blob = ctx.shard_scan(dptr, data, rank, world)
+    blobs = allgather_bytes(blob, group)
+    piece_len, flags, n_recomp, st = ctx.shard_sweep(dptr, data, blobs)
+    meta = allgather_ints([piece_len, n_recomp, len(flags)], group)
+    piece_lens = [m[0] for m in meta]
+    all_flags = allgather_bytes(flags, group)
+    out = None
+    if rank == 0:
+        cap = HEADER + sum(piece_lens) + len(data) + 4096   # the residue is at most the whole file
+        out = torch.empty(cap, dtype=torch.uint8, device=out_device)
+    gather_pieces(ctx, piece_lens, out, out_device, group)
+    if rank != 0:
+        return None, 0, st
+    n = ctx.shard_assemble(dptr, len(data), b"".join(all_flags), sum(m[1] for m in meta), sum(piece_lens),
+                           out.data_ptr(), out.numel())
+    return out, n, st

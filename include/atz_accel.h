@@ -15,6 +15,8 @@
  *   atz_precompress Phase1 + Phase3 + Phase4 (writeATZfile, main.cpp:764-834)  main.cpp:1216-1221
  *   atz_reconstruct ATZreconstructor::reconstructATZ + doDeflate               main.cpp:869-1003
  *   atz_deflate     one deflateInit2/deflate(Z_FINISH)/deflateEnd              main.cpp:976-1003
+ *   atz_shard_*     the precompress of one file split over several GPUs (new: the reference is
+ *                   single-threaded)
  */
 #ifndef ATZ_ACCEL_H
 #define ATZ_ACCEL_H
@@ -133,6 +135,32 @@ int atz_deflate_batch(atz_ctx_t *ctx, const uint8_t *buf, uint64_t len, const ui
  * status[i] in {0 end, 1 error, 2 need input}, consumed[i] = zlib total_in, produced[i] = total_out. */
 int atz_inflate_batch(atz_ctx_t *ctx, const uint8_t *buf, uint64_t len, const uint64_t *offs,
                       const uint64_t *lens, uint64_t n, uint32_t *status, uint64_t *consumed, uint64_t *produced);
+
+/* ---- Multi-GPU precompress of ONE file -----------------------------------------
+ * One process, context and GPU per rank; every rank holds the whole file in HBM (d_file, >= 4096
+ * bytes of slack) and a host copy.  Replaces the same Phase 1 + 3 + 4 as atz_precompress, split
+ * where the ranks exchange data (the caller does the exchanges, e.g. torch.distributed over RCCL):
+ *   1. atz_shard_scan: inflates the scan candidates of this rank's chunk range -> *blob (atz_free).
+ *      Exchange: all-gather every rank's blob.
+ *   2. atz_shard_sweep: replays the whole file's greedy scan (main.cpp:205-246) from all blobs, then
+ *      sweeps (main.cpp:421-763) and writes the ATZ1 descriptors + payloads (writeStreamdesc,
+ *      main.cpp:805-831) of the records its chunk range produced: *piece_len bytes, kept in the
+ *      context.  *recomp_flags (atz_free) = one byte per such record.
+ *      Exchange: all-gather piece lengths, recomp counts and flags; gather the pieces to rank 0.
+ *   3. atz_shard_piece: device copy of this rank's piece to d_dst (rank 0: d_atz + 28 + the pieces
+ *      of the ranks before it).
+ *   4. rank 0, atz_shard_assemble: header + residue (writeATZfile, main.cpp:764-801) around the
+ *      pieces in d_atz (capacity cap); flags = every rank's, in rank order.
+ * The ATZ1 bytes are identical to atz_precompress of the same file on one GPU. */
+int atz_shard_scan(atz_ctx_t *ctx, const uint8_t *d_file, const uint8_t *h_file, uint64_t len, int rank, int world,
+                   uint8_t **blob, uint64_t *blob_len);
+int atz_shard_sweep(atz_ctx_t *ctx, const uint8_t *d_file, const uint8_t *h_file, uint64_t len,
+                    const uint8_t *const *blobs, const uint64_t *blob_lens, int world, uint64_t *piece_len,
+                    uint8_t **recomp_flags, uint64_t *n_flags, uint64_t *n_recomp, atz_stats_t *stats);
+int atz_shard_piece(atz_ctx_t *ctx, uint8_t *d_dst);
+int atz_shard_assemble(atz_ctx_t *ctx, const uint8_t *d_file, uint64_t len, const uint8_t *recomp_flags,
+                       uint64_t n_flags, uint64_t n_recomp, uint64_t pieces_len, uint8_t *d_atz, uint64_t cap,
+                       uint64_t *atz_len);
 
 /* zlib-1.2.8 deflate bound for the parameters (deflateBound, Z/deflate.c:566-621). */
 uint64_t atz_deflate_bound(uint64_t n, int window, int memlevel);

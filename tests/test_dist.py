@@ -59,3 +59,79 @@ def test_aggregate_world1():
     dt, value, sizes = bench.aggregate(1.5, 77, 3_000_000, 3, 1, "cpu")
     assert dt == 1.5 and sizes == [77]
     assert value == pytest.approx(3.0 / 0.5)
+
+
+# ---- antiz_amd.shard: one file over several ranks (host logic; the GPU test runs the real library) ----
+class FakeShardCtx:
+    """Stands in for a libatz_accel context: every shard_* call checks what the driver hands it and
+    writes recognisable bytes, so the exchanges and the placement of the pieces can be checked on CPU."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+        self.calls = []
+
+    def piece_len(self, r):
+        return [5, 0, 7, 3][r % 4]
+
+    def flags(self, r):
+        return bytes([1, 0, 1][: 1 + r % 3])
+
+    def shard_scan(self, dptr, data, rank, world):
+        assert (rank, world) == (self.rank, self.world)
+        self.calls.append("scan")
+        return b"blob-%d-" % rank + bytes(range(rank * 3))
+
+    def shard_sweep(self, dptr, data, blobs):
+        assert blobs == [b"blob-%d-" % q + bytes(range(q * 3)) for q in range(self.world)]
+        self.calls.append("sweep")
+        f = self.flags(self.rank)
+        return self.piece_len(self.rank), f, sum(f), {"rank": self.rank}
+
+    def shard_piece(self, dst):
+        import ctypes
+        n = self.piece_len(self.rank)
+        ctypes.memmove(dst, bytes([0x10 + self.rank]) * n, n)
+
+    def shard_assemble(self, dptr, flen, flags, n_recomp, pieces_len, d_atz, cap):
+        import ctypes
+        assert flags == b"".join(self.flags(q) for q in range(self.world))
+        assert n_recomp == sum(sum(self.flags(q)) for q in range(self.world))
+        assert pieces_len == sum(self.piece_len(q) for q in range(self.world))
+        assert cap >= 28 + pieces_len + flen
+        ctypes.memmove(d_atz, b"H" * 28, 28)
+        ctypes.memmove(d_atz + 28 + pieces_len, b"R" * flen, flen)
+        return 28 + pieces_len + flen
+
+
+def _shard_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from antiz_amd import shard
+    data = b"x" * 11
+    fake = FakeShardCtx(rank, world)
+    out, n, st = shard.precompress_sharded(fake, torch.zeros(16, dtype=torch.uint8), data, out_device="cpu")
+    q.put((rank, None if out is None else out[:n].numpy().tobytes(), n, st, fake.calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_precompress_sharded_exchanges(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (atz, n, st, calls) for r, atz, n, st, calls in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    fake = FakeShardCtx(0, world)
+    want = b"H" * 28 + b"".join(bytes([0x10 + r]) * fake.piece_len(r) for r in range(world)) + b"R" * 11
+    assert res[0][0] == want and res[0][1] == len(want)
+    for r in range(world):
+        assert res[r][2] == {"rank": r} and res[r][3] == ["scan", "sweep"]
+        if r:
+            assert res[r][0] is None and res[r][1] == 0
