@@ -121,6 +121,10 @@ def main():
     ap.add_argument("--cpu-sample-streams", type=int, default=8000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cache", default=os.environ.get("ATZ_BENCH_CACHE", "/tmp/atz_bench_cache"))
+    ap.add_argument("--mode", choices=("shards", "file"), default="shards",
+                    help="shards: every rank precompresses its own 1 GB file (weak scaling, no data-path "
+                         "collective); file: ONE 1 GB file split over the ranks (antiz_amd.shard: all-gather "
+                         "of scan results, RCCL gather of the ATZ1 pieces to rank 0; strong scaling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,14 +132,22 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # ATZ_BENCH_BACKEND=gloo: rehearsal of the N > 1 paths with several ranks on one GPU (RCCL refuses
+    # two ranks on one device); the driver's runs use the default, nccl = RCCL, one rank per GPU
+    backend = os.environ.get("ATZ_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
 
     import antiz_amd
     from antiz_amd import datagen
 
-    seed = 4 + rank
+    seed = 4 + rank if args.mode == "shards" else 4
     t0 = time.time()
     path = datagen.cached("c4", args.cache, seed=seed, n_streams=args.streams)
     with open(path, "rb") as f:
@@ -147,8 +159,16 @@ def main():
     torch.cuda.synchronize()
 
     ctx = antiz_amd.Context(device=local)
+    group = None
 
     def step():
+        if args.mode == "file":
+            from antiz_amd import shard
+            if world == 1:
+                dptr, n, st = ctx.precompress_device(dev.data_ptr(), data)
+                return n, st
+            out, n, st = shard.precompress_sharded(ctx, dev, data, group=group)
+            return n, st
         dptr, n, st = ctx.precompress_device(dev.data_ptr(), data)
         return n, st
 
@@ -166,7 +186,8 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt, value, atz_sizes = aggregate(dt, n, len(data), args.steps, world, "cuda")
+    dt, value, atz_sizes = aggregate(dt, n, len(data) if args.mode == "shards" else len(data) / world,
+                                     args.steps, world, red_dev)
     ms_per_step = dt * 1000.0 / args.steps
 
     last = stats[-1]
@@ -196,13 +217,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.mode == "shards" else "strong",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (antiz_amd.datagen C4, seed 4+rank; text from a seeded 20k-word vocabulary)",
-            "config": {"workload": "C4: %d zlib streams (clevel U1-9, memLevel U1-9, w15), %.3f GB per GPU, "
-                                   "default thresholds" % (args.streams, len(data) / 1e9),
-                       "streams_per_gpu": args.streams, "bytes_per_gpu": len(data), "parallelism": "stream-sharded dp%d" % world},
+            "data": "synthetic (antiz_amd.datagen C4, seed %s; text from a seeded 20k-word vocabulary)"
+                    % ("4+rank" if args.mode == "shards" else "4"),
+            "config": ({"workload": "C4: %d zlib streams (clevel U1-9, memLevel U1-9, w15), %.3f GB per GPU, "
+                                    "default thresholds" % (args.streams, len(data) / 1e9),
+                        "streams_per_gpu": args.streams, "bytes_per_gpu": len(data),
+                        "parallelism": "stream-sharded dp%d" % world}
+                       if args.mode == "shards" else
+                       {"workload": "C4: one file of %d zlib streams (clevel U1-9, memLevel U1-9, w15), %.3f GB, "
+                                    "split over %d GPUs, default thresholds" % (args.streams, len(data) / 1e9, world),
+                        "file_bytes": len(data), "parallelism": "chunk-range sharded x%d + RCCL gather" % world}),
             "roofline": roof,
             "cpu_baseline": cpu,
             "atz_bytes_per_rank": atz_sizes,
