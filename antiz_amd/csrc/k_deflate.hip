@@ -41,6 +41,9 @@
 #define ATZ_VISITED_MAX 8     // ... for levels whose chain budget is at most this (level 3's 32: measured slower)
 #endif
 // Per-step shader-clock counters in the parse loop (diagnostics; s_memtime also forces lgkmcnt waits).
+#ifndef ATZ_NOSLIDE_PATH
+#define ATZ_NOSLIDE_PATH 1    // parse: skip the window-slide checks for streams that never slide
+#endif
 #ifndef ATZ_STEP_CLOCKS
 #define ATZ_STEP_CLOCKS 0
 #endif
@@ -1663,6 +1666,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   if constexpr (KIND != 0) ring = (LDS uint64_t*)shm.ring;   // position & (RING_SLOW - 1); .x low, .y high
   const GLOBAL uint64_t* Rt = (const GLOBAL uint64_t*)(A.R + tr.r_off);
   const uint32_t n = z.n, wsz = z.wsize, maxd = z.maxdist, xlim = (uint32_t)tr.x_lim;
+  // fill_window never slides a stream of at most wsize + MAX_DIST bytes (Z/deflate.c:1419-1451:
+  // strstart stays below it), so S is 0 throughout and the NIL-after-slide checks drop out (wave-
+  // uniform: the walks skip them with a scalar branch)
+  const bool noslide = ATZ_NOSLIDE_PATH && n <= wsz + maxd;
   auto S_iter = [&](uint32_t S0, uint32_t q) -> uint32_t {   // S at an iteration at q >= one with S0
     uint32_t Sx = S0;
 #pragma unroll
@@ -1798,9 +1805,9 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         else {
           const uint64_t e64 = ring[x & (RING_SLOW - 1)];
           ex = (uint32_t)e64; ey = (uint32_t)(e64 >> 32);
-          Sx = S_iter(Sb, x);
+          if (!noslide) Sx = S_iter(Sb, x);
           bool hv = x + 3u <= n && (ey & 1u);
-          if (hv && Sx != 0 && x - Sx <= maxd) {   // hash_head == S is NIL after a slide
+          if (!noslide && hv && Sx != 0 && x - Sx <= maxd) {   // hash_head == S is NIL after a slide
             const uint32_t si = sidx[x];
             hv = (bpos[si] & BUCKET_FIRST) || (bpos[si - 1] & ~BUCKET_FIRST) != Sx;
           }
@@ -2050,7 +2057,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           const uint64_t e64 = ring[qq & (RING_SLOW - 1)];
           const uint32_t ex = (uint32_t)e64, ey = (uint32_t)(e64 >> 32);
           bool hv = qq + 3u <= n && (ey & 1u);
-          if (hv) {   // hash_head == S is NIL after a slide (only right after one)
+          if (!noslide && hv) {   // hash_head == S is NIL after a slide (only right after one)
             const uint32_t Sq = S_iter(Sb, qq);
             if (Sq != 0 && qq - Sq <= maxd) {
               const uint32_t si = sidx[qq];
