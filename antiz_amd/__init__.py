@@ -52,7 +52,7 @@ class Stats(C.Structure):
 EXPORTS = ["atz_open", "atz_close", "atz_strerror", "atz_free", "atz_default_opts", "atz_scan", "atz_sweep",
            "atz_precompress", "atz_precompress_device", "atz_reconstruct", "atz_deflate", "atz_deflate_batch",
            "atz_inflate_batch", "atz_deflate_bound", "atz_shard_scan", "atz_shard_sweep", "atz_shard_piece",
-           "atz_shard_assemble"]
+           "atz_shard_assemble", "atz_reconstruct_device"]
 
 _lib = None
 
@@ -96,6 +96,8 @@ def lib():
                                       C.POINTER(u64), C.c_int, C.POINTER(u64), C.POINTER(u8p), C.POINTER(u64),
                                       C.POINTER(u64), C.POINTER(Stats)]
         L.atz_shard_piece.argtypes = [C.c_void_p, C.c_void_p]
+        L.atz_reconstruct_device.argtypes = [C.c_void_p, C.c_void_p, C.c_char_p, u64, C.POINTER(C.c_void_p),
+                                             C.POINTER(u64)]
         L.atz_shard_assemble.argtypes = [C.c_void_p, C.c_void_p, u64, C.c_char_p, u64, u64, u64, C.c_void_p, u64,
                                          C.POINTER(u64)]
         _lib = L
@@ -191,6 +193,14 @@ class Context:
         out = C.string_at(p, n.value)
         L.atz_free(p)
         return out
+
+    def reconstruct_device(self, d_atz, host_atz):
+        """ATZ1 bytes already in HBM (d_atz: device pointer); returns (device pointer, length) of the original."""
+        dp = C.c_void_p()
+        n = u64(0)
+        _check(lib().atz_reconstruct_device(self.h, C.c_void_p(d_atz), host_atz, len(host_atz), C.byref(dp),
+                                            C.byref(n)))
+        return dp.value, n.value
 
     def scan(self, data):
         L = lib()

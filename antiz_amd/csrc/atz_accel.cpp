@@ -41,7 +41,7 @@ using namespace atz;
 namespace {
 
 struct Seg {           // k_gather segment
-  uint32_t src;        // 0 meta, 1 inflated, 2 file
+  uint32_t src;        // 0 meta, 1 inflated (absolute address), 2 file, 3 zeros
   uint32_t pad;
   uint64_t src_off, dst_off, len;
 };
@@ -52,10 +52,56 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ meta
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (uint32_t s = blockIdx.x * 4 + wave; s < nseg; s += gridDim.x * 4) {
     const Seg g = segs[s];
-    const uint8_t* src = (g.src == 0 ? meta : g.src == 1 ? infl : file) + g.src_off;
     uint8_t* d = dst + g.dst_off;
+    if (g.src == 3) {
+      for (uint64_t k = lane; k < g.len; k += 64) d[k] = 0;
+      continue;
+    }
+    const uint8_t* src = (g.src == 0 ? meta : g.src == 1 ? infl : file) + g.src_off;
     for (uint64_t k = lane; k < g.len; k += 64) d[k] = src[k];
   }
+}
+
+// Adler-32 (Z/adler32.c:65) of each stream at absolute address addr[j]: lane l sums its contiguous
+// share, the shares are joined in order with adler32_combine's arithmetic (Z/adler32.c:139-167).
+__global__ __launch_bounds__(64) void k_adler32(const uint64_t* __restrict__ addr, const uint64_t* __restrict__ len,
+                                               uint32_t* __restrict__ out, uint32_t n) {
+  const uint32_t j = blockIdx.x;
+  if (j >= n) return;
+  const uint32_t lane = threadIdx.x;
+  constexpr uint32_t BASE = 65521;
+  const uint8_t* p = (const uint8_t*)(uintptr_t)addr[j];
+  const uint64_t L = len[j], share = (L + 63) / 64;
+  const uint64_t b0 = share * lane < L ? share * lane : L, b1 = b0 + share < L ? b0 + share : L;
+  uint32_t a = 1, b = 0;
+  for (uint64_t i = b0; i < b1;) {
+    const uint64_t e = b1 - i < 5552 ? b1 : i + 5552;   // NMAX: no overflow before the reduction
+    for (; i < e; i++) { a += p[i]; b += a; }
+    a %= BASE; b %= BASE;
+  }
+  // join the 64 shares in lane order: adler(x||y) from adler(x), adler(y), len(y)
+  uint32_t acc = 1;   // adler of the empty prefix
+  for (int l = 0; l < 64; l++) {
+    const uint32_t ad2 = (uint32_t)__shfl((int)((b << 16) | a), l, 64);
+    const uint64_t ln2 = (uint64_t)__shfl((int)(uint32_t)(b1 - b0), l, 64);
+    const uint32_t rem = (uint32_t)(ln2 % BASE);
+    uint32_t sum1 = acc & 0xffff;
+    uint32_t sum2 = (uint32_t)(((uint64_t)rem * sum1) % BASE);
+    sum1 += (ad2 & 0xffff) + BASE - 1;
+    sum2 += ((acc >> 16) & 0xffff) + ((ad2 >> 16) & 0xffff) + BASE - rem;
+    if (sum1 >= BASE) sum1 -= BASE;
+    if (sum1 >= BASE) sum1 -= BASE;
+    if (sum2 >= ((uint32_t)BASE << 1)) sum2 -= ((uint32_t)BASE << 1);
+    if (sum2 >= BASE) sum2 -= BASE;
+    acc = sum1 | (sum2 << 16);
+  }
+  if (lane == 0) out[j] = acc;
+}
+
+// diff bytes of reconstructed streams (main.cpp:916-926): one byte per thread, distinct addresses
+__global__ __launch_bounds__(256) void k_patch(const uint64_t* __restrict__ at, const uint8_t* __restrict__ val, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) *(uint8_t*)(uintptr_t)at[i] = val[i];
 }
 
 // Mismatch list of a winning trial (main.cpp:699-714): positions i < min(L, C_s) with out[i] != orig[i],
@@ -302,6 +348,7 @@ struct atz_ctx {
   atz_opts_t o{};
   int dev = 0;
   hipStream_t st = nullptr;
+  DBuf d_rec, d_atzin;   // reconstructed original / uploaded ATZ1 bytes (atz_reconstruct*)
   DBuf d_file, d_pos, d_cnt, d_hbase, d_jobs, d_res, d_virt, d_infl, d_chains, d_heads, d_streams, d_trials,
       d_tres, d_out, d_syms, d_adler, d_meta, d_segs, d_atz, d_diffjobs, d_diffpos, d_diffval, d_diffcnt,
       d_cjobs, d_cjobs2, d_cjobs3, d_heads2, d_tmp, d_R, d_mjobs, d_ins, d_arena, d_arena_used;
@@ -504,6 +551,8 @@ static void chunk_bytes(const uint8_t* f, const Chunk& ch, std::vector<uint8_t>&
   v.push_back(ch.b0);
   v.insert(v.end(), f + ch.co + 1, f + ch.co + ch.len);
 }
+
+static uint64_t rd8(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
 
 // ATZ_TIMING=1: host phase timings on stderr
 #define TMARK(name)                                                                        \
@@ -1980,80 +2029,299 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// one-shot deflates (reconstruct / atz_deflate): trials with mode "full output" on a temporary stream set
+// one-shot deflates (reconstruct / atz_deflate): trials in "full output" mode on a temporary record
+// set.  Stream s lives at absolute device address addr[s] (256-byte aligned), len[s] bytes, with its
+// Adler-32 in adl[s] (host) or already in c->d_adler (adl empty).  The streams go in batches whose
+// match tables / symbol buffers / outputs fit the round budget; after each batch on_batch(s0, s1,
+// out_addr, out_len) sees the outputs (device addresses, valid until the next batch).
+static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std::vector<uint64_t>& len,
+                       const std::vector<uint32_t>& adl, const std::vector<uint32_t>& params,
+                       const std::function<int(size_t, size_t, const std::vector<uint64_t>&,
+                                               const std::vector<uint64_t>&)>& on_batch) {
+  c->scan_valid = false; c->shard.stage = 0;   // recs / infl_off / adler / chain_off are replaced below
+  const size_t n = addr.size();
+  if (!n) return 0;
+  c->recs.assign(n, Rec{});
+  c->infl_off = addr;
+  for (size_t s = 0; s < n; s++) {
+    if (len[s] >= (1ull << 31)) return ATZ_E_ARG;   // trial kernels keep 32-bit positions
+    c->recs[s].infl_len = len[s];
+  }
+  if (!adl.empty()) {
+    c->adler = adl;
+    if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;
+  }
+  std::vector<StreamDev> sd(n);
+  for (size_t s = 0; s < n; s++) { sd[s].orig_off = 0; sd[s].infl_off = addr[s]; sd[s].comp_len = 0; sd[s].infl_len = len[s]; }
+  if (int r = upload(c, c->d_streams, sd.data(), n * sizeof(StreamDev))) return r;
+  if (int r = ensure_pipes(c, 1)) return r;
+  HIPCHK(hipStreamSynchronize(c->st));   // tables (context stream) before the pipe's kernels
+  Pipe* p = c->pipes[0].get();
+  if (int r = c->d_tmp.reserve(4096)) return r;   // zero-length "file" for the compare side
+  const uint64_t budget = round_budget_bytes();
+  for (size_t s0 = 0; s0 < n;) {
+    // a batch: streams until the scratch estimate passes the budget (at least one)
+    size_t s1 = s0;
+    uint64_t bytes = 0;
+    while (s1 < n && (s1 == s0 || bytes <= budget)) {
+      const int m = (int)(params[s1] & 0xff);
+      bytes += 9 * len[s1] + 4 * (1ull << (m + 6)) + 4096;
+      s1++;
+    }
+    c->chain_off.assign(n, {});
+    for (auto& a2 : c->chain_off) a2.fill(~0ull);
+    p->streams.clear();
+    for (size_t s = s0; s < s1; s++) p->streams.push_back((uint32_t)s);
+    p->chain_used = 0;
+    p->chain_cap = CHAIN_CACHE_CAP;
+    std::vector<std::pair<uint32_t, int>> need;
+    for (size_t s = s0; s < s1; s++) if ((params[s] >> 16) > 0) need.push_back({(uint32_t)s, (int)(params[s] & 0xff)});
+    if (int r = ensure_chains(c, p, need)) return r;
+    HIPCHK(hipStreamSynchronize(p->st));
+    std::vector<Trial> tr[3];
+    std::vector<uint32_t> idx[3];
+    uint64_t out_tot = 0, sym_tot = 0;
+    for (size_t s = s0; s < s1; s++) {
+      const int cl = (int)(params[s] >> 16), w = (int)((params[s] >> 8) & 0xff), m = (int)(params[s] & 0xff);
+      Trial t{};
+      t.stream = (uint32_t)s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 1;
+      t.best_ident = 0; t.out_off = out_tot; t.out_cap = bound(len[s], w, m) + 64;
+      out_tot += (t.out_cap + 255) & ~255ull;
+      t.sym_off = sym_tot; sym_tot += 1ull << (m + 6);
+      const int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
+      if (kind) t.chain_off = c->chain_off[s][m];
+      tr[kind].push_back(t);
+      idx[kind].push_back((uint32_t)s);
+    }
+    if (int r = p->d_out.reserve(out_tot + 4096)) return r;
+    if (int r = p->d_syms.reserve(sym_tot * 4 + 4096)) return r;
+    SweepOpts so{0, 0, 0, 0};
+    std::vector<TrialRes> rr[3];
+    if (int r = run_trials(c, p, c->d_tmp.as<uint8_t>(), tr, so, rr)) return r;
+    std::vector<uint64_t> oa(s1 - s0), ol(s1 - s0);
+    const uint64_t ob = (uint64_t)(uintptr_t)p->d_out.p;
+    for (int k = 0; k < 3; k++)
+      for (size_t q = 0; q < tr[k].size(); q++) {
+        if (rr[k][q].state != TR_FULL) return ATZ_E_INTERNAL;
+        oa[idx[k][q] - s0] = ob + tr[k][q].out_off;
+        ol[idx[k][q] - s0] = rr[k][q].out_len;
+      }
+    if (int r = on_batch(s0, s1, oa, ol)) return r;
+    s0 = s1;
+  }
+  return 0;
+}
+
+// Host inputs (atz_deflate / atz_deflate_batch): uploaded 256-byte aligned, Adler-32 on the host.
 static int deflate_many(atz_ctx* c, const std::vector<std::pair<const uint8_t*, uint64_t>>& ins,
                         const std::vector<uint32_t>& params, std::vector<std::vector<uint8_t>>& outs) {
-  c->scan_valid = false; c->shard.stage = 0;   // recs / infl_off / adler / chain_off are replaced below
+  c->scan_valid = false; c->shard.stage = 0;
   const size_t n = ins.size();
   outs.assign(n, {});
   if (!n) return 0;
   uint64_t tot = 0;
-  std::vector<uint64_t> off(n);
+  std::vector<uint64_t> off(n), addr(n), len(n);
   for (size_t s = 0; s < n; s++) { off[s] = tot; tot += (ins[s].second + 255) & ~255ull; }
   std::vector<uint8_t> hb(tot + 8);
   for (size_t s = 0; s < n; s++) if (ins[s].second) std::memcpy(hb.data() + off[s], ins[s].first, ins[s].second);
   if (int r = upload(c, c->d_infl, hb.data(), hb.size(), 65536)) return r;
-  // fake record table for chain building
-  c->recs.assign(n, Rec{});
-  c->infl_off.resize(n);
-  for (size_t s = 0; s < n; s++) c->infl_off[s] = (uint64_t)(uintptr_t)c->d_infl.p + off[s];
-  c->adler.resize(n);
+  std::vector<uint32_t> adl(n);
   for (size_t s = 0; s < n; s++) {
-    c->recs[s].infl_len = ins[s].second;
+    addr[s] = (uint64_t)(uintptr_t)c->d_infl.p + off[s];
+    len[s] = ins[s].second;
     uint32_t a = 1, b = 0;
     for (uint64_t k = 0; k < ins[s].second; k++) { a = (a + ins[s].first[k]) % 65521; b = (b + a) % 65521; }
-    c->adler[s] = (b << 16) | a;
+    adl[s] = (b << 16) | a;
   }
-  c->chain_off.assign(n, {});
-  for (auto& a : c->chain_off) a.fill(~0ull);
-  if (int r = ensure_pipes(c, 1)) return r;
-  HIPCHK(hipStreamSynchronize(c->st));   // d_infl (context stream) before the pipe's kernels
-  Pipe* p = c->pipes[0].get();
-  p->streams.clear();
-  for (size_t s = 0; s < n; s++) p->streams.push_back((uint32_t)s);
-  p->chain_used = 0;
-  p->chain_cap = CHAIN_CACHE_CAP;
-  std::vector<std::pair<uint32_t, int>> need;
-  for (size_t s = 0; s < n; s++) if ((params[s] >> 16) > 0) need.push_back({(uint32_t)s, (int)(params[s] & 0xff)});
-  if (int r = ensure_chains(c, p, need)) return r;
-  HIPCHK(hipStreamSynchronize(p->st));
-  std::vector<StreamDev> sd(n);
-  for (size_t s = 0; s < n; s++) {
-    sd[s].orig_off = 0; sd[s].infl_off = c->infl_off[s]; sd[s].comp_len = 0; sd[s].infl_len = ins[s].second;
+  return deflate_dev(c, addr, len, adl, params,
+                     [&](size_t s0, size_t s1, const std::vector<uint64_t>& oa, const std::vector<uint64_t>& ol) -> int {
+                       for (size_t s = s0; s < s1; s++) {
+                         outs[s].resize(ol[s - s0]);
+                         if (ol[s - s0])
+                           HIPCHK(hipMemcpyAsync(outs[s].data(), (const void*)(uintptr_t)oa[s - s0], ol[s - s0],
+                                                 hipMemcpyDeviceToHost, c->pipes[0]->st));
+                       }
+                       HIPCHK(hipStreamSynchronize(c->pipes[0]->st));
+                       return 0;
+                     });
+}
+
+// ---------------------------------------------------------------------------------------------
+// Reconstruct (-r; ATZreconstructor::reconstructATZ, main.cpp:869-950) with the ATZ1 bytes resident
+// in HBM: descriptors parsed on the host (h: host copy), payloads gathered into an aligned slab,
+// Adler-32 on the device, one deflate per stream (doDeflate, main.cpp:976-1003), diff bytes patched
+// (main.cpp:916-926) and the original assembled in c->d_rec by k_gather: residue gaps, the first
+// comp_len bytes of each deflate output (zero-extended, as the reference's buffer is), the tail.
+struct AtzDesc { uint64_t off, cl, il, nd, fd, dpos, ipos; uint8_t c, w, m; };
+
+// ATZ1 parse with the reference's checks (main.cpp:1011-1063); every size field is bounded by the
+// bytes actually left before anything is sized from it (subtraction-only checks: no sum can wrap)
+static int parse_atz(const uint8_t* atz, uint64_t n, std::vector<AtzDesc>& d, uint64_t& origlen, uint64_t& residue) {
+  if (n < 28 || std::memcmp(atz, "ATZ\1", 4) != 0) return ATZ_E_FORMAT;   // main.cpp:1018-1021
+  if (rd8(atz + 4) != n) return ATZ_E_FORMAT;                              // main.cpp:1022-1025
+  origlen = rd8(atz + 12);
+  const uint64_t nstrms = rd8(atz + 20);
+  d.clear();
+  if (nstrms == 0) {
+    if (origlen > n - 28) return ATZ_E_FORMAT;
+    residue = 28;
+    return 0;
   }
-  if (int r = upload(c, c->d_streams, sd.data(), n * sizeof(StreamDev))) return r;
-  if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;
-  HIPCHK(hipStreamSynchronize(c->st));
-  std::vector<Trial> tr[3];
-  std::vector<uint32_t> idx[3];
-  uint64_t out_tot = 0, sym_tot = 0;
-  for (size_t s = 0; s < n; s++) {
-    int cl = (int)(params[s] >> 16), w = (int)((params[s] >> 8) & 0xff), m = (int)(params[s] & 0xff);
-    Trial t{};
-    t.stream = (uint32_t)s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 1;
-    t.best_ident = 0; t.out_off = out_tot; t.out_cap = bound(ins[s].second, w, m) + 64;
-    out_tot += (t.out_cap + 255) & ~255ull;
-    t.sym_off = sym_tot; sym_tot += 1ull << (m + 6);
-    int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
-    if (kind) t.chain_off = c->chain_off[s][m];
-    tr[kind].push_back(t);
-    idx[kind].push_back((uint32_t)s);
-  }
-  if (int r = p->d_out.reserve(out_tot + 4096)) return r;
-  if (int r = p->d_syms.reserve(sym_tot * 4 + 4096)) return r;
-  // zero-length "file" for the compare side
-  if (int r = c->d_tmp.reserve(4096)) return r;
-  SweepOpts so{0, 0, 0, 0};
-  std::vector<TrialRes> rr[3];
-  if (int r = run_trials(c, p, c->d_tmp.as<uint8_t>(), tr, so, rr)) return r;
-  for (int k = 0; k < 3; k++) {
-    for (size_t q = 0; q < tr[k].size(); q++) {
-      if (rr[k][q].state != TR_FULL) return ATZ_E_INTERNAL;
-      std::vector<uint8_t>& o = outs[idx[k][q]];
-      o.resize(rr[k][q].out_len);
-      HIPCHK(hipMemcpy(o.data(), p->d_out.as<uint8_t>() + tr[k][q].out_off, o.size(), hipMemcpyDeviceToHost));
+  if (nstrms > (n - 28) / 35) return ATZ_E_FORMAT;                       // each descriptor is >= 35 bytes
+  d.resize(nstrms);
+  uint64_t lastos = 28;                                                    // main.cpp:1031-1063
+  for (uint64_t j = 0; j < nstrms; j++) {
+    if (n - lastos < 35) return ATZ_E_FORMAT;
+    AtzDesc& x = d[j];
+    x.off = rd8(atz + lastos); x.cl = rd8(atz + lastos + 8); x.il = rd8(atz + lastos + 16);
+    x.c = atz[lastos + 24]; x.w = atz[lastos + 25]; x.m = atz[lastos + 26];
+    x.nd = rd8(atz + lastos + 27);
+    if (x.nd) {
+      if (n - lastos < 43) return ATZ_E_FORMAT;
+      const uint64_t room = n - lastos - 43;
+      if (x.nd > room / 9) return ATZ_E_FORMAT;
+      if (x.il > room - x.nd * 9) return ATZ_E_FORMAT;
+      x.fd = rd8(atz + lastos + 35); x.dpos = lastos + 43; x.ipos = lastos + 43 + x.nd * 9;
+      lastos = x.ipos + x.il;
+    } else {
+      if (x.il > n - lastos - 35) return ATZ_E_FORMAT;
+      x.fd = 0; x.dpos = 0; x.ipos = lastos + 35;
+      lastos = x.ipos + x.il;
     }
+    if (x.c > 9 || x.w < 8 || x.w > 15 || x.m < 1 || x.m > 9) return ATZ_E_REF_ABORT;
   }
+  // streams in file order, inside the original (the writer emits them so; a crafted file with
+  // overlapping or out-of-range streams is rejected before any buffer is sized)
+  uint64_t end = 0;
+  for (uint64_t j = 0; j < nstrms; j++) {
+    if (d[j].off < end || d[j].off > origlen || d[j].cl > origlen - d[j].off) return ATZ_E_FORMAT;
+    end = d[j].off + d[j].cl;
+  }
+  residue = lastos;
+  // the residue must hold every gap and the tail
+  uint64_t gaps = origlen;
+  for (const AtzDesc& x : d) gaps -= x.cl;
+  if (gaps > n - residue) return ATZ_E_FORMAT;
+  return 0;
+}
+
+static int reconstruct_dev(atz_ctx* c, const uint8_t* d_atz, const uint8_t* h, uint64_t n, uint64_t* out_len) {
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<AtzDesc> d;
+  uint64_t origlen = 0, residue = 0;
+  if (int r = parse_atz(h, n, d, origlen, residue)) return r;
+  if (int r = c->d_rec.reserve(origlen + 4096)) return r;
+  const size_t ns = d.size();
+  std::vector<Seg> segs;
+  std::vector<uint8_t> meta(8, 0);
+  uint64_t gapsum = 0, lo = 0, ll = 0, out = 0;
+  // residue gaps and the tail are plain copies; the streams' segments come from their batches
+  std::vector<uint64_t> rec_off(ns);
+  for (size_t j = 0; j < ns; j++) {
+    if (lo + ll != d[j].off) {
+      const uint64_t g = d[j].off - (lo + ll);   // > 0: offsets checked ascending
+      segs.push_back({2, 0, residue + gapsum, out, g});
+      gapsum += g; out += g;
+    }
+    rec_off[j] = out;
+    out += d[j].cl;
+    lo = d[j].off; ll = d[j].cl;
+  }
+  if (lo + ll < origlen) { segs.push_back({2, 0, residue + gapsum, out, origlen - (lo + ll)}); out += origlen - (lo + ll); }
+  if (out != origlen) return ATZ_E_FORMAT;
+  if (!segs.empty())
+    if (int r = gather_segments(c, d_atz, meta, segs, c->d_rec.as<uint8_t>())) return r;
+  if (ns) {
+    // payloads into an aligned slab (the trial kernels read 256-byte aligned streams)
+    std::vector<uint64_t> loc(ns), addr(ns), len(ns);
+    std::vector<uint32_t> params(ns);
+    uint64_t tot = 0;
+    for (size_t j = 0; j < ns; j++) { loc[j] = tot; tot += (d[j].il + 255) & ~255ull; }
+    if (c->slabs.empty()) c->slabs.emplace_back(new DBuf());
+    DBuf& slab = *c->slabs[0];
+    if (int r = slab.reserve(tot + 65536)) return r;
+    segs.clear();
+    for (size_t j = 0; j < ns; j++) {
+      if (d[j].il) segs.push_back({2, 0, d[j].ipos, loc[j], d[j].il});
+      addr[j] = (uint64_t)(uintptr_t)slab.p + loc[j];
+      len[j] = d[j].il;
+      const int w = d[j].w == 8 ? 9 : d[j].w;
+      params[j] = ((uint32_t)d[j].c << 16) | ((uint32_t)w << 8) | d[j].m;
+    }
+    if (!segs.empty())
+      if (int r = gather_segments(c, d_atz, meta, segs, slab.as<uint8_t>())) return r;
+    // Adler-32 of every payload on the device
+    if (int r = upload(c, c->d_pos, addr.data(), ns * 8)) return r;
+    if (int r = upload(c, c->d_hbase, len.data(), ns * 8)) return r;
+    if (int r = c->d_adler.reserve(ns * 4 + 4096)) return r;
+    kbeg(c, 3);
+    hipLaunchKernelGGL(k_adler32, dim3((uint32_t)ns), dim3(64), 0, c->st, c->d_pos.as<uint64_t>(),
+                       c->d_hbase.as<uint64_t>(), c->d_adler.as<uint32_t>(), (uint32_t)ns);
+    kend(c);
+    KCHECK("k_adler32");
+    HIPCHK(hipStreamSynchronize(c->st));
+    kcollect(c);
+    int rc2 = deflate_dev(c, addr, len, {}, params,
+                          [&](size_t s0, size_t s1, const std::vector<uint64_t>& oa, const std::vector<uint64_t>& ol) -> int {
+      std::vector<Seg> sg;
+      std::vector<uint64_t> pat;
+      std::vector<uint8_t> pval;
+      const uint64_t rb = (uint64_t)(uintptr_t)c->d_rec.p;
+      for (size_t j = s0; j < s1; j++) {
+        const uint64_t L = ol[j - s0], cl = d[j].cl;
+        if (L > cl + 65535) return ATZ_E_REF_ABORT;   // deflate() != Z_STREAM_END in a cl+65535 buffer
+        const uint64_t k = L < cl ? L : cl;
+        if (k) sg.push_back({1, 0, oa[j - s0], rec_off[j], k});
+        if (cl > k) sg.push_back({3, 0, 0, rec_off[j] + k, cl - k});   // zero-extended buffer
+        // diff bytes: positions first_diff + prefix sums of the deltas; only those < cl reach the output
+        if (d[j].nd) {
+          const size_t p0 = pat.size();
+          uint64_t sum = 0;
+          bool increasing = true;
+          for (uint64_t i = 0; i < d[j].nd; i++) {
+            const uint64_t delta = rd8(h + d[j].dpos + 8 * i);
+            const uint64_t at = d[j].fd + delta + sum;
+            sum += delta;
+            if (at < cl) {
+              if (pat.size() > p0 && rb + rec_off[j] + at <= pat.back()) increasing = false;
+              pat.push_back(rb + rec_off[j] + at);
+              pval.push_back(h[d[j].dpos + 8 * d[j].nd + i]);
+            }
+          }
+          if (!increasing) {   // crafted deltas (wrap / zero): the last write to a position wins
+            std::vector<std::pair<uint64_t, size_t>> o;
+            for (size_t q = p0; q < pat.size(); q++) o.push_back({pat[q], q});
+            std::stable_sort(o.begin(), o.end(), [](auto& a, auto& b) { return a.first < b.first; });
+            std::vector<uint64_t> pa;
+            std::vector<uint8_t> pv;
+            for (size_t q = 0; q < o.size(); q++)
+              if (q + 1 == o.size() || o[q + 1].first != o[q].first) { pa.push_back(o[q].first); pv.push_back(pval[o[q].second]); }
+            pat.resize(p0); pval.resize(p0);
+            pat.insert(pat.end(), pa.begin(), pa.end());
+            pval.insert(pval.end(), pv.begin(), pv.end());
+          }
+        }
+      }
+      if (!sg.empty())
+        if (int r = gather_segments(c, d_atz, meta, sg, c->d_rec.as<uint8_t>())) return r;
+      if (!pat.empty()) {
+        if (int r = upload(c, c->d_diffjobs, pat.data(), pat.size() * 8)) return r;
+        if (int r = upload(c, c->d_diffval, pval.data(), pval.size())) return r;
+        kbeg(c, 3);
+        hipLaunchKernelGGL(k_patch, dim3((uint32_t)((pat.size() + 255) / 256)), dim3(256), 0, c->st,
+                           c->d_diffjobs.as<uint64_t>(), c->d_diffval.as<uint8_t>(), (uint64_t)pat.size());
+        kend(c);
+        KCHECK("k_patch");
+        HIPCHK(hipStreamSynchronize(c->st));
+        kcollect(c);
+      }
+      return 0;
+    });
+    if (rc2) return rc2;
+  }
+  HIPCHK(hipStreamSynchronize(c->st));
+  *out_len = origlen;
+  c->stats.total_ms = ms_since(t0);
   return 0;
 }
 
@@ -2506,102 +2774,36 @@ int atz_shard_assemble(atz_ctx_t* c, const uint8_t* d_file, uint64_t len, const 
   });
 }
 
-static uint64_t rd8(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
 
 int atz_reconstruct(atz_ctx_t* c, const uint8_t* atz, uint64_t n, uint8_t** out, uint64_t* out_len) {
   return guarded([&]() -> int {
     (void)hipGetLastError();
     if (!c || !atz || !out || !out_len) return ATZ_E_ARG;
     c->scan_valid = false; c->shard.stage = 0;
-    if (n < 28 || std::memcmp(atz, "ATZ\1", 4) != 0) return ATZ_E_FORMAT;   // main.cpp:1018-1021
-    if (rd8(atz + 4) != n) return ATZ_E_FORMAT;                              // main.cpp:1022-1025
-    const uint64_t origlen = rd8(atz + 12), nstrms = rd8(atz + 20);
-    // Every size field below comes from the file.  The reference trusts them (a huge count or
-    // length makes its new[] throw and the process abort); here each is bounded by the bytes that
-    // are actually left, with subtraction-only checks (no sum can wrap), before anything is sized
-    // from it.
-    std::vector<uint8_t> o;
-    if (nstrms == 0) {
-      if (origlen > n - 28) return ATZ_E_FORMAT;
-      o.assign(atz + 28, atz + 28 + origlen);
-    } else {
-      if (nstrms > (n - 28) / 35) return ATZ_E_FORMAT;                     // each descriptor is >= 35 bytes
-      struct D { uint64_t off, cl, il, nd, fd, dpos, ipos; uint8_t c, w, m; };
-      std::vector<D> d(nstrms);
-      uint64_t lastos = 28;                                                  // main.cpp:1031-1063
-      for (uint64_t j = 0; j < nstrms; j++) {
-        if (n - lastos < 35) return ATZ_E_FORMAT;
-        D& x = d[j];
-        x.off = rd8(atz + lastos); x.cl = rd8(atz + lastos + 8); x.il = rd8(atz + lastos + 16);
-        x.c = atz[lastos + 24]; x.w = atz[lastos + 25]; x.m = atz[lastos + 26];
-        x.nd = rd8(atz + lastos + 27);
-        if (x.nd) {
-          if (n - lastos < 43) return ATZ_E_FORMAT;
-          const uint64_t room = n - lastos - 43;
-          if (x.nd > room / 9) return ATZ_E_FORMAT;
-          if (x.il > room - x.nd * 9) return ATZ_E_FORMAT;
-          x.fd = rd8(atz + lastos + 35); x.dpos = lastos + 43; x.ipos = lastos + 43 + x.nd * 9;
-          lastos = x.ipos + x.il;
-        } else {
-          if (x.il > n - lastos - 35) return ATZ_E_FORMAT;
-          x.fd = 0; x.dpos = 0; x.ipos = lastos + 35;
-          lastos = x.ipos + x.il;
-        }
-        if (x.c > 9 || x.w < 8 || x.w > 15 || x.m < 1 || x.m > 9) return ATZ_E_REF_ABORT;
-      }
-      // streams in file order, inside the original (the writer emits them so; a crafted file
-      // with overlapping or out-of-range streams is rejected before any buffer is sized)
-      uint64_t end = 0;
-      for (uint64_t j = 0; j < nstrms; j++) {
-        if (d[j].off < end || d[j].off > origlen || d[j].cl > origlen - d[j].off) return ATZ_E_FORMAT;
-        end = d[j].off + d[j].cl;
-      }
-      std::vector<std::pair<const uint8_t*, uint64_t>> ins;
-      std::vector<uint32_t> params;
-      for (auto& x : d) {
-        ins.push_back({atz + x.ipos, x.il});
-        int w = x.w == 8 ? 9 : x.w;
-        params.push_back(((uint32_t)x.c << 16) | ((uint32_t)w << 8) | x.m);
-      }
-      std::vector<std::vector<uint8_t>> defl;
-      if (int r = deflate_many(c, ins, params, defl)) return r;
-      const uint64_t residue = lastos;
-      uint64_t gapsum = 0, lo = 0, ll = 0;
-      auto take = [&](uint64_t g) -> bool {   // g residue bytes: inside the file?
-        return residue + gapsum <= n && g <= n - (residue + gapsum);
-      };
-      for (uint64_t j = 0; j < nstrms; j++) {
-        if (lo + ll != d[j].off) {
-          const uint64_t g = d[j].off - (lo + ll);   // > 0: offsets checked ascending above
-          if (!take(g)) return ATZ_E_FORMAT;
-          o.insert(o.end(), atz + residue + gapsum, atz + residue + gapsum + g);
-          gapsum += g;
-        }
-        std::vector<uint8_t>& cb = defl[j];
-        if (cb.size() > d[j].cl + 65535) return ATZ_E_REF_ABORT;            // deflate() != Z_STREAM_END
-        cb.resize(std::max<uint64_t>(cb.size(), d[j].cl), 0);
-        if (d[j].nd) {
-          uint64_t sum = 0;
-          for (uint64_t i = 0; i < d[j].nd; i++) {
-            uint64_t delta = rd8(atz + d[j].dpos + 8 * i);
-            uint64_t at = d[j].fd + delta + sum;
-            if (at < cb.size()) cb[at] = atz[d[j].dpos + 8 * d[j].nd + i];
-            sum += delta;
-          }
-        }
-        o.insert(o.end(), cb.begin(), cb.begin() + d[j].cl);
-        lo = d[j].off; ll = d[j].cl;
-      }
-      if (lo + ll < origlen) {
-        const uint64_t t = origlen - (lo + ll);
-        if (!take(t)) return ATZ_E_FORMAT;
-        o.insert(o.end(), atz + residue + gapsum, atz + residue + gapsum + t);
-      }
-    }
-    uint8_t* h = (uint8_t*)std::malloc(o.size() + 1);
+    if (int r = upload(c, c->d_atzin, atz, n)) return r;
+    uint64_t L = 0;
+    if (int r = reconstruct_dev(c, c->d_atzin.as<uint8_t>(), atz, n, &L)) return r;
+    uint8_t* h = (uint8_t*)std::malloc(L + 1);
     if (!h) return ATZ_E_NOMEM;
-    if (!o.empty()) std::memcpy(h, o.data(), o.size());
-    *out = h; *out_len = o.size();
+    if (L) {
+      const hipError_t e = hipMemcpy(h, c->d_rec.p, L, hipMemcpyDeviceToHost);
+      if (e != hipSuccess) { std::free(h); return ATZ_E_HIP; }
+    }
+    *out = h; *out_len = L;
+    return ATZ_OK;
+  });
+}
+
+int atz_reconstruct_device(atz_ctx_t* c, const uint8_t* d_atz, const uint8_t* h_atz, uint64_t len,
+                           const uint8_t** d_out, uint64_t* out_len) {
+  return guarded([&]() -> int {
+    (void)hipGetLastError();
+    if (!c || !d_atz || !h_atz || !d_out || !out_len) return ATZ_E_ARG;
+    c->scan_valid = false; c->shard.stage = 0;
+    uint64_t L = 0;
+    if (int r = reconstruct_dev(c, d_atz, h_atz, len, &L)) return r;
+    *d_out = c->d_rec.as<uint8_t>();
+    *out_len = L;
     return ATZ_OK;
   });
 }

@@ -77,6 +77,15 @@ def cpu_baseline(n_streams, seed, ctx):
                       "%.1f s wall" % (n_streams, len(data) / 1e6, seed, dt)}
 
 
+def hip_copy(dst, src, n):
+    """hipMemcpy(dst, src, n, hipMemcpyDefault) on raw pointers (the library's device buffers)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    if n and hip.hipMemcpy(dst, src, n, 4) != 0:
+        raise RuntimeError("hipMemcpy failed")
+
+
 def pmc_traffic():
     """HBM traffic per k_trial launch from the newest committed PMC summary (profiles/r*_pmc_traffic.json:
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench, FETCH_SIZE doubled per the
@@ -120,6 +129,7 @@ def main():
     ap.add_argument("--streams", type=int, default=100000, help="streams per rank (C4: 100000 = 1 GB)")
     ap.add_argument("--cpu-sample-streams", type=int, default=8000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-recon", action="store_true", help="skip the reconstruct (-r / verify) measurement")
     ap.add_argument("--cache", default=os.environ.get("ATZ_BENCH_CACHE", "/tmp/atz_bench_cache"))
     ap.add_argument("--mode", choices=("shards", "file"), default="shards",
                     help="shards: every rank precompresses its own 1 GB file (weak scaling, no data-path "
@@ -203,6 +213,31 @@ def main():
             "avg_launch_ms": round(last["k_trial_ms"] / launches, 4),
             "alg_bytes_per_launch": int(alg / launches)}
 
+    # reconstruct (-r, and precompress's default verify: main.cpp:869-950, 1173-1203) of the last ATZ1,
+    # resident in HBM; not part of the metric: its own wall time, and the round trip checked
+    recon = None
+    if args.mode == "shards" and not args.no_recon:
+        dptr, alen, _ = ctx.precompress_device(dev.data_ptr(), data)
+        hdev = torch.empty(alen + 4096, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        hip_copy(hdev.data_ptr(), dptr, alen)                # the context reuses its own ATZ1 buffer
+        h = torch.empty(alen, dtype=torch.uint8)
+        hip_copy(h.data_ptr(), dptr, alen)
+        hb = h.numpy().tobytes()
+        ctx.reconstruct_device(hdev.data_ptr(), hb)          # warm-up (buffers sized)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            rp, rl = ctx.reconstruct_device(hdev.data_ptr(), hb)
+        torch.cuda.synchronize()
+        rdt = (time.perf_counter() - t1) / args.steps
+        back = torch.empty(rl, dtype=torch.uint8)
+        hip_copy(back.data_ptr(), rp, rl)
+        recon = {"value": round(len(data) / 1e6 / rdt, 3), "unit": "MB/s restored (ATZ1 resident in HBM)",
+                 "ms_per_step": round(rdt * 1000, 2), "atz_bytes": alen,
+                 "identical": rl == len(data) and back.numpy().tobytes() == data}
+        del hdev
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_sample_streams, seed, ctx)
@@ -233,6 +268,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "atz_bytes_per_rank": atz_sizes,
+            "reconstruct": recon,
             "detail": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in last.items()},
         }
         print(json.dumps(out), flush=True)

@@ -121,6 +121,11 @@ int atz_precompress_device(atz_ctx_t *ctx, const uint8_t *d_file, const uint8_t 
 /* -r: rebuild the original from ATZ1 bytes. *out (atz_free). */
 int atz_reconstruct(atz_ctx_t *ctx, const uint8_t *atz, uint64_t len, uint8_t **out, uint64_t *out_len);
 
+/* -r with the ATZ1 bytes resident in HBM (d_atz, >= 4096 bytes of slack; h_atz: host copy for the
+ * descriptors): *d_out (device, owned by ctx, valid until the next call) receives *out_len bytes. */
+int atz_reconstruct_device(atz_ctx_t *ctx, const uint8_t *d_atz, const uint8_t *h_atz, uint64_t len,
+                           const uint8_t **d_out, uint64_t *out_len);
+
 /* One zlib-1.2.8-exact deflate (level 0..9, windowBits 9..15, memLevel 1..9, default strategy). */
 int atz_deflate(atz_ctx_t *ctx, const uint8_t *in, uint64_t in_len, int clevel, int window, int memlevel,
                 uint8_t *out, uint64_t out_cap, uint64_t *out_len);

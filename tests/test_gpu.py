@@ -340,3 +340,57 @@ def test_sweep_requires_its_scan(atz):
         recs = c.scan(data)
         res, _ = c.sweep()
         assert len(res) == len(recs) == 20
+
+
+def _atz1(orig_len, streams, residue):
+    """ATZ1 bytes: streams = [(offset, comp_len, infl bytes, c, w, m, first_diff,
+    deltas, values)]."""
+    import struct
+    body = b""
+    for off, cl, infl, c, w, m, fd, deltas, vals in streams:
+        body += struct.pack("<QQQBBBQ", off, cl, len(infl), c, w, m, len(deltas))
+        if deltas:
+            body += struct.pack("<Q", fd) + b"".join(struct.pack("<Q", d) for d in deltas) + bytes(vals)
+        body += infl
+    n = 28 + len(body) + len(residue)
+    return b"ATZ\x01" + struct.pack("<QQQ", n, orig_len, len(streams)) + body + residue
+
+
+def test_reconstruct_diffs_match_oracle(atz):
+    """Diff patching (main.cpp:916-926) as the reference does it, sequentially: repeated positions
+    (zero deltas) keep the last byte, positions past comp_len are dropped, a stream whose deflate is
+    shorter than comp_len is zero-extended; every case against the oracle's reconstruct."""
+    r = random.Random(11)
+    text = _libs.text(r, 3000)
+    real, _ = _libs.ora_deflate(text, 6, 15, 8)
+    cl = len(real)
+    cases = [
+        (0, [0, 3, 0, 0, 7], [1, 2, 3, 4, 5]),                 # repeated positions: the last byte wins
+        (5, [0, 1, 1, 1 << 40], [9, 8, 7, 6]),                  # a position far past comp_len
+        (cl - 2, [0, 1, 5], [0xaa, 0xbb, 0xcc]),                # straddling the end of the stream
+    ]
+    with atz.Context() as c:
+        for fd, deltas, vals in cases:
+            for extra in (0, 9):                               # comp_len beyond the deflate output: zeros
+                a = _atz1(cl + extra + 6, [(2, cl + extra, text, 6, 15, 8, fd, deltas, vals)], b"ab" + b"wxyz")
+                rc, want = _libs.ora_reconstruct(a)
+                assert rc == 0
+                assert c.reconstruct(a) == want
+
+
+def test_reconstruct_device_roundtrip(atz):
+    """atz_reconstruct_device (ATZ1 resident in HBM) restores a C4 slice bit-exactly."""
+    import torch
+    import ctypes
+    from antiz_amd import datagen
+    data = datagen.gen_c4(seed=13, n_streams=300)
+    with atz.Context() as c:
+        a, _ = c.precompress(data)
+        d = torch.frombuffer(bytearray(a) + bytearray(4096), dtype=torch.uint8).to("cuda")
+        p, n = c.reconstruct_device(d.data_ptr(), a)
+        assert n == len(data)
+        out = torch.empty(n, dtype=torch.uint8)
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        assert hip.hipMemcpy(out.data_ptr(), p, n, 4) == 0
+        assert out.numpy().tobytes() == data
