@@ -380,17 +380,23 @@ def test_reconstruct_diffs_match_oracle(atz):
 
 def test_reconstruct_device_roundtrip(atz):
     """atz_reconstruct_device (ATZ1 resident in HBM) restores a C4 slice bit-exactly."""
-    import torch
     import ctypes
     from antiz_amd import datagen
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
     data = datagen.gen_c4(seed=13, n_streams=300)
     with atz.Context() as c:
         a, _ = c.precompress(data)
-        d = torch.frombuffer(bytearray(a) + bytearray(4096), dtype=torch.uint8).to("cuda")
-        p, n = c.reconstruct_device(d.data_ptr(), a)
-        assert n == len(data)
-        out = torch.empty(n, dtype=torch.uint8)
-        hip = ctypes.CDLL("libamdhip64.so")
-        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-        assert hip.hipMemcpy(out.data_ptr(), p, n, 4) == 0
-        assert out.numpy().tobytes() == data
+        d = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(d), len(a) + 4096) == 0
+        try:
+            assert hip.hipMemcpy(d, a, len(a), 1) == 0                      # host to device
+            p, n = c.reconstruct_device(d.value, a)
+            assert n == len(data)
+            out = ctypes.create_string_buffer(n)
+            assert hip.hipMemcpy(out, p, n, 2) == 0                         # device to host
+            assert out.raw == data
+        finally:
+            hip.hipFree(d)
