@@ -58,7 +58,38 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ meta
       continue;
     }
     const uint8_t* src = (g.src == 0 ? meta : g.src == 1 ? infl : file) + g.src_off;
-    for (uint64_t k = lane; k < g.len; k += 64) d[k] = src[k];
+    // head bytes up to a 4-byte aligned destination, then aligned dword stores whose 4 source bytes
+    // come from two aligned dword loads joined with v_alignbyte (any source alignment), 4 per lane in
+    // flight, then the tail bytes.  Reads stay inside the source's 4-byte words that hold segment bytes.
+    const uint64_t head = ((4 - ((uintptr_t)d & 3)) & 3) < g.len ? ((4 - ((uintptr_t)d & 3)) & 3) : g.len;
+    if (lane < head) d[lane] = src[lane];
+    const uint64_t nw = (g.len - head) >> 2;
+    const uint8_t* sb = src + head;
+    uint32_t* dw = (uint32_t*)(d + head);
+    const uint32_t sh = (uint32_t)((uintptr_t)sb & 3);
+    const uint32_t* sw = (const uint32_t*)(sb - sh);
+    if (sh == 0) {
+      uint64_t k = lane;
+      for (; k + 192 < nw; k += 256) {
+        const uint32_t a0 = sw[k], a1 = sw[k + 64], a2 = sw[k + 128], a3 = sw[k + 192];
+        dw[k] = a0; dw[k + 64] = a1; dw[k + 128] = a2; dw[k + 192] = a3;
+      }
+      for (; k < nw; k += 64) dw[k] = sw[k];
+    } else {
+      // word k takes source bytes [4k, 4k + 4): aligned words k and k + 1 (the last of which holds a
+      // segment byte whenever it is read: 4k + 3 < 4 nw <= len - head)
+      uint64_t k = lane;
+      for (; k + 192 < nw; k += 256) {
+        uint32_t lo[4], hi[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) { lo[u] = sw[k + 64 * u]; hi[u] = sw[k + 64 * u + 1]; }
+#pragma unroll
+        for (int u = 0; u < 4; u++) dw[k + 64 * u] = __builtin_amdgcn_alignbyte(hi[u], lo[u], sh);
+      }
+      for (; k < nw; k += 64) dw[k] = __builtin_amdgcn_alignbyte(sw[k + 1], sw[k], sh);
+    }
+    const uint64_t t0 = head + 4 * nw;
+    if (t0 + lane < g.len) d[t0 + lane] = src[t0 + lane];
   }
 }
 
@@ -736,34 +767,44 @@ static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, Sca
   TMARK("scan: candidate inflate");
   {
     // speculative first continuations: pending candidate of chunk j (selection from 0) + buffer
-    // j+1, assembled in HBM by k_gather from file ranges and the chunks' buffer[0] bytes
-    std::vector<Seg> segs;
-    std::vector<uint8_t> meta;
-    uint64_t out = 0;
-    auto add_file = [&](uint64_t off, uint64_t len) { if (len) segs.push_back({2, 0, off, out, len}); out += len; };
-    auto add_byte = [&](uint8_t b) { segs.push_back({0, 0, meta.size(), out, 1}); meta.push_back(b); out += 1; };
-    std::vector<InfJob> cj;
-    std::vector<uint32_t> cj_chunk;
+    // j+1, assembled in HBM by k_gather from file ranges and the chunks' buffer[0] bytes.  The first
+    // pass offers only the first CONT_PROBE bytes of buffer j+1: a decode that ends or fails inside
+    // them reads no further, so its status / total_in / total_out are those of the whole buffer
+    // (k_inflate consumes exactly zlib's bits); one that runs out of input is decoded again with
+    // the whole buffer.  (The duplicated byte almost always ends them within a few symbols.)
+    static constexpr uint64_t CONT_PROBE = 65536;
+    std::vector<uint32_t> todo;
     for (uint32_t j = ja; j < jb && j + 1 < chunks.size(); j++) {
       const long k = scan_select(S, j, 0, nullptr);
       S.pend0[j] = k;
-      if (k < 0) continue;
-      const ScanCand& cd = S.cands[k];
-      const Chunk& ch = chunks[j];
-      const Chunk& nx = chunks[j + 1];
-      InfJob jb2;
-      jb2.in_off = out;
-      if (cd.i == 0) { add_byte(ch.b0); add_file(ch.co + 1, ch.len - 1); }
-      else add_file(ch.co + cd.i, ch.len - cd.i);
-      add_byte(nx.b0);
-      add_file(nx.co + 1, nx.len - 1);
-      // output into arena slots after the scan's (small-ring decoder); the bytes are not used
-      jb2.in_len = out - jb2.in_off; jb2.out_off = ARENA_OUT; jb2.out_cap = ARENA_SLOT;
-      cj.push_back(jb2);
-      cj_chunk.push_back(j);
-      out = (out + 3) & ~3ull;
+      if (k >= 0) todo.push_back(j);
     }
-    if (!cj.empty()) {
+    c->stats.n_continuations += todo.size();
+    for (int pass = 0; pass < 2 && !todo.empty(); pass++) {
+      std::vector<Seg> segs;
+      std::vector<uint8_t> meta;
+      uint64_t out = 0;
+      auto add_file = [&](uint64_t off, uint64_t len) { if (len) segs.push_back({2, 0, off, out, len}); out += len; };
+      auto add_byte = [&](uint8_t b) { segs.push_back({0, 0, meta.size(), out, 1}); meta.push_back(b); out += 1; };
+      std::vector<InfJob> cj;
+      std::vector<bool> cut;
+      for (uint32_t j : todo) {
+        const ScanCand& cd = S.cands[S.pend0[j]];
+        const Chunk& ch = chunks[j];
+        const Chunk& nx = chunks[j + 1];
+        InfJob jb2;
+        jb2.in_off = out;
+        if (cd.i == 0) { add_byte(ch.b0); add_file(ch.co + 1, ch.len - 1); }
+        else add_file(ch.co + cd.i, ch.len - cd.i);
+        add_byte(nx.b0);
+        const uint64_t take = (pass == 0 && nx.len - 1 > CONT_PROBE) ? CONT_PROBE : nx.len - 1;
+        add_file(nx.co + 1, take);
+        cut.push_back(take < nx.len - 1);
+        // output into arena slots after the scan's (small-ring decoder); the bytes are not used
+        jb2.in_len = out - jb2.in_off; jb2.out_off = ARENA_OUT; jb2.out_cap = ARENA_SLOT;
+        cj.push_back(jb2);
+        out = (out + 3) & ~3ull;
+      }
       if (int r = upload(c, c->d_meta, meta.data(), meta.size())) return r;
       if (int r = upload(c, c->d_segs, segs.data(), segs.size() * sizeof(Seg))) return r;
       if (int r = c->d_virt.reserve(out + 4096)) return r;
@@ -776,9 +817,24 @@ static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, Sca
       KCHECK("k_gather");
       std::vector<InfRes> cr;
       if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, cj, cr, S.arena_cap, false, false)) return r;
-      for (size_t q = 0; q < cj.size(); q++) S.cont0[cj_chunk[q]] = cr[q];
+      if (timing_on()) {
+        uint64_t cmax = 0, ctot = 0, pmax = 0, st[4] = {};
+        for (size_t q = 0; q < cj.size(); q++) {
+          cmax = std::max<uint64_t>(cmax, cr[q].consumed); ctot += cr[q].consumed;
+          pmax = std::max<uint64_t>(pmax, cr[q].produced); st[cr[q].status & 3]++;
+        }
+        std::fprintf(stderr, "atz: continuations pass %d: %zu jobs, %.1f MB offered, consumed %.1f MB (max %llu), "
+                     "max produced %llu, end/error/need/retry %llu/%llu/%llu/%llu, %.2f ms\n", pass, cj.size(), out / 1e6,
+                     ctot / 1e6, (unsigned long long)cmax, (unsigned long long)pmax, (unsigned long long)st[0],
+                     (unsigned long long)st[1], (unsigned long long)st[2], (unsigned long long)st[3], ms_since(tm_));
+      }
+      std::vector<uint32_t> again;
+      for (size_t q = 0; q < cj.size(); q++) {
+        if (cut[q] && cr[q].status == INF_NEED) again.push_back(todo[q]);
+        else S.cont0[todo[q]] = cr[q];
+      }
+      todo.swap(again);
     }
-    c->stats.n_continuations += cj.size();
   }
   TMARK("scan: continuations");
   return 0;
@@ -872,6 +928,7 @@ static int scan_impl(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
 // c->infl_off[s] receives the absolute device address of stream s's bytes (the kernels take a null
 // base), so the records of different pieces may live in different allocations.
 static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F, size_t r0, size_t r1, DBuf& slab) {
+  auto tm_ = std::chrono::steady_clock::now();
   if (c->infl_off.size() < r1) c->infl_off.resize(r1);
   if (c->adler.size() < r1) c->adler.resize(r1);
   uint64_t tot = 0;
@@ -912,8 +969,16 @@ static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F, size_t
     kend(c);
     KCHECK("k_gather");
   }
+  TMARK("records: arena gather launch");
   std::vector<InfRes> res;
   if (int r = run_inflate_jobs(c, d_file, slab.as<uint8_t>(), jobs, res)) return r;
+  if (timing_on()) {
+    uint64_t mx = 0, tot = 0;
+    for (const InfJob& jb : jobs) { mx = std::max(mx, jb.in_len); tot += jb.in_len; }
+    std::fprintf(stderr, "atz: records: %zu re-inflated (%llu input bytes, largest %llu)\n", jobs.size(),
+                 (unsigned long long)tot, (unsigned long long)mx);
+  }
+  TMARK("records: re-inflate");
   for (size_t q = 0; q < jobs.size(); q++) {
     const size_t s = job_rec[q];
     if (res[q].status != INF_END) return ATZ_E_REF_ABORT;          // main.cpp:450-452

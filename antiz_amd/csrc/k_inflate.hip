@@ -33,6 +33,9 @@ static_assert(INF_RING_SMALL >= 2048 && (INF_RING_SMALL & (INF_RING_SMALL - 1)) 
 #ifndef INF_SMALL_WAVES
 #define INF_SMALL_WAVES 6   // waves per SIMD the small-ring decoder is register-bounded for (8 KiB ring: 3 -> 183 ms, 4 -> 154 ms)
 #endif
+#ifndef ATZ_INF_LITRUN
+#define ATZ_INF_LITRUN 1   // fast path: short-code literals in their own tight loop
+#endif
 #ifndef ATZ_INF_CLOCKS
 #define ATZ_INF_CLOCKS 0                       // 1: per-job clocks and symbol counts in InfRes
 #endif
@@ -516,6 +519,18 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
         while (used <= rem) {
           if (bc <= 32) refill1();
           uint32_t e = rl(lh.root, (uint32_t)bb & 63);
+#if ATZ_INF_LITRUN
+          // literal run: root-table literals (codes of <= 6 bits: e in [1, 4095]) go straight into
+          // the stage in a loop with one back edge; anything else takes the general path below
+          while (e - 1u < 4095u && used <= rem) {
+            const uint32_t L = e & 15;
+            bb >>= L; bc -= L; used += L;
+            put_lit(e >> 4);
+            if (bc <= 32) refill1();
+            e = rl(lh.root, (uint32_t)bb & 63);
+          }
+          if (used > rem) break;   // rc == 1: the careful path resumes at this symbol
+#endif
           if (e == 0) {   // code longer than 6 bits (or invalid): canonical compare
             const uint32_t v = __builtin_bitreverse32((uint32_t)bb) >> 17;
             const uint32_t c = v >> lsh;

@@ -400,3 +400,21 @@ def test_reconstruct_device_roundtrip(atz):
             assert out.raw == data
         finally:
             hip.hipFree(d)
+
+
+def test_continuation_probe_rerun(atz):
+    """A stored-block stream that crosses a chunk boundary decodes straight through the duplicated
+    byte (main.cpp:207-217), past the continuation probe: the scan must redo it with the whole next
+    buffer and end exactly where the reference does."""
+    import zlib
+    r = random.Random(5)
+    noise = bytes(r.getrandbits(8) for _ in range(150000))
+    payload = bytes(r.getrandbits(8) for _ in range(400000))
+    for body in (zlib.compress(payload, 0), zlib.compress(payload[:120000], 0)):
+        data = noise + body + b"tail" * 10
+        for cs in (200000, 524288):
+            rc, want, _ = _libs.ora_precompress(data, chunksize=cs)
+            assert rc == 0
+            with atz.Context(chunksize=cs) as c:
+                got, _ = c.precompress(data)
+            assert got == want
