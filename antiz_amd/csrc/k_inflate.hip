@@ -522,11 +522,17 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
 #if ATZ_INF_LITRUN
           // literal run: root-table literals (codes of <= 6 bits: e in [1, 4095]) go straight into
           // the stage in a loop with one back edge; anything else takes the general path below
-          while (e - 1u < 4095u && used <= rem) {
+          // The end-of-fast-path test (used <= rem: >= 64 input bits left) is made at each refill
+          // only: after a passing test the buffer holds bits up to at most 64 past it, all before
+          // the input limit, and the run decodes only buffered bits (bc > 32 at every lookup).
+          while (e - 1u < 4095u) {
             const uint32_t L = e & 15;
             bb >>= L; bc -= L; used += L;
             put_lit(e >> 4);
-            if (bc <= 32) refill1();
+            if (bc <= 32) {
+              if (used > rem) break;
+              refill1();
+            }
             e = rl(lh.root, (uint32_t)bb & 63);
           }
           if (used > rem) break;   // rc == 1: the careful path resumes at this symbol
