@@ -201,6 +201,25 @@ struct DBuf {              // device buffer, freed with its owner (atz_close del
   template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+struct PinBuf {            // pinned host buffer that kernels write directly
+  void* p = nullptr;
+  size_t n = 0;
+  PinBuf() = default;
+  PinBuf(const PinBuf&) = delete;
+  PinBuf& operator=(const PinBuf&) = delete;
+  ~PinBuf() { if (p) (void)hipHostFree(p); }
+  int reserve(size_t need) {
+    if (need <= n) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    if (hipHostMalloc(&p, need, hipHostMallocDefault) != hipSuccess) return ATZ_E_NOMEM;
+    n = need;
+    return 0;
+  }
+  template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
 struct Rec {
   uint64_t offset, comp_len, infl_len;
   int type;
@@ -220,6 +239,7 @@ struct StreamState {
   std::vector<uint8_t> diffval;
   uint32_t trials = 0;
   uint32_t full_at = ~0u;         // list index whose trial ran past its match-table prefix: rerun with a full table
+  int32_t rp = -1;                // symbol-replay entries (levels 6-9) in the owning pipe's rp_pool
   bool recomp = false;
 };
 
@@ -337,6 +357,14 @@ struct KTimer {   // HIP events bracketing kernel launches on the library stream
 // One HIP stream of sweep work with its own buffers, kernel timers and counters.  The sweep runs
 // several pipes at once (streams partitioned among them, one host thread each), so one pipe's
 // launch tails, host gaps and small launches overlap another's work.
+// A saved symbol sequence of (stream, level 6-9): the first slow trial at that level whose chain walks
+// cannot reach their budget saves it; later ones at that level replay it (see trial_body).
+struct RpEntry {
+  uint64_t addr = 0;      // device address of the arena slot (n + 64 symbols)
+  uint32_t nsym = 0, flags = 0;
+  uint8_t state = 0;      // 0 free (addr may hold a reusable slot), 1 a saving trial in flight, 2 saved
+  uint8_t window = 0;
+};
 struct ChainBufs {   // bucket-build job lists and scratch (one set per HIP stream that builds)
   DBuf d_cjobs, d_cjobs2, d_cjobs3, d_heads, d_heads2;
 };
@@ -354,6 +382,10 @@ struct Pipe {
   KTimer pkt;
   uint64_t chain_used = 0, chain_cap = 0;
   std::vector<uint32_t> streams;   // the streams whose chain tables this pipe owns
+  // symbol replay: saved sequences (bump arena, reset per sweep) and per-stream entries
+  DBuf d_rp;
+  uint64_t rp_used = 0;
+  std::vector<std::array<struct RpEntry, 4>> rp_pool;
   // streams handed to this pipe (scan pieces arrive while it sweeps); closed after the last piece
   std::mutex in_mu;
   std::condition_variable in_cv;
@@ -398,6 +430,9 @@ struct atz_ctx {
   atz_stats_t stats{};
   // chains cache: per record and memlevel
   std::vector<std::array<uint64_t, 10>> chain_off;   // offset in the owning pipe's d_chains
+  // deepest bucket - 1 per (stream, memLevel) at [10 s + m], written by k_buckets_sort into pinned
+  // host memory (~0: not built yet); read after the building stream has been synchronised
+  PinBuf depth_pin;
   std::vector<std::unique_ptr<Pipe>> pipes;
   std::vector<std::unique_ptr<DBuf>> slabs;   // inflated records, one allocation per scan piece
   size_t pipes_running = 1;
@@ -1049,7 +1084,7 @@ static int chains_prefetch(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint
 }
 // The kernels of one set of bucket jobs, writing at chains + job.chain_off.
 static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<ChainJob> jobs, uint32_t* chains,
-                             bool use_sort) {
+                             bool use_sort, uint32_t* depth = nullptr) {
   // streams whose sort fits in LDS: k_buckets_sort (every memLevel), one launch per size class
   if (use_sort) {
     static const uint32_t cls[] = {4096, 8192, 12288, 16384, 20480, BSORT_MAX_NPAD};
@@ -1073,7 +1108,7 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
         kbeg(c, 2);
         hipLaunchKernelGGL(k_buckets_sort, dim3((uint32_t)cnt), dim3(BSORT_THREADS), bsort_lds_bytes(cls[k]), c->st,
                            INFL_BASE, B.d_cjobs2.as<ChainJob>() + beg[k], chains,
-                           (uint32_t)cnt);
+                           (uint32_t)cnt, depth);
         kend(c);
         KCHECK("k_buckets_sort");
       }
@@ -1181,6 +1216,8 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     jb.chain_off = c->chain_used;
     jb.memlevel = (uint32_t)m;
     jb.slot = 0;
+    jb.dslot = 10 * s + (uint32_t)m;
+    jb.pad_ = 0;
     x->chain_off[s][m] = c->chain_used;
     c->chain_used += words(s);
     jobs.push_back(jb);
@@ -1202,7 +1239,7 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     c->d_chains.p = np;
     c->d_chains.n = cap;
   }
-  if (int r = build_bucket_jobs(x, c, B, jobs, c->d_chains.as<uint32_t>(), bucket_sort_on())) return r;
+  if (int r = build_bucket_jobs(x, c, B, jobs, c->d_chains.as<uint32_t>(), bucket_sort_on(), x->depth_pin.as<uint32_t>())) return r;
   if (bucket_verify() && bucket_sort_on()) {
     // diagnostics (ATZ_BUCKETS_VERIFY=1): the same jobs again on the in-order kernels, compared
     uint64_t tot = 0;
@@ -1210,7 +1247,7 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     for (ChainJob& jb : alt) { jb.chain_off = tot; tot += 2 * ((jb.n + 63) & ~63ull); }
     DBuf tmp;
     if (int r = tmp.reserve(tot * 4 + 4096)) return r;
-    if (int r = build_bucket_jobs(x, c, B, alt, tmp.as<uint32_t>(), false)) return r;
+    if (int r = build_bucket_jobs(x, c, B, alt, tmp.as<uint32_t>(), false, nullptr)) return r;
     std::vector<uint32_t> h1(tot), h2(tot);
     for (size_t k = 0; k < jobs.size(); k++)
       HIPCHK(hipMemcpyAsync(h1.data() + alt[k].chain_off, c->d_chains.as<uint32_t>() + jobs[k].chain_off,
@@ -1354,7 +1391,8 @@ static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Tri
     std::vector<uint64_t> key(n);
     for (size_t q = 0; q < n; q++) {
       const Trial& t = tr[k][q];
-      key[q] = x->recs[t.stream].infl_len * (uint64_t)(k == 1 ? 3 : 1) * (uint64_t)(10 - t.memlevel);
+      key[q] = x->recs[t.stream].infl_len * (uint64_t)(k == 1 ? 3 : 1) * (uint64_t)(10 - t.memlevel) *
+               (uint64_t)((t.mode & 8) ? 1 : 4);   // replays skip the match walks
       perm[k][q] = (uint32_t)q;
     }
     std::stable_sort(perm[k].begin(), perm[k].end(), [&](uint32_t a, uint32_t b) { return key[a] > key[b]; });
@@ -1383,6 +1421,7 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
   for (int k = 1; k < 3; k++)
     for (Trial& t : tr[k]) {
       const uint64_t n = x->recs[t.stream].infl_len;
+      if (t.mode & 8) { t.r_off = 0; t.x_lim = n; continue; }   // replays: no match table
       t.r_off = r_tot;
       r_tot += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
       t.x_lim = ((t.mode & 3) || full) ? n : match_prefix(n, t.memlevel);
@@ -1503,6 +1542,54 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
   return 0;
 }
 
+// ATZ_REPLAY=0 disables symbol replay (every slow trial parses); 2 saves sequences but never replays
+// them (diagnostics)
+static int replay_mode() {
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_REPLAY"); v = e ? std::atoi(e) : 1; }
+  return v;
+}
+static bool replay_on() { return replay_mode() != 0; }
+static constexpr uint64_t RP_ARENA_CAP = 24ull << 30;   // saved sequences, all pipes
+
+// Symbol replay (trial_body): a slow trial at level L in {6..9}, window w, memLevel m whose deepest
+// bucket holds at most B/4 + 1 positions (B = max_chain of L) walks exactly like every other memLevel
+// with that property.  The first such trial of a stream (never-sliding window) saves its symbol
+// sequence; once a complete sequence is saved, the stream's later such trials at (L, w) replay it.
+static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, std::vector<Trial>& slow,
+                        std::vector<std::array<uint32_t, 3>>& savers) {
+  const uint64_t cap = RP_ARENA_CAP / std::max<size_t>(1, x->pipes_running);
+  for (size_t q = 0; q < slow.size(); q++) {
+    Trial& t = slow[q];
+    if (t.clevel < 6 || (t.mode & 1)) continue;
+    const uint64_t n = x->recs[t.stream].infl_len;
+    const uint64_t wsz = 1ull << t.window;
+    if (n > wsz + (wsz - 262)) continue;                                  // the window may slide
+    const uint32_t Bq = (uint32_t)(c_cfg_host(t.clevel) >> 2);
+    if (x->depth_pin.as<uint32_t>()[10 * (size_t)t.stream + t.memlevel] > Bq) continue;                  // a walk could reach its budget
+    StreamState& st = ss[t.stream];
+    if (st.rp < 0) { st.rp = (int32_t)c->rp_pool.size(); c->rp_pool.emplace_back(); }
+    RpEntry& e = c->rp_pool[st.rp][t.clevel - 6];
+    if (e.state == 2 && e.window == t.window && replay_mode() == 1) {
+      t.mode |= 8;
+      t.rp_syms = e.addr; t.rp_nsym = e.nsym; t.rp_flags = e.flags;
+    } else if (e.state == 0) {
+      const uint64_t bytes = (4 * (n + 64) + 255) & ~255ull;
+      if (!e.addr) {
+        if (c->rp_used + bytes > cap) continue;
+        if (c->d_rp.reserve(cap) != 0) { (void)hipGetLastError(); continue; }   // once per pipe (no replay without it)
+        e.addr = (uint64_t)(uintptr_t)c->d_rp.p + c->rp_used;
+        c->rp_used += bytes;
+      }
+      e.state = 1;
+      e.window = t.window;
+      t.mode |= 4;
+      t.rp_syms = e.addr;
+      savers.push_back({(uint32_t)q, (uint32_t)st.rp, (uint32_t)(t.clevel - 6)});   // indices: rp_pool may grow
+    }
+  }
+}
+
 // ATZ_ROUND_GB=g: match tables + output scratch of one round, over all pipes (default 24 GB)
 static uint64_t round_budget_bytes() {
   static int64_t v = -1;
@@ -1589,6 +1676,16 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     auto tb = std::chrono::steady_clock::now();
     for (int k = 1; k < 3; k++)
       for (Trial& t : tr[k]) t.chain_off = x->chain_off[t.stream][t.memlevel];
+    std::vector<std::array<uint32_t, 3>> savers;   // (index in tr[2], rp_pool entry, level - 6)
+    if (replay_on() && x->depth_pin.p) plan_replay(x, c, ss, tr[2], savers);
+    for (const Trial& t : tr[2]) {   // saved sequences stay inside the arena (a bad slot would fault the GPU)
+      if (!(t.mode & 12)) continue;
+      const uint64_t lo = (uint64_t)(uintptr_t)c->d_rp.p, n = x->recs[t.stream].infl_len;
+      if (t.rp_syms < lo || t.rp_syms + 4 * (n + 64) > lo + c->rp_used || ((t.mode & 8) && t.rp_nsym > n)) {
+        std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
+        return ATZ_E_INTERNAL;
+      }
+    }
     if (int r = c->d_out.reserve(out_tot + 4096)) return r;
     if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
     // while the trials run: the bucket tables the next round will likely need (each stream's next
@@ -1607,6 +1704,16 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     };
     if (int r = run_trials(x, c, d_file, tr, so, trres, prefetch, true)) return r;
     auto tc = std::chrono::steady_clock::now();
+    for (const auto& sv : savers) {   // a complete saved sequence serves the stream's later trials at that level
+      const TrialRes& r = trres[2][sv[0]];
+      RpEntry& e = c->rp_pool[sv[1]][sv[2]];
+      if (r.state != TR_NEED_R && (r.saved_flags & 1u)) {
+        e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags;
+      } else {
+        e.state = 0;   // the slot stays for the next saving trial
+      }
+    }
+    for (const Trial& t : tr[2]) c->stats.n_trials_replayed += (t.mode & 8) ? 1 : 0;
     c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
     c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
     if (timing_level() >= 2)
@@ -1814,6 +1921,8 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
   ss.assign(n_max, StreamState());
   c->chain_off.assign(n_max, {});
   for (auto& a : c->chain_off) a.fill(~0ull);
+  if (int r = c->depth_pin.reserve(n_max * 40 + 64)) return r;
+  std::memset(c->depth_pin.p, 0xff, n_max * 40);
   if (c->infl_off.size() < n_max) c->infl_off.resize(n_max);
   if (c->adler.size() < n_max) c->adler.resize(n_max);
   R.sd.assign(n_max, StreamDev{});
@@ -1830,6 +1939,8 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
     p->stats = atz_stats_t{};
     p->chain_used = 0;
     p->chain_cap = CHAIN_CACHE_CAP / R.np;
+    p->rp_used = 0;
+    p->rp_pool.clear();
     p->t_list = p->t_chains = p->t_trials = p->t_apply = 0;
     std::memset(p->kind, 0, sizeof(p->kind));
   }
@@ -1898,7 +2009,7 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
     t.n_trials_rerun += q.n_trials_rerun; t.n_fast_fallbacks += q.n_fast_fallbacks;
     t.trial_cyc_total += q.trial_cyc_total; t.trial_cyc_tree += q.trial_cyc_tree; t.trial_cyc_emit += q.trial_cyc_emit;
     t.trial_blocks += q.trial_blocks; t.trial_cyc_heap += q.trial_cyc_heap; t.trial_cyc_fallback += q.trial_cyc_fallback;
-    t.trial_symbols += q.trial_symbols;
+    t.trial_symbols += q.trial_symbols; t.n_trials_replayed += q.n_trials_replayed;
     tch = std::max(tch, p->t_chains); ttr = std::max(ttr, p->t_trials); tap = std::max(tap, p->t_apply);
     for (int k = 0; k < 3; k++) for (int l = 0; l < 10; l++) for (int i = 0; i < 14; i++) kind[k][l][i] += p->kind[k][l][i];
   }

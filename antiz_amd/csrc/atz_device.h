@@ -48,6 +48,11 @@ struct Trial {
   uint64_t chain_off;   // hash buckets of (stream, memlevel) (uint32 units, k_buckets); unused for level 0
   uint64_t r_off;       // match table of this trial (uint2 units, indexed by absolute position)
   uint64_t x_lim;       // match-table entries exist for positions < x_lim (else the trial stops: TR_NEED_R)
+  // symbol replay (slow levels): mode bit2 = this trial saves its whole symbol sequence at rp_syms;
+  // mode bit3 = this trial replays the rp_nsym symbols saved there (rp_flags bit1: the last one is
+  // deflate_slow's end-of-input pending literal) instead of parsing
+  uint64_t rp_syms;     // absolute device address (u32 symbols)
+  uint32_t rp_nsym, rp_flags;
 };
 
 // ---- match tables (k_match) ----------------------------------------------------------------
@@ -85,6 +90,8 @@ struct TrialRes {
   uint64_t cyc_heap, cyc_fallback;                  // tree heap steps (ATZ_STEP_CLOCKS) / fast-level exact walks
   uint64_t cyc_scan, cyc_send;                      // scan_tree / send_tree (ATZ_STEP_CLOCKS)
   uint64_t cyc_sec[4];                              // parse window phases: refill / steps / path / tally (ATZ_STEP_CLOCKS)
+  uint32_t saved_syms;  // mode bit2: symbols saved at rp_syms
+  uint32_t saved_flags; // bit0: the whole input was parsed (the sequence is complete), bit1: end-of-input literal
 };
 enum : uint32_t {
   TR_FULL = 0,        // full output produced and compared: ident valid

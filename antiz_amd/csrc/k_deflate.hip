@@ -102,6 +102,8 @@ struct ChainJob {
   uint64_t chain_off;  // u32 units in the chain buffer
   uint32_t memlevel;
   uint32_t slot;       // scratch slot (2 x 65536 words)
+  uint32_t dslot;      // k_buckets_sort: index of the job's deepest-bucket entry in its depth output
+  uint32_t pad_;
 };
 static constexpr uint32_t BUCKET_FIRST = 0x80000000u;
 
@@ -396,7 +398,8 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, uint32_t
 }
 __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* __restrict__ infl,
                                                               const ChainJob* __restrict__ jobs,
-                                                              uint32_t* __restrict__ chains, uint32_t njobs) {
+                                                              uint32_t* __restrict__ chains, uint32_t njobs,
+                                                              uint32_t* __restrict__ depth_out) {
   extern __shared__ uint32_t dyn_lds[];
   __shared__ uint32_t wtot[BSORT_W];
   const uint32_t j = blockIdx.x;
@@ -474,11 +477,30 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
     pass(A, Bo, hbits - 8, 8);
   }
   __syncthreads();
+  LDS uint16_t* F = A;   // bucket-start flags (A is free after the last pass)
   for (uint32_t i = tid; i < nh; i += BSORT_THREADS) {
     const uint32_t p = Bo[i];
     const bool first = i == 0 || H[Bo[i - 1]] != H[p];
     bpos[i] = p | (first ? BUCKET_FIRST : 0u);
     sidx[p] = i;
+    F[i] = first ? 1 : 0;
+  }
+  // deepest bucket: its size - 1 bounds the nodes any chain walk of this (stream, memLevel) can
+  // visit (the host's proof that a walk is never cut by its budget)
+  if (depth_out) {
+    __shared__ uint32_t dmax;
+    if (tid == 0) dmax = 0;
+    __syncthreads();
+    uint32_t mine = 0;
+    for (uint32_t i = tid; i < nh; i += BSORT_THREADS)
+      if (F[i]) {
+        uint32_t e = i + 1;
+        while (e < nh && !F[e]) e++;
+        mine = mine > e - i - 1 ? mine : e - i - 1;
+      }
+    if (mine) atomicMax(&dmax, mine);
+    __syncthreads();
+    if (tid == 0) depth_out[jb.dslot] = dmax;
   }
 }
 
@@ -1639,7 +1661,13 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   b.orig = (const GLOBAL uint8_t*)(A.file + sd.orig_off); b.clen = sd.comp_len;
   b.shortcut = sd.comp_len > A.o.shortcut_len ? A.o.shortcut_len : 0;
   b.eq_all = 0; b.eq_sc = 0; b.overflow = 0;
-  uint32_t* const syms = A.syms + tr.sym_off;
+  // slow levels: a saving trial writes its whole symbol sequence at rp_syms (block k's symbols at
+  // sbase, the count of symbols in the blocks before it); a replaying trial reads one from there
+  const bool saving = KIND == 2 && (tr.mode & 4);
+  const bool replay = KIND == 2 && (tr.mode & 8);
+  uint32_t* const syms = saving || replay ? (uint32_t*)(uintptr_t)tr.rp_syms : A.syms + tr.sym_off;
+  uint32_t sbase = 0;            // symbols in the flushed blocks
+  uint32_t saved_flags = 0;
   b.cyc_tree = b.cyc_emit = b.blocks = 0;
   b.cyc_heap = b.cyc_scan = b.cyc_send = 0;
   const uint64_t cstart = clock64();
@@ -1683,14 +1711,15 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   // ring: chunks of 64 entries below `hi` are resident; the chunk at `hi` is in flight in pf
   uint32_t hi = 0;
   uint64_t pf = 0;
-  if (KIND != 0 && n) pf = Rt[lane];
+  if (KIND != 0 && n && !replay) pf = Rt[lane];
   auto FLUSH = [&](int last) {
-    hazard |= uni(flush_block(s, *(LDS TreeScratch*)shm.ring, b, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in,
-                              (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last, A.o, tr.best_ident,
-                              full_needed, lane));
+    hazard |= uni(flush_block(s, *(LDS TreeScratch*)shm.ring, b, (const GLOBAL uint32_t*)syms + ((saving || replay) ? sbase : 0u),
+                              (const GLOBAL uint8_t*)in, (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last,
+                              A.o, tr.best_ident, full_needed, lane));
+    sbase += z.last_lit;
     z.last_lit = 0;
     z.block_start = z.p;
-    if constexpr (KIND != 0) {   // the tree scratch overlaid the ring: reload its resident chunks
+    if (KIND != 0 && !replay) {   // the tree scratch overlaid the ring: reload its resident chunks
       for (uint32_t c0 = hi >= RING_SLOW ? hi - RING_SLOW : 0u; c0 < hi; c0 += 64) {
         const uint32_t pos = c0 + (uint32_t)lane;
         if (pos < n) ring[pos & (RING_SLOW - 1)] = Rt[pos];
@@ -2022,6 +2051,62 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       z.p = n;
       z.S = S_iter(Sb, n);
     }
+  } else if (replay) {
+    // Symbol replay.  The sequence saved by a trial of this stream at the same (level, window) and
+    // another memLevel is this trial's own: the host proved that no chain walk of either memLevel
+    // reaches its budget (every bucket holds at most B/4 + 1 positions), so each walk examines the
+    // same-trigram positions in the same order (other hashes in a chain never match: their first two
+    // bytes differ) and returns the same match, and deflate_slow's parse does not depend on lit_bufsize.
+    // Only the blocks differ: the symbols are tallied into this memLevel's blocks of lit_bufsize - 1,
+    // each flushed at the position after its last symbol (a literal is tallied at iteration pos + 1,
+    // a match when strstart reaches its end); deflate_slow's end-of-input pending literal is tallied
+    // without a flush check (Z/deflate.c:1842-1846).
+    const GLOBAL uint32_t* sv = (const GLOBAL uint32_t*)syms;
+    const uint32_t nsv = tr.rp_nsym;
+    const bool endlit = (tr.rp_flags & 2u) != 0;
+    uint32_t k = 0, pos = 0;
+    while (k < nsv) {
+      const uint32_t cnt = nsv - k < 64u ? nsv - k : 64u;
+      const bool valid = (uint32_t)lane < cnt;
+      const uint32_t v = valid ? sv[k + (uint32_t)lane] : 0u;
+      const uint32_t len = valid ? ((v >> 8) ? (v & 0xffu) + 3u : 1u) : 0u;
+      uint32_t incl = len;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t2 = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += t2;
+      }
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      uint32_t base = 0;
+      while (base < cnt) {
+        const uint32_t room = z.lbs - 1u - z.last_lit;
+        const uint32_t seg_end = cnt - base < room ? cnt : base + room;
+        if ((uint32_t)lane >= base && (uint32_t)lane < seg_end) {
+          if (v >> 8) {
+            const uint32_t lc = 257u + len_code(v & 0xffu), dc = dist_code((v >> 8) - 1u);
+            __hip_atomic_fetch_add(&s.lfreq2[lc >> 1], 1u << (16 * (lc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.dfreq2[dc >> 1], 1u << (16 * (dc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            __hip_atomic_fetch_add(&s.lfreq2[v >> 1], 1u << (16 * (v & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+        z.last_lit += seg_end - base;
+        z.nsym += seg_end - base;
+        if (z.last_lit == z.lbs - 1u && !(endlit && k + seg_end == nsv)) {
+          z.p = pos + (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)seg_end - 1);
+          FLUSH(0);
+          state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+          if (state != ~0u) break;
+        }
+        base = seg_end;
+      }
+      if (state != ~0u) break;
+      pos += tot;
+      k += cnt;
+    }
+    if (state == ~0u) {
+      z.p = n;
+      z.S = 0;
+    }
   } else {
     // deflate_slow (Z/deflate.c:1730-1853), lane-parallel.
     // After an emitted match (and at the start) deflate_slow's state is canonical: prev_length 2,
@@ -2119,7 +2204,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           } else {
             __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
-          syms[z.last_lit + (o + k - base)] = v;
+          syms[(saving ? sbase : 0u) + z.last_lit + (o + k - base)] = v;
         }
         z.last_lit += seg_end - base;
         if (z.last_lit == z.lbs - 1u) {
@@ -2155,8 +2240,9 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       // end of input: the pending literal goes into the final block without a flush check
       if (ma) {
         const uint32_t v = prevb;
+        saved_flags |= 2;
         if (lane == 0) {
-          syms[z.last_lit] = v;
+          syms[(saving ? sbase : 0u) + z.last_lit] = v;
           __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         z.last_lit++;
@@ -2167,6 +2253,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     }
   }
   if (state == ~0u) {
+    saved_flags |= 1;   // every symbol tallied: a saving trial's sequence is complete
     FLUSH(1);
     // adler32 trailer
     uint32_t ad = A.adler[tr.stream];
@@ -2204,6 +2291,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     r.cyc_send = b.cyc_send;
     for (int i = 0; i < 4; i++) r.cyc_sec[i] = csec[i];
     r.cyc_fallback = cyc_fb;
+    r.saved_syms = sbase;
+    r.saved_flags = saved_flags;
     A.res[t] = r;
   }
 }

@@ -18,6 +18,7 @@ cpu_baseline: the REAL reference (oracle/_ref/uncomp, built from /root/reference
 sample of the same workload (first seed, fewer streams), 1 core, --notest.
 """
 import argparse
+import hashlib
 import json
 import os
 import subprocess
@@ -235,6 +236,7 @@ def main():
         hip_copy(back.data_ptr(), rp, rl)
         recon = {"value": round(len(data) / 1e6 / rdt, 3), "unit": "MB/s restored (ATZ1 resident in HBM)",
                  "ms_per_step": round(rdt * 1000, 2), "atz_bytes": alen,
+                 "atz_sha256": hashlib.sha256(hb).hexdigest()[:16],
                  "identical": rl == len(data) and back.numpy().tobytes() == data}
         del hdev
 

@@ -76,6 +76,7 @@ typedef struct {
     uint64_t n_trials_speculative;                       /* trials run ahead of a stream's stop and discarded */
     uint64_t n_reinflated;                               /* recorded streams inflated again (scan output not kept) */
     uint64_t n_inflate_retries;                          /* inflates rerun with the 32 KiB history ring */
+    uint64_t n_trials_replayed;                          /* slow trials that replayed a saved symbol sequence */
 } atz_stats_t;
 
 enum {
