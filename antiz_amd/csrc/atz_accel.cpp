@@ -239,7 +239,7 @@ struct StreamState {
   std::vector<uint8_t> diffval;
   uint32_t trials = 0;
   uint32_t full_at = ~0u;         // list index whose trial ran past its match-table prefix: rerun with a full table
-  int32_t rp = -1;                // symbol-replay entries (levels 6-9) in the owning pipe's rp_pool
+  int32_t rp = -1;                // symbol-replay entries (levels 1-9) in the owning pipe's rp_pool
   bool recomp = false;
 };
 
@@ -354,11 +354,8 @@ struct KTimer {   // HIP events bracketing kernel launches on the library stream
   }
 };
 
-// One HIP stream of sweep work with its own buffers, kernel timers and counters.  The sweep runs
-// several pipes at once (streams partitioned among them, one host thread each), so one pipe's
-// launch tails, host gaps and small launches overlap another's work.
-// A saved symbol sequence of (stream, level 6-9): the first slow trial at that level whose chain walks
-// cannot reach their budget saves it; later ones at that level replay it (see trial_body).
+// A saved symbol sequence of (stream, level): the first trial at that level whose chain walks cannot
+// reach their budget saves it; later ones at that level replay it (see plan_replay, trial_body).
 struct RpEntry {
   uint64_t addr = 0;      // device address of the arena slot (n + 64 symbols)
   uint32_t nsym = 0, flags = 0;
@@ -368,6 +365,9 @@ struct RpEntry {
 struct ChainBufs {   // bucket-build job lists and scratch (one set per HIP stream that builds)
   DBuf d_cjobs, d_cjobs2, d_cjobs3, d_heads, d_heads2;
 };
+// One HIP stream of sweep work with its own buffers, kernel timers and counters.  The sweep runs
+// several pipes at once (streams partitioned among them, one host thread each), so one pipe's
+// launch tails, host gaps and small launches overlap another's work.
 struct Pipe {
   hipStream_t st = nullptr;
   KTimer kt;
@@ -385,7 +385,7 @@ struct Pipe {
   // symbol replay: saved sequences (bump arena, reset per sweep) and per-stream entries
   DBuf d_rp;
   uint64_t rp_used = 0;
-  std::vector<std::array<struct RpEntry, 4>> rp_pool;
+  std::vector<std::array<struct RpEntry, 9>> rp_pool;   // [stream's entry][level - 1]
   // streams handed to this pipe (scan pieces arrive while it sweeps); closed after the last piece
   std::mutex in_mu;
   std::condition_variable in_cv;
@@ -1552,24 +1552,26 @@ static int replay_mode() {
 static bool replay_on() { return replay_mode() != 0; }
 static constexpr uint64_t RP_ARENA_CAP = 24ull << 30;   // saved sequences, all pipes
 
-// Symbol replay (trial_body): a slow trial at level L in {6..9}, window w, memLevel m whose deepest
-// bucket holds at most B/4 + 1 positions (B = max_chain of L) walks exactly like every other memLevel
-// with that property.  The first such trial of a stream (never-sliding window) saves its symbol
-// sequence; once a complete sequence is saved, the stream's later such trials at (L, w) replay it.
-static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, std::vector<Trial>& slow,
-                        std::vector<std::array<uint32_t, 3>>& savers) {
+// Symbol replay (trial_body): a trial at level L >= 1, window w, memLevel m whose deepest bucket
+// holds at most B + 1 positions walks exactly like every other memLevel with that property, where
+// B = max_chain for deflate_fast (levels 1-3: prev_length stays below good_match) and max_chain / 4
+// for deflate_slow (its budget after a good match).  The first such trial of a stream (never-sliding
+// window) saves its symbol sequence; once a complete sequence is saved, the stream's later such
+// trials at (L, w) replay it.
+static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int kind, std::vector<Trial>& trs,
+                        std::vector<std::array<uint32_t, 4>>& savers) {
   const uint64_t cap = RP_ARENA_CAP / std::max<size_t>(1, x->pipes_running);
-  for (size_t q = 0; q < slow.size(); q++) {
-    Trial& t = slow[q];
-    if (t.clevel < 6 || (t.mode & 1)) continue;
+  for (size_t q = 0; q < trs.size(); q++) {
+    Trial& t = trs[q];
+    if (t.clevel < 1 || t.clevel > 9 || (t.mode & 1)) continue;
     const uint64_t n = x->recs[t.stream].infl_len;
     const uint64_t wsz = 1ull << t.window;
     if (n > wsz + (wsz - 262)) continue;                                  // the window may slide
-    const uint32_t Bq = (uint32_t)(c_cfg_host(t.clevel) >> 2);
-    if (x->depth_pin.as<uint32_t>()[10 * (size_t)t.stream + t.memlevel] > Bq) continue;                  // a walk could reach its budget
+    const uint32_t Bq = (uint32_t)(c_cfg_host(t.clevel) >> (kind == 1 ? 0 : 2));
+    if (x->depth_pin.as<uint32_t>()[10 * (size_t)t.stream + t.memlevel] > Bq) continue;   // a walk could reach its budget
     StreamState& st = ss[t.stream];
     if (st.rp < 0) { st.rp = (int32_t)c->rp_pool.size(); c->rp_pool.emplace_back(); }
-    RpEntry& e = c->rp_pool[st.rp][t.clevel - 6];
+    RpEntry& e = c->rp_pool[st.rp][t.clevel - 1];
     if (e.state == 2 && e.window == t.window && replay_mode() == 1) {
       t.mode |= 8;
       t.rp_syms = e.addr; t.rp_nsym = e.nsym; t.rp_flags = e.flags;
@@ -1585,7 +1587,7 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, std::
       e.window = t.window;
       t.mode |= 4;
       t.rp_syms = e.addr;
-      savers.push_back({(uint32_t)q, (uint32_t)st.rp, (uint32_t)(t.clevel - 6)});   // indices: rp_pool may grow
+      savers.push_back({(uint32_t)kind, (uint32_t)q, (uint32_t)st.rp, (uint32_t)(t.clevel - 1)});   // indices: rp_pool may grow
     }
   }
 }
@@ -1676,16 +1678,18 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     auto tb = std::chrono::steady_clock::now();
     for (int k = 1; k < 3; k++)
       for (Trial& t : tr[k]) t.chain_off = x->chain_off[t.stream][t.memlevel];
-    std::vector<std::array<uint32_t, 3>> savers;   // (index in tr[2], rp_pool entry, level - 6)
-    if (replay_on() && x->depth_pin.p) plan_replay(x, c, ss, tr[2], savers);
-    for (const Trial& t : tr[2]) {   // saved sequences stay inside the arena (a bad slot would fault the GPU)
-      if (!(t.mode & 12)) continue;
-      const uint64_t lo = (uint64_t)(uintptr_t)c->d_rp.p, n = x->recs[t.stream].infl_len;
-      if (t.rp_syms < lo || t.rp_syms + 4 * (n + 64) > lo + c->rp_used || ((t.mode & 8) && t.rp_nsym > n)) {
-        std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
-        return ATZ_E_INTERNAL;
+    std::vector<std::array<uint32_t, 4>> savers;   // (kind, index in tr[kind], rp_pool entry, level - 1)
+    if (replay_on() && x->depth_pin.p)
+      for (int k = 1; k < 3; k++) plan_replay(x, c, ss, k, tr[k], savers);
+    for (int k = 1; k < 3; k++)
+      for (const Trial& t : tr[k]) {   // saved sequences stay inside the arena (a bad slot would fault the GPU)
+        if (!(t.mode & 12)) continue;
+        const uint64_t lo = (uint64_t)(uintptr_t)c->d_rp.p, n = x->recs[t.stream].infl_len;
+        if (t.rp_syms < lo || t.rp_syms + 4 * (n + 64) > lo + c->rp_used || ((t.mode & 8) && t.rp_nsym > n)) {
+          std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
+          return ATZ_E_INTERNAL;
+        }
       }
-    }
     if (int r = c->d_out.reserve(out_tot + 4096)) return r;
     if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
     // while the trials run: the bucket tables the next round will likely need (each stream's next
@@ -1705,15 +1709,16 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     if (int r = run_trials(x, c, d_file, tr, so, trres, prefetch, true)) return r;
     auto tc = std::chrono::steady_clock::now();
     for (const auto& sv : savers) {   // a complete saved sequence serves the stream's later trials at that level
-      const TrialRes& r = trres[2][sv[0]];
-      RpEntry& e = c->rp_pool[sv[1]][sv[2]];
+      const TrialRes& r = trres[sv[0]][sv[1]];
+      RpEntry& e = c->rp_pool[sv[2]][sv[3]];
       if (r.state != TR_NEED_R && (r.saved_flags & 1u)) {
         e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags;
       } else {
         e.state = 0;   // the slot stays for the next saving trial
       }
     }
-    for (const Trial& t : tr[2]) c->stats.n_trials_replayed += (t.mode & 8) ? 1 : 0;
+    for (int k = 1; k < 3; k++)
+      for (const Trial& t : tr[k]) c->stats.n_trials_replayed += (t.mode & 8) ? 1 : 0;
     c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
     c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
     if (timing_level() >= 2)

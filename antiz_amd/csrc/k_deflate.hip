@@ -1661,10 +1661,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   b.orig = (const GLOBAL uint8_t*)(A.file + sd.orig_off); b.clen = sd.comp_len;
   b.shortcut = sd.comp_len > A.o.shortcut_len ? A.o.shortcut_len : 0;
   b.eq_all = 0; b.eq_sc = 0; b.overflow = 0;
-  // slow levels: a saving trial writes its whole symbol sequence at rp_syms (block k's symbols at
-  // sbase, the count of symbols in the blocks before it); a replaying trial reads one from there
-  const bool saving = KIND == 2 && (tr.mode & 4);
-  const bool replay = KIND == 2 && (tr.mode & 8);
+  // fast and slow levels: a saving trial writes its whole symbol sequence at rp_syms (block k's
+  // symbols at sbase, the count of symbols in the blocks before it); a replaying trial reads one
+  const bool saving = KIND != 0 && (tr.mode & 4);
+  const bool replay = KIND != 0 && (tr.mode & 8);
   uint32_t* const syms = saving || replay ? (uint32_t*)(uintptr_t)tr.rp_syms : A.syms + tr.sym_off;
   uint32_t sbase = 0;            // symbols in the flushed blocks
   uint32_t saved_flags = 0;
@@ -1748,6 +1748,64 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         if (state != ~0u) break;
       }
     }
+  } else if (replay) {
+    // Symbol replay.  The sequence saved by a trial of this stream at the same (level, window) and
+    // another memLevel is this trial's own: the host proved that no chain walk of either memLevel
+    // reaches its budget (every bucket holds at most B + 1 positions, B = max_chain for deflate_fast,
+    // whose prev_length never reaches good_match, and max_chain / 4 for deflate_slow), so each walk
+    // examines the same-trigram positions in the same order (other hashes in a chain never match:
+    // their first two bytes differ) and returns the same match; deflate_fast's insertions follow the
+    // match lengths, and neither parse depends on lit_bufsize.  Only the blocks differ: the symbols
+    // are tallied into this memLevel's blocks of lit_bufsize - 1, each flushed at the position after
+    // its last symbol (deflate_slow tallies a literal at iteration pos + 1, a match when strstart
+    // reaches its end; deflate_fast flushes after strstart moved past the symbol); deflate_slow's
+    // end-of-input pending literal is tallied without a flush check (Z/deflate.c:1842-1846).
+    const GLOBAL uint32_t* sv = (const GLOBAL uint32_t*)syms;
+    const uint32_t nsv = tr.rp_nsym;
+    const bool endlit = (tr.rp_flags & 2u) != 0;
+    uint32_t k = 0, pos = 0;
+    while (k < nsv) {
+      const uint32_t cnt = nsv - k < 64u ? nsv - k : 64u;
+      const bool valid = (uint32_t)lane < cnt;
+      const uint32_t v = valid ? sv[k + (uint32_t)lane] : 0u;
+      const uint32_t len = valid ? ((v >> 8) ? (v & 0xffu) + 3u : 1u) : 0u;
+      uint32_t incl = len;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t2 = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += t2;
+      }
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      uint32_t base = 0;
+      while (base < cnt) {
+        const uint32_t room = z.lbs - 1u - z.last_lit;
+        const uint32_t seg_end = cnt - base < room ? cnt : base + room;
+        if ((uint32_t)lane >= base && (uint32_t)lane < seg_end) {
+          if (v >> 8) {
+            const uint32_t lc = 257u + len_code(v & 0xffu), dc = dist_code((v >> 8) - 1u);
+            __hip_atomic_fetch_add(&s.lfreq2[lc >> 1], 1u << (16 * (lc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.dfreq2[dc >> 1], 1u << (16 * (dc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            __hip_atomic_fetch_add(&s.lfreq2[v >> 1], 1u << (16 * (v & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+        z.last_lit += seg_end - base;
+        z.nsym += seg_end - base;
+        if (z.last_lit == z.lbs - 1u && !(endlit && k + seg_end == nsv)) {
+          z.p = pos + (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)seg_end - 1);
+          FLUSH(0);
+          state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+          if (state != ~0u) break;
+        }
+        base = seg_end;
+      }
+      if (state != ~0u) break;
+      pos += tot;
+      k += cnt;
+    }
+    if (state == ~0u) {
+      z.p = n;
+      z.S = 0;
+    }
   } else if constexpr (KIND == 1) {
     // deflate_fast (Z/deflate.c:1628-1722), lane-parallel.  Every deflate_fast iteration starts in
     // the same state, so a window takes the match table's step at each of its 64 positions in
@@ -1801,7 +1859,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     // one symbol, tallied by the scalar unit; returns true when the block is full
     auto tally1 = [&](uint32_t v) -> bool {
       if (lane == 0) {
-        syms[z.last_lit] = v;
+        syms[(saving ? sbase : 0u) + z.last_lit] = v;
         if (v >> 8) {
           __hip_atomic_fetch_add(&s.lfreq2[(257u + len_code(v & 0xffu)) >> 1], 1u << (16 * ((257u + len_code(v & 0xffu)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           __hip_atomic_fetch_add(&s.dfreq2[(dist_code((v >> 8) - 1u)) >> 1], 1u << (16 * ((dist_code((v >> 8) - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1924,7 +1982,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
               v = ex & 0xffu;
               __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            syms[z.last_lit + (o - base)] = v;
+            syms[(saving ? sbase : 0u) + z.last_lit + (o - base)] = v;
           }
           z.last_lit += seg_end - base;
           if (z.last_lit == z.lbs - 1u) {   // flush after the node tallied last: strstart past its step
@@ -2050,62 +2108,6 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     if (state == ~0u) {
       z.p = n;
       z.S = S_iter(Sb, n);
-    }
-  } else if (replay) {
-    // Symbol replay.  The sequence saved by a trial of this stream at the same (level, window) and
-    // another memLevel is this trial's own: the host proved that no chain walk of either memLevel
-    // reaches its budget (every bucket holds at most B/4 + 1 positions), so each walk examines the
-    // same-trigram positions in the same order (other hashes in a chain never match: their first two
-    // bytes differ) and returns the same match, and deflate_slow's parse does not depend on lit_bufsize.
-    // Only the blocks differ: the symbols are tallied into this memLevel's blocks of lit_bufsize - 1,
-    // each flushed at the position after its last symbol (a literal is tallied at iteration pos + 1,
-    // a match when strstart reaches its end); deflate_slow's end-of-input pending literal is tallied
-    // without a flush check (Z/deflate.c:1842-1846).
-    const GLOBAL uint32_t* sv = (const GLOBAL uint32_t*)syms;
-    const uint32_t nsv = tr.rp_nsym;
-    const bool endlit = (tr.rp_flags & 2u) != 0;
-    uint32_t k = 0, pos = 0;
-    while (k < nsv) {
-      const uint32_t cnt = nsv - k < 64u ? nsv - k : 64u;
-      const bool valid = (uint32_t)lane < cnt;
-      const uint32_t v = valid ? sv[k + (uint32_t)lane] : 0u;
-      const uint32_t len = valid ? ((v >> 8) ? (v & 0xffu) + 3u : 1u) : 0u;
-      uint32_t incl = len;
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t2 = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += t2;
-      }
-      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-      uint32_t base = 0;
-      while (base < cnt) {
-        const uint32_t room = z.lbs - 1u - z.last_lit;
-        const uint32_t seg_end = cnt - base < room ? cnt : base + room;
-        if ((uint32_t)lane >= base && (uint32_t)lane < seg_end) {
-          if (v >> 8) {
-            const uint32_t lc = 257u + len_code(v & 0xffu), dc = dist_code((v >> 8) - 1u);
-            __hip_atomic_fetch_add(&s.lfreq2[lc >> 1], 1u << (16 * (lc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&s.dfreq2[dc >> 1], 1u << (16 * (dc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            __hip_atomic_fetch_add(&s.lfreq2[v >> 1], 1u << (16 * (v & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-        }
-        z.last_lit += seg_end - base;
-        z.nsym += seg_end - base;
-        if (z.last_lit == z.lbs - 1u && !(endlit && k + seg_end == nsv)) {
-          z.p = pos + (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)seg_end - 1);
-          FLUSH(0);
-          state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
-          if (state != ~0u) break;
-        }
-        base = seg_end;
-      }
-      if (state != ~0u) break;
-      pos += tot;
-      k += cnt;
-    }
-    if (state == ~0u) {
-      z.p = n;
-      z.S = 0;
     }
   } else {
     // deflate_slow (Z/deflate.c:1730-1853), lane-parallel.
