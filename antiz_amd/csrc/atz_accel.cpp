@@ -357,7 +357,8 @@ struct KTimer {   // HIP events bracketing kernel launches on the library stream
 // A saved symbol sequence of (stream, level): the first trial at that level whose chain walks cannot
 // reach their budget saves it; later ones at that level replay it (see plan_replay, trial_body).
 struct RpEntry {
-  uint64_t addr = 0;      // device address of the arena slot (n + 64 symbols)
+  uint64_t addr = 0;      // device address of the arena slot (n + 64 symbols, then n table entries for slow levels)
+  uint64_t tab = 0;       // its match-table part (0: none)
   uint32_t nsym = 0, flags = 0;
   uint8_t state = 0;      // 0 free (addr may hold a reusable slot), 1 a saving trial in flight, 2 saved
   uint8_t window = 0;
@@ -1421,7 +1422,7 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
   for (int k = 1; k < 3; k++)
     for (Trial& t : tr[k]) {
       const uint64_t n = x->recs[t.stream].infl_len;
-      if (t.mode & 8) { t.r_off = 0; t.x_lim = n; continue; }   // replays: no match table
+      if ((t.mode & 24) == 8) { t.r_off = 0; t.x_lim = n; continue; }   // unchecked replays: no match table
       t.r_off = r_tot;
       r_tot += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
       t.x_lim = ((t.mode & 3) || full) ? n : match_prefix(n, t.memlevel);
@@ -1542,8 +1543,8 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
   return 0;
 }
 
-// ATZ_REPLAY=0 disables symbol replay (every slow trial parses); 2 saves sequences but never replays
-// them (diagnostics)
+// ATZ_REPLAY=0 disables symbol replay (every trial parses); 2 saves sequences but never replays them,
+// 3 replays only between budget-free trials (diagnostics)
 static int replay_mode() {
   static int v = -1;
   if (v < 0) { const char* e = std::getenv("ATZ_REPLAY"); v = e ? std::atoi(e) : 1; }
@@ -1552,15 +1553,18 @@ static int replay_mode() {
 static bool replay_on() { return replay_mode() != 0; }
 static constexpr uint64_t RP_ARENA_CAP = 24ull << 30;   // saved sequences, all pipes
 
-// Symbol replay (trial_body): a trial at level L >= 1, window w, memLevel m whose deepest bucket
-// holds at most B + 1 positions walks exactly like every other memLevel with that property, where
-// B = max_chain for deflate_fast (levels 1-3: prev_length stays below good_match) and max_chain / 4
-// for deflate_slow (its budget after a good match).  The first such trial of a stream (never-sliding
-// window) saves its symbol sequence; once a complete sequence is saved, the stream's later such
-// trials at (L, w) replay it.
+// Symbol replay (trial_body).  A trial at level L, window w, memLevel m whose deepest bucket holds at
+// most B + 1 positions is "budget-free": its walks cannot reach their budget, so they walk exactly
+// like those of every other budget-free memLevel (B = max_chain for deflate_fast, levels 1-3, whose
+// prev_length stays below good_match; max_chain / 4 for deflate_slow, its budget after a good match).
+// The first budget-free trial at (L, w) of a stream whose window never slides saves its symbol
+// sequence (slow levels: and the match-table entries its parse read).  Once a complete sequence is
+// saved, the stream's later trials at (L, w) replay it: unchecked when budget-free too, else (slow
+// levels) only if their own table agrees on those entries, which the kernel checks before parsing.
 static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int kind, std::vector<Trial>& trs,
                         std::vector<std::array<uint32_t, 4>>& savers) {
   const uint64_t cap = RP_ARENA_CAP / std::max<size_t>(1, x->pipes_running);
+  const bool checked = replay_mode() != 3 && kind == 2;   // ATZ_REPLAY=3: budget-free replays only
   for (size_t q = 0; q < trs.size(); q++) {
     Trial& t = trs[q];
     if (t.clevel < 1 || t.clevel > 9 || (t.mode & 1)) continue;
@@ -1568,25 +1572,36 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
     const uint64_t wsz = 1ull << t.window;
     if (n > wsz + (wsz - 262)) continue;                                  // the window may slide
     const uint32_t Bq = (uint32_t)(c_cfg_host(t.clevel) >> (kind == 1 ? 0 : 2));
-    if (x->depth_pin.as<uint32_t>()[10 * (size_t)t.stream + t.memlevel] > Bq) continue;   // a walk could reach its budget
+    const bool bf = x->depth_pin.as<uint32_t>()[10 * (size_t)t.stream + t.memlevel] <= Bq;
+    if (!bf && !checked) continue;
     StreamState& st = ss[t.stream];
     if (st.rp < 0) { st.rp = (int32_t)c->rp_pool.size(); c->rp_pool.emplace_back(); }
     RpEntry& e = c->rp_pool[st.rp][t.clevel - 1];
-    if (e.state == 2 && e.window == t.window && replay_mode() == 1) {
-      t.mode |= 8;
+    if (e.state == 2 && e.window == t.window) {
+      if (replay_mode() == 2) continue;
+      if (bf) {
+        t.mode |= 8;
+      } else if (e.tab) {
+        t.mode |= 8 | 16;
+        t.rp_tab = e.tab;
+      } else {
+        continue;
+      }
       t.rp_syms = e.addr; t.rp_nsym = e.nsym; t.rp_flags = e.flags;
-    } else if (e.state == 0) {
-      const uint64_t bytes = (4 * (n + 64) + 255) & ~255ull;
+    } else if (e.state == 0 && bf) {
+      const uint64_t sb = (4 * (n + 64) + 255) & ~255ull, tb = kind == 2 ? ((8 * n + 255) & ~255ull) : 0;
       if (!e.addr) {
-        if (c->rp_used + bytes > cap) continue;
+        if (c->rp_used + sb + tb > cap) continue;
         if (c->d_rp.reserve(cap) != 0) { (void)hipGetLastError(); continue; }   // once per pipe (no replay without it)
         e.addr = (uint64_t)(uintptr_t)c->d_rp.p + c->rp_used;
-        c->rp_used += bytes;
+        e.tab = tb ? e.addr + sb : 0;
+        c->rp_used += sb + tb;
       }
       e.state = 1;
       e.window = t.window;
       t.mode |= 4;
       t.rp_syms = e.addr;
+      if (e.tab) { t.mode |= 32; t.rp_tab = e.tab; }
       savers.push_back({(uint32_t)kind, (uint32_t)q, (uint32_t)st.rp, (uint32_t)(t.clevel - 1)});   // indices: rp_pool may grow
     }
   }
@@ -1685,7 +1700,8 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       for (const Trial& t : tr[k]) {   // saved sequences stay inside the arena (a bad slot would fault the GPU)
         if (!(t.mode & 12)) continue;
         const uint64_t lo = (uint64_t)(uintptr_t)c->d_rp.p, n = x->recs[t.stream].infl_len;
-        if (t.rp_syms < lo || t.rp_syms + 4 * (n + 64) > lo + c->rp_used || ((t.mode & 8) && t.rp_nsym > n)) {
+        const bool tab_ok = !(t.mode & 48) || (t.rp_tab >= lo && t.rp_tab + 8 * n <= lo + c->rp_used);
+        if (t.rp_syms < lo || t.rp_syms + 4 * (n + 64) > lo + c->rp_used || ((t.mode & 8) && t.rp_nsym > n) || !tab_ok) {
           std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
           return ATZ_E_INTERNAL;
         }
@@ -1718,7 +1734,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       }
     }
     for (int k = 1; k < 3; k++)
-      for (const Trial& t : tr[k]) c->stats.n_trials_replayed += (t.mode & 8) ? 1 : 0;
+      for (size_t q = 0; q < tr[k].size(); q++) {
+        c->stats.n_trials_replayed += (trres[k][q].saved_flags >> 2) & 1u;
+        c->stats.n_replay_checked += (tr[k][q].mode >> 4) & 1u;
+      }
     c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
     c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
     if (timing_level() >= 2)
@@ -2014,7 +2033,7 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
     t.n_trials_rerun += q.n_trials_rerun; t.n_fast_fallbacks += q.n_fast_fallbacks;
     t.trial_cyc_total += q.trial_cyc_total; t.trial_cyc_tree += q.trial_cyc_tree; t.trial_cyc_emit += q.trial_cyc_emit;
     t.trial_blocks += q.trial_blocks; t.trial_cyc_heap += q.trial_cyc_heap; t.trial_cyc_fallback += q.trial_cyc_fallback;
-    t.trial_symbols += q.trial_symbols; t.n_trials_replayed += q.n_trials_replayed;
+    t.trial_symbols += q.trial_symbols; t.n_trials_replayed += q.n_trials_replayed; t.n_replay_checked += q.n_replay_checked;
     tch = std::max(tch, p->t_chains); ttr = std::max(ttr, p->t_trials); tap = std::max(tap, p->t_apply);
     for (int k = 0; k < 3; k++) for (int l = 0; l < 10; l++) for (int i = 0; i < 14; i++) kind[k][l][i] += p->kind[k][l][i];
   }

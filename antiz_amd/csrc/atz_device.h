@@ -48,10 +48,12 @@ struct Trial {
   uint64_t chain_off;   // hash buckets of (stream, memlevel) (uint32 units, k_buckets); unused for level 0
   uint64_t r_off;       // match table of this trial (uint2 units, indexed by absolute position)
   uint64_t x_lim;       // match-table entries exist for positions < x_lim (else the trial stops: TR_NEED_R)
-  // symbol replay (slow levels): mode bit2 = this trial saves its whole symbol sequence at rp_syms;
-  // mode bit3 = this trial replays the rp_nsym symbols saved there (rp_flags bit1: the last one is
-  // deflate_slow's end-of-input pending literal) instead of parsing
+  // symbol replay: mode bit2 = this trial saves its whole symbol sequence at rp_syms (bit5: and its
+  // match table at rp_tab); bit3 = this trial replays the rp_nsym symbols saved there (rp_flags bit1:
+  // the last one is deflate_slow's end-of-input pending literal) instead of parsing -- with bit4 only
+  // if its own match table equals the one saved at rp_tab (else it parses)
   uint64_t rp_syms;     // absolute device address (u32 symbols)
+  uint64_t rp_tab;      // absolute device address (uint2 match-table entries)
   uint32_t rp_nsym, rp_flags;
 };
 
@@ -91,7 +93,8 @@ struct TrialRes {
   uint64_t cyc_scan, cyc_send;                      // scan_tree / send_tree (ATZ_STEP_CLOCKS)
   uint64_t cyc_sec[4];                              // parse window phases: refill / steps / path / tally (ATZ_STEP_CLOCKS)
   uint32_t saved_syms;  // mode bit2: symbols saved at rp_syms
-  uint32_t saved_flags; // bit0: the whole input was parsed (the sequence is complete), bit1: end-of-input literal
+  uint32_t saved_flags; // bit0: the whole input was parsed (the sequence is complete), bit1: end-of-input
+                        // literal, bit2: the trial replayed a saved sequence
 };
 enum : uint32_t {
   TR_FULL = 0,        // full output produced and compared: ident valid

@@ -1664,8 +1664,39 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   // fast and slow levels: a saving trial writes its whole symbol sequence at rp_syms (block k's
   // symbols at sbase, the count of symbols in the blocks before it); a replaying trial reads one
   const bool saving = KIND != 0 && (tr.mode & 4);
-  const bool replay = KIND != 0 && (tr.mode & 8);
+  bool replay = KIND != 0 && (tr.mode & 8);
+  if (KIND == 2 && replay && (tr.mode & 16)) {
+    const uint32_t tlim = tr.x_lim < sd.infl_len ? (uint32_t)tr.x_lim : (uint32_t)sd.infl_len;   // entries present
+    // replay only if this trial's table agrees with the saver's on every entry the saver's parse
+    // read (bit 0 of a saved half: that half was read): then this trial's parse reads the same
+    // entries, step by step, and takes the same path.  A read compares the length and distance
+    // (the head-valid bit only matters with a length > 2, which it implies; the literal byte is
+    // the input's)
+    const GLOBAL uint64_t* mt = (const GLOBAL uint64_t*)(A.R + tr.r_off);   // .x low, .y high
+    const GLOBAL uint64_t* st = (const GLOBAL uint64_t*)(uintptr_t)tr.rp_tab;
+    bool same = true;
+    for (uint32_t p0 = 0; p0 < tlim && same; p0 += 256) {
+      bool d = false;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t p = p0 + 64u * (uint32_t)u + (uint32_t)lane;
+        if (p < tlim) {
+          const uint64_t sv = st[p], df = mt[p] ^ sv;
+          d |= ((sv & 1ull) && (df & 0xffffff00ull)) || ((sv >> 32) & 1ull && (df & 0xffffff0000000000ull));
+        }
+      }
+      same = __ballot(d) == 0;
+    }
+    replay = same;
+  }
   uint32_t* const syms = saving || replay ? (uint32_t*)(uintptr_t)tr.rp_syms : A.syms + tr.sym_off;
+  // a saving slow trial records the match-table entries its parse reads (rp_tab, cleared first)
+  const bool rec = KIND == 2 && saving && (tr.mode & 32);
+  GLOBAL uint64_t* const rtab = (GLOBAL uint64_t*)(uintptr_t)tr.rp_tab;
+  if (rec) {
+    for (uint32_t p = (uint32_t)lane; p < sd.infl_len; p += 64) rtab[p] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the clears land before the records
+  }
   uint32_t sbase = 0;            // symbols in the flushed blocks
   uint32_t saved_flags = 0;
   b.cyc_tree = b.cyc_emit = b.blocks = 0;
@@ -1760,9 +1791,11 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     // its last symbol (deflate_slow tallies a literal at iteration pos + 1, a match when strstart
     // reaches its end; deflate_fast flushes after strstart moved past the symbol); deflate_slow's
     // end-of-input pending literal is tallied without a flush check (Z/deflate.c:1842-1846).
+    // A replay checked against a table prefix (x_lim < n) stops where the parse would read past it.
     const GLOBAL uint32_t* sv = (const GLOBAL uint32_t*)syms;
     const uint32_t nsv = tr.rp_nsym;
     const bool endlit = (tr.rp_flags & 2u) != 0;
+    saved_flags |= 4;
     uint32_t k = 0, pos = 0;
     while (k < nsv) {
       const uint32_t cnt = nsv - k < 64u ? nsv - k : 64u;
@@ -1775,6 +1808,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         if (lane >= d) incl += t2;
       }
       const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      if (xlim < n && pos + tot + 2u > xlim) { state = TR_NEED_R; z.p = pos; break; }
       uint32_t base = 0;
       while (base < cnt) {
         const uint32_t room = z.lbs - 1u - z.last_lit;
@@ -2137,10 +2171,15 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       // ---- the walk from x = wb + lane: wt 0 none (x >= n), 1 no match, 2 match, 3 needs R >= x_lim
       const uint32_t x = wb + lane;
       uint32_t wt = 0, nxt = 0, c = 0, L = 0, D = 0;
+      uint32_t rd_last = 0, rd_ey = ~0u;   // rec: last entry the walk read, first quarter-budget read
       if (x < n) {
         uint32_t qq = x, PL = 2, PD = 0;
         for (;;) {
           if (qq >= xlim) { wt = 3; break; }
+          if (rec && (PL == 2 || PL < z.lazy)) {
+            rd_last = qq;
+            if (PL != 2 && PL >= z.good && rd_ey == ~0u) rd_ey = qq;
+          }
           const uint64_t e64 = ring[qq & (RING_SLOW - 1)];
           const uint32_t ex = (uint32_t)e64, ey = (uint32_t)(e64 >> 32);
           bool hv = qq + 3u <= n && (ey & 1u);
@@ -2178,6 +2217,11 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       path_lane(wp, Am, ma, lane, onp, mab);
       need = wp.need;
       const uint32_t qn = wb + wp.end;
+      if (rec && onp && (wt == 1 || wt == 2))   // the walk's reads: x full-budget, then by PL
+        for (uint32_t i = x; i <= rd_last; i++) {
+          const uint64_t e64 = ring[i & (RING_SLOW - 1)];
+          rtab[i] = (i == x || i < rd_ey) ? ((e64 & 0xffffff00ull) | 1ull) : ((e64 & 0xffffff0000000000ull) | (1ull << 32));
+        }
       // pending literal at qn: after a run yes, after a match no
       const uint32_t man = wp.H ? (uint32_t)((Am >> (63 - __builtin_clzll(wp.H))) & 1ull) : ma;
       // ---- tally the path's symbols: node x emits [literal x-1 if pending], literals x..m-1, match

@@ -76,7 +76,8 @@ typedef struct {
     uint64_t n_trials_speculative;                       /* trials run ahead of a stream's stop and discarded */
     uint64_t n_reinflated;                               /* recorded streams inflated again (scan output not kept) */
     uint64_t n_inflate_retries;                          /* inflates rerun with the 32 KiB history ring */
-    uint64_t n_trials_replayed;                          /* slow trials that replayed a saved symbol sequence */
+    uint64_t n_trials_replayed;                          /* trials that replayed a saved symbol sequence */
+    uint64_t n_replay_checked;                           /* replays offered under a match-table check (passed or not) */
 } atz_stats_t;
 
 enum {
