@@ -477,28 +477,45 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
     pass(A, Bo, hbits - 8, 8);
   }
   __syncthreads();
-  LDS uint16_t* F = A;   // bucket-start flags (A is free after the last pass)
-  for (uint32_t i = tid; i < nh; i += BSORT_THREADS) {
-    const uint32_t p = Bo[i];
-    const bool first = i == 0 || H[Bo[i - 1]] != H[p];
-    bpos[i] = p | (first ? BUCKET_FIRST : 0u);
-    sidx[p] = i;
-    F[i] = first ? 1 : 0;
+  // per wave, its contiguous tile [t0, t1) of the sorted order: bucket starts by ballot, and (when
+  // asked) the deepest bucket, as the largest distance from an element back to its bucket's start
+  // (carried across chunks and, after one barrier, across the waves' tiles)
+  __shared__ uint32_t dmax;
+  uint32_t* const last_start = wtot;   // free after the last pass's scan
+  if (tid == 0) dmax = 0;
+  uint32_t carry = 0, mine = 0;   // start of the bucket open at the tile's current chunk (0: before the tile)
+  bool before = true;              // no start seen yet in this tile
+  uint32_t lead = 0;               // elements of the tile before its first start (belong to an earlier bucket)
+  for (uint32_t i0 = t0; i0 < t1; i0 += 64) {
+    const uint32_t i = i0 + (uint32_t)lane;
+    const bool valid = i < t1;
+    const uint32_t p = valid ? (uint32_t)Bo[i] : 0u;
+    const bool first = valid && (i == 0 || H[Bo[i - 1]] != H[p]);
+    if (valid) {
+      bpos[i] = p | (first ? BUCKET_FIRST : 0u);
+      sidx[p] = i;
+    }
+    if (depth_out) {
+      const uint64_t fm = __ballot(first);
+      const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+      const uint64_t at = fm & le;
+      const uint32_t st = at ? i0 + (63u - (uint32_t)__builtin_clzll(at)) : carry;
+      if (valid && (at || !before)) mine = mine > i - st ? mine : i - st;
+      if (valid && !at && before) lead = i - t0 + 1;   // counted after the barrier
+      if (fm) { carry = i0 + 63u - (uint32_t)__builtin_clzll(fm); before = false; }
+    }
   }
-  // deepest bucket: its size - 1 bounds the nodes any chain walk of this (stream, memLevel) can
-  // visit (the host's proof that a walk is never cut by its budget)
   if (depth_out) {
-    __shared__ uint32_t dmax;
-    if (tid == 0) dmax = 0;
+    if (lane == 0) last_start[wave] = before ? ~0u : carry;
     __syncthreads();
-    uint32_t mine = 0;
-    for (uint32_t i = tid; i < nh; i += BSORT_THREADS)
-      if (F[i]) {
-        uint32_t e = i + 1;
-        while (e < nh && !F[e]) e++;
-        mine = mine > e - i - 1 ? mine : e - i - 1;
-      }
-    if (mine) atomicMax(&dmax, mine);
+    // the tile's leading elements continue the last bucket started in an earlier tile
+    uint32_t prev = ~0u;
+    for (int w = wave - 1; w >= 0 && prev == ~0u; w--) prev = last_start[w];
+    uint32_t lm = 0;
+    if (lead && prev != ~0u) lm = t0 + lead - 1u - prev;   // the last leading element is the farthest
+    lm = lm > mine ? lm : mine;
+    for (int d = 32; d >= 1; d >>= 1) { const uint32_t o = __shfl_xor(lm, d, 64); lm = lm > o ? lm : o; }
+    if (lane == 0 && lm) atomicMax(&dmax, lm);
     __syncthreads();
     if (tid == 0) depth_out[jb.dslot] = dmax;
   }
