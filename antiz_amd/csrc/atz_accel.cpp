@@ -1553,6 +1553,23 @@ static int replay_mode() {
 static bool replay_on() { return replay_mode() != 0; }
 static constexpr uint64_t RP_ARENA_CAP = 24ull << 30;   // saved sequences, all pipes
 
+// a trial replays entry e's saved sequence: unchecked if budget-free, else against the saved reads
+static void replay_from(Trial& t, const RpEntry& e, bool bf) {
+  if (bf) {
+    t.mode |= 8;
+  } else if (e.tab) {
+    t.mode |= 8 | 16;
+    t.rp_tab = e.tab;
+  } else {
+    return;
+  }
+  t.rp_syms = e.addr; t.rp_nsym = e.nsym; t.rp_flags = e.flags;
+}
+static bool budget_free(atz_ctx* x, int kind, const Trial& t) {
+  const uint32_t Bq = (uint32_t)(c_cfg_host(t.clevel) >> (kind == 1 ? 0 : 2));
+  return x->depth_pin.as<uint32_t>()[10 * (size_t)t.stream + t.memlevel] <= Bq;
+}
+
 // Symbol replay (trial_body).  A trial at level L, window w, memLevel m whose deepest bucket holds at
 // most B + 1 positions is "budget-free": its walks cannot reach their budget, so they walk exactly
 // like those of every other budget-free memLevel (B = max_chain for deflate_fast, levels 1-3, whose
@@ -1571,23 +1588,16 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
     const uint64_t n = x->recs[t.stream].infl_len;
     const uint64_t wsz = 1ull << t.window;
     if (n > wsz + (wsz - 262)) continue;                                  // the window may slide
-    const uint32_t Bq = (uint32_t)(c_cfg_host(t.clevel) >> (kind == 1 ? 0 : 2));
-    const bool bf = x->depth_pin.as<uint32_t>()[10 * (size_t)t.stream + t.memlevel] <= Bq;
+    const bool bf = budget_free(x, kind, t);
     if (!bf && !checked) continue;
     StreamState& st = ss[t.stream];
     if (st.rp < 0) { st.rp = (int32_t)c->rp_pool.size(); c->rp_pool.emplace_back(); }
     RpEntry& e = c->rp_pool[st.rp][t.clevel - 1];
     if (e.state == 2 && e.window == t.window) {
       if (replay_mode() == 2) continue;
-      if (bf) {
-        t.mode |= 8;
-      } else if (e.tab) {
-        t.mode |= 8 | 16;
-        t.rp_tab = e.tab;
-      } else {
-        continue;
-      }
-      t.rp_syms = e.addr; t.rp_nsym = e.nsym; t.rp_flags = e.flags;
+      replay_from(t, e, bf);
+    } else if (e.state == 1 && e.window == t.window && replay_mode() != 2 && (bf || e.tab)) {
+      t.mode |= 64;   // its saver runs in this round: wait for it (second launch of the round)
     } else if (e.state == 0 && bf) {
       const uint64_t sb = (4 * (n + 64) + 255) & ~255ull, tb = kind == 2 ? ((8 * n + 255) & ~255ull) : 0;
       if (!e.addr) {
@@ -1722,17 +1732,63 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       }
       return nx.empty() ? 0 : chains_prefetch(x, c, nx);
     };
-    if (int r = run_trials(x, c, d_file, tr, so, trres, prefetch, true)) return r;
-    auto tc = std::chrono::steady_clock::now();
-    for (const auto& sv : savers) {   // a complete saved sequence serves the stream's later trials at that level
-      const TrialRes& r = trres[sv[0]][sv[1]];
-      RpEntry& e = c->rp_pool[sv[2]][sv[3]];
-      if (r.state != TR_NEED_R && (r.saved_flags & 1u)) {
-        e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags;
-      } else {
-        e.state = 0;   // the slot stays for the next saving trial
+    auto finish_savers = [&]() {   // a complete saved sequence serves the stream's later trials at that level
+      for (const auto& sv : savers) {
+        const TrialRes& r = trres[sv[0]][sv[1]];
+        RpEntry& e = c->rp_pool[sv[2]][sv[3]];
+        if (r.state != TR_NEED_R && (r.saved_flags & 1u)) {
+          e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags;
+        } else {
+          e.state = 0;   // the slot stays for the next saving trial
+        }
       }
+    };
+    bool waiting_trials = false;
+    for (int k = 1; k < 3 && !waiting_trials; k++)
+      for (const Trial& t : tr[k]) if (t.mode & 64) { waiting_trials = true; break; }
+    if (!waiting_trials) {
+      if (int r = run_trials(x, c, d_file, tr, so, trres, prefetch, true)) return r;
+      finish_savers();
+    } else {
+      // speculative rounds (K > 1) can hold a saver and later trials of its (stream, level): those
+      // run in a second launch once the saver's sequence is in, as replays
+      std::vector<Trial> t1[3], t2[3];
+      std::vector<uint32_t> i1[3], i2[3];
+      std::vector<TrialRes> r1[3], r2[3];
+      for (int k = 0; k < 3; k++)
+        for (uint32_t q = 0; q < tr[k].size(); q++) {
+          const bool w = (tr[k][q].mode & 64) != 0;
+          (w ? t2 : t1)[k].push_back(tr[k][q]);
+          (w ? i2 : i1)[k].push_back(q);
+        }
+      if (int r = run_trials(x, c, d_file, t1, so, r1, prefetch, true)) return r;
+      for (int k = 0; k < 3; k++) {
+        trres[k].resize(tr[k].size());
+        for (size_t j = 0; j < i1[k].size(); j++) trres[k][i1[k][j]] = r1[k][j];
+      }
+      finish_savers();
+      for (int k = 1; k < 3; k++)
+        for (size_t j = 0; j < t2[k].size(); j++) {
+          Trial& t = t2[k][j];
+          t.mode &= ~64u;
+          const RpEntry& e = c->rp_pool[ss[t.stream].rp][t.clevel - 1];
+          if (e.state == 2 && e.window == t.window) replay_from(t, e, budget_free(x, k, t));
+          tr[k][i2[k][j]].mode = t.mode;
+        }
+      for (int k = 1; k < 3; k++)   // as in the first launch: replay slots inside the arena
+        for (const Trial& t : t2[k]) {
+          const uint64_t lo = (uint64_t)(uintptr_t)c->d_rp.p, n = x->recs[t.stream].infl_len;
+          if ((t.mode & 8) && (t.rp_syms < lo || t.rp_syms + 4 * (n + 64) > lo + c->rp_used || t.rp_nsym > n ||
+                               ((t.mode & 16) && (t.rp_tab < lo || t.rp_tab + 8 * n > lo + c->rp_used)))) {
+            std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
+            return ATZ_E_INTERNAL;
+          }
+        }
+      if (int r = run_trials(x, c, d_file, t2, so, r2, nullptr, true)) return r;
+      for (int k = 1; k < 3; k++)
+        for (size_t j = 0; j < i2[k].size(); j++) trres[k][i2[k][j]] = r2[k][j];
     }
+    auto tc = std::chrono::steady_clock::now();
     for (int k = 1; k < 3; k++)
       for (size_t q = 0; q < tr[k].size(); q++) {
         c->stats.n_trials_replayed += (trres[k][q].saved_flags >> 2) & 1u;

@@ -418,3 +418,35 @@ def test_continuation_probe_rerun(atz):
             with atz.Context(chunksize=cs) as c:
                 got, _ = c.precompress(data)
             assert got == want
+
+
+def test_symbol_replay_matches_oracle(atz):
+    """Symbol replay (a trial reuses the symbol sequence another memLevel's trial of the stream saved
+    at the same level and window, unchecked when both walks are budget-free, else after matching the
+    saver's read table entries): streams whose parameters sit late in their trial lists, so most of
+    their trials are replays, with text of a small vocabulary (deep buckets: checked replays) and of
+    a large one (budget-free), blocks of every lit_bufsize, end-of-input literals, and windows that
+    slide (never replayed).  The .atz bytes must equal the oracle's."""
+    rng = random.Random(21)
+    small = ["".join(rng.choice("etaoinshr") for _ in range(rng.randint(1, 5))) for _ in range(40)]
+    parts = []
+    params = [(2, 15, 1), (3, 15, 2), (4, 15, 1), (5, 15, 3), (3, 15, 1), (7, 15, 1), (8, 15, 2), (9, 15, 1),
+              (6, 15, 1), (7, 15, 9), (2, 15, 9), (9, 12, 1), (4, 10, 2), (1, 15, 1)]
+    for k in range(84):
+        c, w, m = params[k % len(params)]
+        n = rng.choice([300, 1500, 4000, 9000, 17000, 24000])
+        if k % 2:
+            d = " ".join(rng.choice(small) for _ in range(n // 3)).encode()[:n]
+        else:
+            d = _libs.text(rng, n)
+        s, _ = _libs.ora_deflate(d, c, w, m)
+        parts.append(bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 40))) + s)
+    data = b"".join(parts)
+    rc, ref, _ = _libs.ora_precompress(data)
+    assert rc == 0
+    with atz.Context() as c:
+        out, st = c.precompress(data)
+        assert st["n_trials_replayed"] > 100, st
+        assert st["n_replay_checked"] > 0, st
+        assert sha(out) == sha(ref)
+        assert c.reconstruct(out) == data
