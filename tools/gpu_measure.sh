@@ -20,10 +20,10 @@ if has bench; then
   timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || exit 3
 fi
 if has prof; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o p --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu > $O/prof.json 2> $O/prof.err || exit 4
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o p --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-recon > $O/prof.json 2> $O/prof.err || exit 4
 fi
 if has pmc; then
-  timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmcf -o p --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu > $O/pmcf.json 2> $O/pmcf.err || exit 5
-  timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -d $O/pmcw -o p --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu > $O/pmcw.json 2> $O/pmcw.err || exit 6
+  timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmcf -o p --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-recon > $O/pmcf.json 2> $O/pmcf.err || exit 5
+  timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -d $O/pmcw -o p --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-recon > $O/pmcw.json 2> $O/pmcw.err || exit 6
 fi
 echo done

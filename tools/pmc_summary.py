@@ -43,7 +43,7 @@ def main():
     w = sum(kern[k]["write_bytes_total"] for k in tk)
     res = {
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- python3 bench.py --steps 1 "
-                  "--warmup 0 --no-cpu, full C4 (100 000 streams, 1.007 GB), one MI355X",
+                  "--warmup 0 --no-cpu --no-recon, full C4 (100 000 streams, 1.007 GB), one MI355X",
         "units": "bytes per launch; fetch_bytes_raw = FETCH_SIZE kB x 1000; fetch_bytes = 2 x raw (guide: gfx950 "
                  "FETCH_SIZE reports half the bytes of wide reads); write_bytes = WRITE_SIZE kB x 1000",
         "kernels": kern,
