@@ -362,6 +362,7 @@ struct RpEntry {
   uint32_t nsym = 0, flags = 0;
   uint8_t state = 0;      // 0 free (addr may hold a reusable slot), 1 a saving trial in flight, 2 saved
   uint8_t window = 0;
+  uint8_t memlevel = 0;   // the saver's
 };
 struct ChainBufs {   // bucket-build job lists and scratch (one set per HIP stream that builds)
   DBuf d_cjobs, d_cjobs2, d_cjobs3, d_heads, d_heads2;
@@ -1554,9 +1555,22 @@ static bool replay_on() { return replay_mode() != 0; }
 static constexpr uint64_t RP_ARENA_CAP = 24ull << 30;   // saved sequences, all pipes
 
 // a trial replays entry e's saved sequence: unchecked if budget-free, else against the saved reads
+// ATZ_DEDUP=0: launch duplicate trials anyway (diagnostics)
+static bool dedup_on() {
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_DEDUP"); v = e ? std::atoi(e) : 1; }
+  return v != 0;
+}
+// A budget-free replay whose saved sequence fits one block of both its own and the saver's
+// lit_bufsize (at most lit_bufsize - 2 symbols: with lit_bufsize - 1 the tally flushes a block and the
+// end adds an empty final one) compresses to the saver's bytes: same symbols, same single block,
+// same header (level, window).  Its result can then only equal the saver's, which the stream's rule
+// already applied without stopping, so it is not launched (mode bit 7; TR_CANT_BEAT on the host).
 static void replay_from(Trial& t, const RpEntry& e, bool bf) {
   if (bf) {
     t.mode |= 8;
+    const uint32_t lm = std::min<uint32_t>(e.memlevel, t.memlevel);
+    if (dedup_on() && (uint64_t)e.nsym + 2 <= (1ull << (lm + 6))) t.mode |= 128;
   } else if (e.tab) {
     t.mode |= 8 | 16;
     t.rp_tab = e.tab;
@@ -1609,6 +1623,7 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
       }
       e.state = 1;
       e.window = t.window;
+      e.memlevel = t.memlevel;
       t.mode |= 4;
       t.rp_syms = e.addr;
       if (e.tab) { t.mode |= 32; t.rp_tab = e.tab; }
@@ -1743,56 +1758,64 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         }
       }
     };
-    bool waiting_trials = false;
-    for (int k = 1; k < 3 && !waiting_trials; k++)
-      for (const Trial& t : tr[k]) if (t.mode & 64) { waiting_trials = true; break; }
-    if (!waiting_trials) {
+    // duplicates are not launched; trials waiting for a saver of this round go in a second launch
+    // (speculative rounds, K > 1: small files, the sweep's tail) once the saver's sequence is in
+    TrialRes dup{};
+    dup.state = TR_CANT_BEAT;
+    bool waiting_trials = false, dups = false;
+    for (int k = 1; k < 3; k++)
+      for (const Trial& t : tr[k]) { waiting_trials |= (t.mode & 64) != 0; dups |= (t.mode & 128) != 0; }
+    if (!waiting_trials && !dups) {
       if (int r = run_trials(x, c, d_file, tr, so, trres, prefetch, true)) return r;
       finish_savers();
     } else {
-      // speculative rounds (K > 1) can hold a saver and later trials of its (stream, level): those
-      // run in a second launch once the saver's sequence is in, as replays
       std::vector<Trial> t1[3], t2[3];
       std::vector<uint32_t> i1[3], i2[3];
       std::vector<TrialRes> r1[3], r2[3];
-      for (int k = 0; k < 3; k++)
+      for (int k = 0; k < 3; k++) {
+        trres[k].assign(tr[k].size(), dup);
         for (uint32_t q = 0; q < tr[k].size(); q++) {
+          if (tr[k][q].mode & 128) continue;
           const bool w = (tr[k][q].mode & 64) != 0;
           (w ? t2 : t1)[k].push_back(tr[k][q]);
           (w ? i2 : i1)[k].push_back(q);
         }
-      if (int r = run_trials(x, c, d_file, t1, so, r1, prefetch, true)) return r;
-      for (int k = 0; k < 3; k++) {
-        trres[k].resize(tr[k].size());
-        for (size_t j = 0; j < i1[k].size(); j++) trres[k][i1[k][j]] = r1[k][j];
       }
+      if (int r = run_trials(x, c, d_file, t1, so, r1, prefetch, true)) return r;
+      for (int k = 0; k < 3; k++)
+        for (size_t j = 0; j < i1[k].size(); j++) trres[k][i1[k][j]] = r1[k][j];
       finish_savers();
-      for (int k = 1; k < 3; k++)
-        for (size_t j = 0; j < t2[k].size(); j++) {
-          Trial& t = t2[k][j];
-          t.mode &= ~64u;
-          const RpEntry& e = c->rp_pool[ss[t.stream].rp][t.clevel - 1];
-          if (e.state == 2 && e.window == t.window) replay_from(t, e, budget_free(x, k, t));
-          tr[k][i2[k][j]].mode = t.mode;
-        }
-      for (int k = 1; k < 3; k++)   // as in the first launch: replay slots inside the arena
-        for (const Trial& t : t2[k]) {
-          const uint64_t lo = (uint64_t)(uintptr_t)c->d_rp.p, n = x->recs[t.stream].infl_len;
-          if ((t.mode & 8) && (t.rp_syms < lo || t.rp_syms + 4 * (n + 64) > lo + c->rp_used || t.rp_nsym > n ||
-                               ((t.mode & 16) && (t.rp_tab < lo || t.rp_tab + 8 * n > lo + c->rp_used)))) {
-            std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
-            return ATZ_E_INTERNAL;
+      if (waiting_trials) {
+        std::vector<Trial> t3[3];
+        std::vector<uint32_t> i3[3];
+        for (int k = 1; k < 3; k++)
+          for (size_t j = 0; j < t2[k].size(); j++) {
+            Trial& t = t2[k][j];
+            t.mode &= ~64u;
+            const RpEntry& e = c->rp_pool[ss[t.stream].rp][t.clevel - 1];
+            if (e.state == 2 && e.window == t.window) replay_from(t, e, budget_free(x, k, t));
+            tr[k][i2[k][j]].mode = t.mode;
+            if (t.mode & 128) continue;
+            const uint64_t lo = (uint64_t)(uintptr_t)c->d_rp.p, n = x->recs[t.stream].infl_len;
+            if ((t.mode & 8) && (t.rp_syms < lo || t.rp_syms + 4 * (n + 64) > lo + c->rp_used || t.rp_nsym > n ||
+                                 ((t.mode & 16) && (t.rp_tab < lo || t.rp_tab + 8 * n > lo + c->rp_used)))) {
+              std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
+              return ATZ_E_INTERNAL;
+            }
+            t3[k].push_back(t);
+            i3[k].push_back(i2[k][j]);
           }
-        }
-      if (int r = run_trials(x, c, d_file, t2, so, r2, nullptr, true)) return r;
-      for (int k = 1; k < 3; k++)
-        for (size_t j = 0; j < i2[k].size(); j++) trres[k][i2[k][j]] = r2[k][j];
+        if (int r = run_trials(x, c, d_file, t3, so, r2, nullptr, true)) return r;
+        for (int k = 1; k < 3; k++)
+          for (size_t j = 0; j < i3[k].size(); j++) trres[k][i3[k][j]] = r2[k][j];
+      }
     }
     auto tc = std::chrono::steady_clock::now();
     for (int k = 1; k < 3; k++)
       for (size_t q = 0; q < tr[k].size(); q++) {
         c->stats.n_trials_replayed += (trres[k][q].saved_flags >> 2) & 1u;
         c->stats.n_replay_checked += (tr[k][q].mode >> 4) & 1u;
+        c->stats.n_trials_duplicate += (tr[k][q].mode >> 7) & 1u;
       }
     c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
     c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
@@ -1817,7 +1840,8 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         gk[5] += r.cyc_fallback; gk[6] += r.parsed; gk[7] += r.symbols; gk[8] += r.cyc_scan; gk[9] += r.cyc_send;
         for (int i = 0; i < 4; i++) gk[10 + i] += r.cyc_sec[i];
         // trial input read + compare read (bytes emitted and compared against the original)
-        c->stats.k_trial_alg_bytes += x->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
+        if (!(tr[k][q].mode & 128))   // duplicates are not launched
+          c->stats.k_trial_alg_bytes += x->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
       }
     if (timing_on()) {   // slowest trials of the round (diagnostics)
       std::vector<std::pair<uint64_t, std::pair<int, size_t>>> top;
@@ -2090,6 +2114,7 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
     t.trial_cyc_total += q.trial_cyc_total; t.trial_cyc_tree += q.trial_cyc_tree; t.trial_cyc_emit += q.trial_cyc_emit;
     t.trial_blocks += q.trial_blocks; t.trial_cyc_heap += q.trial_cyc_heap; t.trial_cyc_fallback += q.trial_cyc_fallback;
     t.trial_symbols += q.trial_symbols; t.n_trials_replayed += q.n_trials_replayed; t.n_replay_checked += q.n_replay_checked;
+    t.n_trials_duplicate += q.n_trials_duplicate;
     tch = std::max(tch, p->t_chains); ttr = std::max(ttr, p->t_trials); tap = std::max(tap, p->t_apply);
     for (int k = 0; k < 3; k++) for (int l = 0; l < 10; l++) for (int i = 0; i < 14; i++) kind[k][l][i] += p->kind[k][l][i];
   }

@@ -78,6 +78,7 @@ typedef struct {
     uint64_t n_inflate_retries;                          /* inflates rerun with the 32 KiB history ring */
     uint64_t n_trials_replayed;                          /* trials that replayed a saved symbol sequence */
     uint64_t n_replay_checked;                           /* replays offered under a match-table check (passed or not) */
+    uint64_t n_trials_duplicate;                         /* replays whose output equals their saver's: not launched */
 } atz_stats_t;
 
 enum {

@@ -13,6 +13,6 @@ for ((i=1;i<=R;i++)); do
     k=$((k+1))
     [ "$E" = "-" ] && E=""
     env $E timeout -k 10 240 python3 bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/$TAG/v$k.$i.json 2> gpurun_out/$TAG/v$k.$i.err || exit 1
-    echo "v$k.$i [$E] $(python3 -c "import json;d=json.load(open('gpurun_out/$TAG/v$k.$i.json'));print(d['value'],(d['reconstruct'] or {}).get('atz_sha256'),{x:d['detail'].get(x) for x in ('k_trial_ms','k_match_ms','k_chains_ms','k_inflate_ms','n_trials','n_trials_replayed','n_replay_checked')})")"
+    echo "v$k.$i [$E] $(python3 -c "import json;d=json.load(open('gpurun_out/$TAG/v$k.$i.json'));print(d['value'],(d['reconstruct'] or {}).get('atz_sha256'),{x:d['detail'].get(x) for x in ('k_trial_ms','k_match_ms','k_chains_ms','k_inflate_ms','n_trials','n_trials_replayed','n_replay_checked','n_trials_duplicate')})")"
   done
 done
