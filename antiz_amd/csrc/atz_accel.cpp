@@ -374,7 +374,7 @@ struct Pipe {
   hipStream_t st = nullptr;
   KTimer kt;
   atz_stats_t stats{};
-  DBuf d_trials, d_tres, d_out, d_syms, d_R, d_mjobs, d_chains, d_diffjobs, d_diffpos, d_diffval, d_diffcnt;
+  DBuf d_trials, d_tres, d_out, d_syms, d_R, d_mjobs, d_chains, d_diffjobs, d_diffpos, d_diffval, d_diffcnt, d_djobs;
   ChainBufs cb[2];   // [0] builds on st, [1] prefetch builds on pst
   // next-round bucket builds run ahead on their own stream while this round's trials run
   hipStream_t pst = nullptr;
@@ -388,6 +388,9 @@ struct Pipe {
   DBuf d_rp;
   uint64_t rp_used = 0;
   std::vector<std::array<struct RpEntry, 9>> rp_pool;   // [stream's entry][level - 1]
+  // diagnostics (ATZ_TIMING): bucket builds, and per stream the memLevels a table-reading trial used
+  uint64_t diag_builds = 0;
+  std::vector<uint16_t> diag_need;
   // streams handed to this pipe (scan pieces arrive while it sweeps); closed after the last piece
   std::mutex in_mu;
   std::condition_variable in_cv;
@@ -1070,6 +1073,47 @@ static int ensure_chains(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32
   if (c->pev_pending) HIPCHK(hipStreamWaitEvent(c->st, c->pev, 0));
   return ensure_chains_on(x, c, need, c->cb[0], false);
 }
+// The deepest-bucket sizes (symbol replay's budget-free test) of pairs not known yet, without building
+// their tables (k_bucket_depth; streams < 64 Ki positions, larger ones are never budget-free): a pair
+// whose trials all turn out to be replays never needs its tables.  Runs on the pipe's stream.
+static int ensure_depths(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need) {
+  if (!x->depth_pin.p) return 0;
+  uint32_t* dp = x->depth_pin.as<uint32_t>();
+  std::vector<ChainJob> byl[10];
+  size_t tot = 0;
+  for (const auto& q : need) {
+    const uint32_t s = q.first;
+    const int m = q.second;
+    const size_t i = 10 * (size_t)s + (size_t)m;
+    if (dp[i] != ~0u || x->recs[s].infl_len >= 65536) continue;
+    dp[i] = 0xfffffffeu;   // queued (the kernel overwrites it)
+    ChainJob jb{};
+    jb.infl_off = x->infl_off[s];
+    jb.n = x->recs[s].infl_len;
+    jb.memlevel = (uint32_t)m;
+    jb.dslot = (uint32_t)i;
+    byl[m].push_back(jb);
+    tot++;
+  }
+  if (!tot) return 0;
+  std::vector<ChainJob> all;
+  all.reserve(tot);
+  size_t beg[11] = {};
+  for (int m = 0; m < 10; m++) { beg[m] = all.size(); all.insert(all.end(), byl[m].begin(), byl[m].end()); }
+  beg[10] = all.size();
+  if (int r = upload(c, c->d_djobs, all.data(), all.size() * sizeof(ChainJob))) return r;
+  for (int m = 1; m < 10; m++) {
+    const size_t cnt = beg[m + 1] - beg[m];
+    if (!cnt) continue;
+    kbeg(c, 2);
+    hipLaunchKernelGGL(k_bucket_depth, dim3((uint32_t)cnt), dim3(BDEPTH_THREADS), 4u << (m + 6), c->st, INFL_BASE,
+                       c->d_djobs.as<ChainJob>() + beg[m], (uint32_t)cnt, dp);
+    kend(c);
+    KCHECK("k_bucket_depth");
+  }
+  for (const ChainJob& jb : all) c->stats.k_chains_alg_bytes += jb.n;
+  return 0;
+}
 // Speculative builds for the next round on the prefetch stream; skipped when they would need the
 // cache dropped or grown (both are only done between rounds, on the pipe's stream).
 static int chains_prefetch(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need) {
@@ -1223,6 +1267,7 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     x->chain_off[s][m] = c->chain_used;
     c->chain_used += words(s);
     jobs.push_back(jb);
+    c->diag_builds++;
   }
   if (jobs.empty()) return 0;
   // grow the cache (keeps contents)
@@ -1711,16 +1756,27 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     mbeg.resize(active.size() + 1);
     mbeg[active.size()] = (uint32_t)mine.size();
     auto ta = std::chrono::steady_clock::now();
+    // replays first (they need the pairs' bucket depths only), then the tables the other trials read
+    std::vector<std::array<uint32_t, 4>> savers;   // (kind, index in tr[kind], rp_pool entry, level - 1)
+    if (replay_on() && x->depth_pin.p) {
+      if (int r = ensure_depths(x, c, need)) return r;
+      HIPCHK(hipStreamSynchronize(c->st));
+      for (int k = 1; k < 3; k++) plan_replay(x, c, ss, k, tr[k], savers);
+      need.clear();
+      for (int k = 1; k < 3; k++)
+        for (const Trial& t : tr[k])
+          if ((t.mode & 24) != 8 && !(t.mode & 128)) need.push_back({t.stream, (int)t.memlevel});
+    }
     size_t nbuild = 0;
     for (auto& q : need) nbuild += x->chain_off[q.first][q.second] == ~0ull;
     if (int r = ensure_chains(x, c, need)) return r;
     HIPCHK(hipStreamSynchronize(c->st));
     auto tb = std::chrono::steady_clock::now();
     for (int k = 1; k < 3; k++)
-      for (Trial& t : tr[k]) t.chain_off = x->chain_off[t.stream][t.memlevel];
-    std::vector<std::array<uint32_t, 4>> savers;   // (kind, index in tr[kind], rp_pool entry, level - 1)
-    if (replay_on() && x->depth_pin.p)
-      for (int k = 1; k < 3; k++) plan_replay(x, c, ss, k, tr[k], savers);
+      for (Trial& t : tr[k]) {
+        const uint64_t off = x->chain_off[t.stream][t.memlevel];
+        t.chain_off = off == ~0ull ? 0 : off;   // unchecked replays read no table
+      }
     for (int k = 1; k < 3; k++)
       for (const Trial& t : tr[k]) {   // saved sequences stay inside the arena (a bad slot would fault the GPU)
         if (!(t.mode & 12)) continue;
@@ -1816,6 +1872,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         c->stats.n_trials_replayed += (trres[k][q].saved_flags >> 2) & 1u;
         c->stats.n_replay_checked += (tr[k][q].mode >> 4) & 1u;
         c->stats.n_trials_duplicate += (tr[k][q].mode >> 7) & 1u;
+        if (timing_on() && (tr[k][q].mode & 24) != 8 && !(tr[k][q].mode & 128)) {
+          if (c->diag_need.size() <= tr[k][q].stream) c->diag_need.resize(tr[k][q].stream + 1, 0);
+          c->diag_need[tr[k][q].stream] |= (uint16_t)(1u << tr[k][q].memlevel);
+        }
       }
     c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
     c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
@@ -2118,9 +2178,20 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
     tch = std::max(tch, p->t_chains); ttr = std::max(ttr, p->t_trials); tap = std::max(tap, p->t_apply);
     for (int k = 0; k < 3; k++) for (int l = 0; l < 10; l++) for (int i = 0; i < 14; i++) kind[k][l][i] += p->kind[k][l][i];
   }
-  if (timing_on())
+  if (timing_on()) {
     std::fprintf(stderr, "atz: sweep host: chains %.1f ms (incl. kernels), trials %.1f ms (incl. kernels), apply %.1f ms, total %.1f ms\n",
                  tch, ttr, tap, ms_since(R.t0));
+    uint64_t nb = 0, nn = 0;
+    for (size_t g = 0; g < np; g++) {
+      Pipe* p = c->pipes[g].get();
+      nb += p->diag_builds;
+      for (uint16_t v : p->diag_need) nn += (uint64_t)__builtin_popcount(v);
+      p->diag_builds = 0;
+      p->diag_need.clear();
+    }
+    std::fprintf(stderr, "atz: bucket builds %llu, (stream, memLevel) pairs a table-reading trial used %llu\n",
+                 (unsigned long long)nb, (unsigned long long)nn);
+  }
   if (timing_on())
     for (int k = 0; k < 3; k++)
       for (int l = 0; l < 10; l++) {

@@ -44,6 +44,9 @@
 #ifndef ATZ_NOSLIDE_PATH
 #define ATZ_NOSLIDE_PATH 1    // parse: skip the window-slide checks for streams that never slide
 #endif
+#ifndef ATZ_STEP_SPLIT
+#define ATZ_STEP_SPLIT 0
+#endif
 #ifndef ATZ_STEP_CLOCKS
 #define ATZ_STEP_CLOCKS 0
 #endif
@@ -519,6 +522,42 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
     __syncthreads();
     if (tid == 0) depth_out[jb.dslot] = dmax;
   }
+}
+
+// k_bucket_depth: only the deepest bucket of a (stream, memLevel) (size - 1, as k_buckets_sort
+// reports it), for pairs whose trials may all be symbol replays: one returning LDS atomic per
+// position on packed 16-bit hash counters (streams < 64 Ki positions), no sort, no tables written.
+static constexpr uint32_t BDEPTH_THREADS = 1024;
+__global__ __launch_bounds__(BDEPTH_THREADS) void k_bucket_depth(const uint8_t* __restrict__ infl,
+                                                                const ChainJob* __restrict__ jobs, uint32_t njobs,
+                                                                uint32_t* __restrict__ depth_out) {
+  extern __shared__ uint32_t dyn_lds[];
+  __shared__ uint32_t dmax;
+  const uint32_t j = blockIdx.x;
+  if (j >= njobs) return;
+  const int tid = threadIdx.x;
+  const ChainJob jb = jobs[j];
+  const uint8_t* in = infl + jb.infl_off;
+  const uint32_t n = (uint32_t)jb.n;
+  const uint32_t hbits = jb.memlevel + 7, hmask = (1u << hbits) - 1, hshift = (hbits + 2) / 3;
+  const uint32_t nw = 1u << (hbits - 1);   // two counters per word
+  LDS uint32_t* cnt = (LDS uint32_t*)dyn_lds;
+  for (uint32_t w = tid; w < nw; w += BDEPTH_THREADS) cnt[w] = 0;
+  if (tid == 0) dmax = 0;
+  __syncthreads();
+  const uint32_t nh = n >= 3 ? n - 2 : 0;
+  uint32_t mine = 0;
+  for (uint32_t p = tid; p < nh; p += BDEPTH_THREADS) {
+    const uint32_t h = (((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask;
+    const uint32_t sh = 16u * (h & 1u);
+    const uint32_t old = __hip_atomic_fetch_add(&cnt[h >> 1], 1u << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t c = ((old >> sh) & 0xffffu) + 1u;
+    mine = mine > c ? mine : c;
+  }
+  for (int d = 32; d >= 1; d >>= 1) { const uint32_t o = __shfl_xor(mine, d, 64); mine = mine > o ? mine : o; }
+  if ((tid & 63) == 0 && mine) atomicMax(&dmax, mine);
+  __syncthreads();
+  if (tid == 0) depth_out[jb.dslot] = dmax ? dmax - 1u : 0u;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1976,6 +2015,9 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           y = wb + yl;
           Ly = (uint32_t)__shfl((int)L, (int)yl, 64);
         });
+#if ATZ_STEP_SPLIT
+      t1 = STEP_CLOCK(); csec[0] += t1 - t0; t0 = t1;   // (diagnostics: span_set counted with refill)
+#endif
       bool bad = false;
       if (onp && x + 3u <= n) {
         const uint32_t hl = holes[(ey >> 1) & (HOLE_SLOTS - 1)];
@@ -2013,6 +2055,9 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       }
       const uint64_t badm = __ballot(bad);
       const uint64_t Pc = badm ? P & ((1ull << __builtin_ctzll(badm)) - 1ull) : P;
+#if ATZ_STEP_SPLIT
+      t1 = STEP_CLOCK(); csec[1] += t1 - t0; t0 = t1;   // (diagnostics: node checks counted with steps)
+#endif
       // ---- tally the committed nodes' symbols lane-parallel, in position order
       {
         const bool mine = (Pc >> lane) & 1ull;
