@@ -364,6 +364,36 @@ struct RpEntry {
   uint8_t window = 0;
   uint8_t memlevel = 0;   // the saver's
 };
+// Saved sequences of one pipe: device memory in chunks (allocated on demand, kept across sweeps),
+// handed out by a bump pointer that each sweep resets.
+struct RpArena {
+  static constexpr uint64_t CHUNK = 1ull << 30;
+  std::vector<std::unique_ptr<DBuf>> chunks;
+  size_t cur = 0;
+  uint64_t used = 0, total = 0;   // bytes in chunks[cur]; bytes handed out this sweep
+  void reset() { cur = 0; used = 0; total = 0; }
+  uint64_t alloc(uint64_t bytes, uint64_t cap) {   // device address, 0: none (cap reached, no memory)
+    if (total + bytes > cap) return 0;
+    while (cur < chunks.size() && used + bytes > chunks[cur]->n) { cur++; used = 0; }
+    if (cur == chunks.size()) {
+      auto b = std::make_unique<DBuf>();
+      if (b->reserve(std::max(CHUNK, bytes)) != 0) { (void)hipGetLastError(); return 0; }
+      chunks.push_back(std::move(b));
+      used = 0;
+    }
+    const uint64_t a = (uint64_t)(uintptr_t)chunks[cur]->p + used;
+    used += bytes;
+    total += bytes;
+    return a;
+  }
+  bool holds(uint64_t a, uint64_t len) const {   // [a, a + len) inside one chunk
+    for (const auto& b : chunks) {
+      const uint64_t lo = (uint64_t)(uintptr_t)b->p;
+      if (a >= lo && a + len <= lo + b->n) return true;
+    }
+    return false;
+  }
+};
 struct ChainBufs {   // bucket-build job lists and scratch (one set per HIP stream that builds)
   DBuf d_cjobs, d_cjobs2, d_cjobs3, d_heads, d_heads2;
 };
@@ -385,8 +415,7 @@ struct Pipe {
   uint64_t chain_used = 0, chain_cap = 0;
   std::vector<uint32_t> streams;   // the streams whose chain tables this pipe owns
   // symbol replay: saved sequences (bump arena, reset per sweep) and per-stream entries
-  DBuf d_rp;
-  uint64_t rp_used = 0;
+  RpArena rp;
   std::vector<std::array<struct RpEntry, 9>> rp_pool;   // [stream's entry][level - 1]
   // diagnostics (ATZ_TIMING): bucket builds, and per stream the memLevels a table-reading trial used
   uint64_t diag_builds = 0;
@@ -1660,11 +1689,9 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
     } else if (e.state == 0 && bf) {
       const uint64_t sb = (4 * (n + 64) + 255) & ~255ull, tb = kind == 2 ? ((8 * n + 255) & ~255ull) : 0;
       if (!e.addr) {
-        if (c->rp_used + sb + tb > cap) continue;
-        if (c->d_rp.reserve(cap) != 0) { (void)hipGetLastError(); continue; }   // once per pipe (no replay without it)
-        e.addr = (uint64_t)(uintptr_t)c->d_rp.p + c->rp_used;
+        e.addr = c->rp.alloc(sb + tb, cap);
+        if (!e.addr) continue;
         e.tab = tb ? e.addr + sb : 0;
-        c->rp_used += sb + tb;
       }
       e.state = 1;
       e.window = t.window;
@@ -1780,9 +1807,9 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     for (int k = 1; k < 3; k++)
       for (const Trial& t : tr[k]) {   // saved sequences stay inside the arena (a bad slot would fault the GPU)
         if (!(t.mode & 12)) continue;
-        const uint64_t lo = (uint64_t)(uintptr_t)c->d_rp.p, n = x->recs[t.stream].infl_len;
-        const bool tab_ok = !(t.mode & 48) || (t.rp_tab >= lo && t.rp_tab + 8 * n <= lo + c->rp_used);
-        if (t.rp_syms < lo || t.rp_syms + 4 * (n + 64) > lo + c->rp_used || ((t.mode & 8) && t.rp_nsym > n) || !tab_ok) {
+        const uint64_t n = x->recs[t.stream].infl_len;
+        const bool tab_ok = !(t.mode & 48) || c->rp.holds(t.rp_tab, 8 * n);
+        if (!c->rp.holds(t.rp_syms, 4 * (n + 64)) || ((t.mode & 8) && t.rp_nsym > n) || !tab_ok) {
           std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
           return ATZ_E_INTERNAL;
         }
@@ -1852,9 +1879,9 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
             if (e.state == 2 && e.window == t.window) replay_from(t, e, budget_free(x, k, t));
             tr[k][i2[k][j]].mode = t.mode;
             if (t.mode & 128) continue;
-            const uint64_t lo = (uint64_t)(uintptr_t)c->d_rp.p, n = x->recs[t.stream].infl_len;
-            if ((t.mode & 8) && (t.rp_syms < lo || t.rp_syms + 4 * (n + 64) > lo + c->rp_used || t.rp_nsym > n ||
-                                 ((t.mode & 16) && (t.rp_tab < lo || t.rp_tab + 8 * n > lo + c->rp_used)))) {
+            const uint64_t n = x->recs[t.stream].infl_len;
+            if ((t.mode & 8) && (!c->rp.holds(t.rp_syms, 4 * (n + 64)) || t.rp_nsym > n ||
+                                 ((t.mode & 16) && !c->rp.holds(t.rp_tab, 8 * n)))) {
               std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
               return ATZ_E_INTERNAL;
             }
@@ -2103,7 +2130,7 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
     p->stats = atz_stats_t{};
     p->chain_used = 0;
     p->chain_cap = CHAIN_CACHE_CAP / R.np;
-    p->rp_used = 0;
+    p->rp.reset();
     p->rp_pool.clear();
     p->t_list = p->t_chains = p->t_trials = p->t_apply = 0;
     std::memset(p->kind, 0, sizeof(p->kind));
