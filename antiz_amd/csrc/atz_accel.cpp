@@ -241,6 +241,9 @@ struct StreamState {
   uint32_t full_at = ~0u;         // list index whose trial ran past its match-table prefix: rerun with a full table
   int32_t rp = -1;                // symbol-replay entries (levels 1-9) in the owning pipe's rp_pool
   bool recomp = false;
+  // levels 7-9 already run budget-free at (window, memLevel): level, longest PL a lazy read improved,
+  // longest length read (cross-level duplicates, see level_dups)
+  std::vector<std::array<uint16_t, 5>> xl;   // {window, memLevel, level, imp, len}
 };
 
 
@@ -357,6 +360,7 @@ struct KTimer {   // HIP events bracketing kernel launches on the library stream
 // A saved symbol sequence of (stream, level): the first trial at that level whose chain walks cannot
 // reach their budget saves it; later ones at that level replay it (see plan_replay, trial_body).
 struct RpEntry {
+  uint32_t reads_max = 0;   // the saver's TrialRes::reads_max (its whole parse)
   uint64_t addr = 0;      // device address of the arena slot (n + 64 symbols, then n table entries for slow levels)
   uint64_t tab = 0;       // its match-table part (0: none)
   uint32_t nsym = 0, flags = 0;
@@ -1358,6 +1362,12 @@ static uint64_t match_prefix(uint64_t n, int memlevel) {
   return std::min(n, x);
 }
 
+static uint32_t lazy_host(uint32_t level) {   // max_lazy of levels 7-9 (Z/deflate.c:141-143)
+  return level == 7 ? 32u : level == 8 ? 128u : 258u;
+}
+static uint32_t nice_host(uint32_t level) {   // nice_length of levels 7-9
+  return level == 7 ? 128u : 258u;
+}
 static uint64_t c_cfg_host(uint32_t level) {   // max_chain of a level (Z/deflate.c:131-143)
   static const uint16_t chain[10] = {0, 4, 8, 32, 16, 32, 128, 256, 1024, 4096};
   return chain[level < 10 ? level : 9];
@@ -1658,6 +1668,50 @@ static bool budget_free(atz_ctx* x, int kind, const Trial& t) {
   return x->depth_pin.as<uint32_t>()[10 * (size_t)t.stream + t.memlevel] <= Bq;
 }
 
+// Cross-level duplicates.  Levels 7, 8 and 9 write the same zlib header (FLEVEL 3) and differ only in
+// good_length, max_lazy, nice_length and max_chain (Z/deflate.c:141-143).  When both levels are
+// budget-free at the stream's (window, memLevel) -- every walk visits all its same-trigram nodes,
+// under either budget, so good_length has no effect -- a level-L' trial parses exactly like an
+// earlier level-L trial there if, over what that trial parsed, no read length reached L''s
+// nice_length (its walks would stop no earlier) and no lazy read improved a match of length >= L''s
+// max_lazy (the reads L' skips are ones that did not change the parse).  Same symbols, same
+// blocks, same header: the output, and so the result, is the earlier trial's, which the stream's
+// rule already applied without stopping.  Such a trial is not launched (mode bit 7).
+static bool budget_free(atz_ctx* x, int kind, const Trial& t);
+static void level_dups(atz_ctx* x, std::vector<StreamState>& ss, std::vector<Trial>& slow) {
+  for (Trial& t : slow) {
+    if (t.clevel < 7 || t.clevel > 9 || (t.mode & 1)) continue;
+    const StreamState& st = ss[t.stream];
+    for (const auto& r : st.xl) {
+      if (r[0] != t.window || r[1] != t.memlevel || r[2] == t.clevel) continue;
+      if (r[3] < lazy_host(t.clevel) && r[4] < nice_host(t.clevel) && budget_free(x, 2, t)) t.mode |= 128;
+      break;
+    }
+  }
+}
+// after a round: what the budget-free level-7-9 trials that ran parsed (a replay parsed its saver's
+// whole sequence)
+static void level_record(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, const std::vector<Trial>& slow,
+                         const std::vector<TrialRes>& res) {
+  for (size_t q = 0; q < slow.size(); q++) {
+    const Trial& t = slow[q];
+    const TrialRes& r = res[q];
+    if (t.clevel < 7 || t.clevel > 9 || (t.mode & 128) || r.state == TR_NEED_R || r.state == TR_OVERFLOW) continue;
+    if (!budget_free(x, 2, t)) continue;
+    StreamState& st = ss[t.stream];
+    bool have = false;
+    for (const auto& e : st.xl) have |= e[0] == t.window && e[1] == t.memlevel;
+    if (have) continue;
+    uint32_t rm = r.reads_max;
+    if (r.saved_flags & 4) {   // a replay: its saver's reads
+      if (st.rp < 0) continue;
+      rm = c->rp_pool[st.rp][t.clevel - 1].reads_max;
+    }
+    st.xl.push_back({(uint16_t)t.window, (uint16_t)t.memlevel, (uint16_t)t.clevel, (uint16_t)(rm >> 16),
+                     (uint16_t)(rm & 0xffffu)});
+  }
+}
+
 // Symbol replay (trial_body).  A trial at level L, window w, memLevel m whose deepest bucket holds at
 // most B + 1 positions is "budget-free": its walks cannot reach their budget, so they walk exactly
 // like those of every other budget-free memLevel (B = max_chain for deflate_fast, levels 1-3, whose
@@ -1672,7 +1726,7 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
   const bool checked = replay_mode() != 3 && kind == 2;   // ATZ_REPLAY=3: budget-free replays only
   for (size_t q = 0; q < trs.size(); q++) {
     Trial& t = trs[q];
-    if (t.clevel < 1 || t.clevel > 9 || (t.mode & 1)) continue;
+    if (t.clevel < 1 || t.clevel > 9 || (t.mode & (1 | 128))) continue;
     const uint64_t n = x->recs[t.stream].infl_len;
     const uint64_t wsz = 1ull << t.window;
     if (n > wsz + (wsz - 262)) continue;                                  // the window may slide
@@ -1788,6 +1842,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     if (replay_on() && x->depth_pin.p) {
       if (int r = ensure_depths(x, c, need)) return r;
       HIPCHK(hipStreamSynchronize(c->st));
+      if (dedup_on()) level_dups(x, ss, tr[2]);
       for (int k = 1; k < 3; k++) plan_replay(x, c, ss, k, tr[k], savers);
       need.clear();
       for (int k = 1; k < 3; k++)
@@ -1835,7 +1890,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         const TrialRes& r = trres[sv[0]][sv[1]];
         RpEntry& e = c->rp_pool[sv[2]][sv[3]];
         if (r.state != TR_NEED_R && (r.saved_flags & 1u)) {
-          e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags;
+          e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags; e.reads_max = r.reads_max;
         } else {
           e.state = 0;   // the slot stays for the next saving trial
         }
@@ -1893,6 +1948,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
           for (size_t j = 0; j < i3[k].size(); j++) trres[k][i3[k][j]] = r2[k][j];
       }
     }
+    if (dedup_on() && x->depth_pin.p) level_record(x, c, ss, tr[2], trres[2]);
     auto tc = std::chrono::steady_clock::now();
     for (int k = 1; k < 3; k++)
       for (size_t q = 0; q < tr[k].size(); q++) {

@@ -95,6 +95,8 @@ struct TrialRes {
   uint32_t saved_syms;  // mode bit2: symbols saved at rp_syms
   uint32_t saved_flags; // bit0: the whole input was parsed (the sequence is complete), bit1: end-of-input
                         // literal, bit2: the trial replayed a saved sequence
+  uint32_t reads_max;   // slow parses: (longest prev_length a lazy read improved) << 16 | longest length read
+  uint32_t pad_;
 };
 enum : uint32_t {
   TR_FULL = 0,        // full output produced and compared: ident valid

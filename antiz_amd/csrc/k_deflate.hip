@@ -1755,6 +1755,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   }
   uint32_t sbase = 0;            // symbols in the flushed blocks
   uint32_t saved_flags = 0;
+  uint32_t run_len = 0, run_imp = 0;   // slow parses: longest match length any of its reads saw, longest
+                                       // prev_length a lazy read improved (per lane, reduced at the end)
   b.cyc_tree = b.cyc_emit = b.blocks = 0;
   b.cyc_heap = b.cyc_scan = b.cyc_send = 0;
   const uint64_t cstart = clock64();
@@ -2234,6 +2236,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       const uint32_t x = wb + lane;
       uint32_t wt = 0, nxt = 0, c = 0, L = 0, D = 0;
       uint32_t rd_last = 0, rd_ey = ~0u;   // rec: last entry the walk read, first quarter-budget read
+      uint32_t w_len = 0, w_imp = 0;       // longest length the walk read; longest PL a lazy read improved
       if (x < n) {
         uint32_t qq = x, PL = 2, PD = 0;
         for (;;) {
@@ -2254,6 +2257,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           }
           if (PL == 2) {   // first iteration of the walk (qq == x)
             const uint32_t len = ex >> 23, dist = (ex >> 8) & 0x7fffu;
+            if (hv && len > w_len) w_len = len;
             uint32_t ML = hv && len > 2 ? len : 2u;
             if (ML == 3 && dist > 4096) ML = 2;   // TOO_FAR
             if (ML == 2) { wt = 1; nxt = x + 1; break; }
@@ -2263,7 +2267,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           if (PL < z.lazy && hv) {
             const uint32_t ev = PL >= z.good ? ey : ex;
             const uint32_t len = ev >> 23;
-            if (len > PL) { PL = len; PD = (ev >> 8) & 0x7fffu; c++; qq++; continue; }
+            if (len > w_len) w_len = len;
+            if (len > PL) { if (PL > w_imp) w_imp = PL; PL = len; PD = (ev >> 8) & 0x7fffu; c++; qq++; continue; }
           }
           wt = 2; L = PL; D = PD; nxt = qq - 1 + PL;
           break;
@@ -2279,6 +2284,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       path_lane(wp, Am, ma, lane, onp, mab);
       need = wp.need;
       const uint32_t qn = wb + wp.end;
+      if (onp && (wt == 1 || wt == 2)) {   // the parse's own walks (diagnostics for level equivalence)
+        run_len = w_len > run_len ? w_len : run_len;
+        run_imp = w_imp > run_imp ? w_imp : run_imp;
+      }
       if (rec && onp && (wt == 1 || wt == 2))   // the walk's reads: x full-budget, then by PL
         for (uint32_t i = x; i <= rd_last; i++) {
           const uint64_t e64 = ring[i & (RING_SLOW - 1)];
@@ -2381,6 +2390,15 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       else state = TR_FULL;
     }
   }
+  uint32_t rmax = (run_imp << 16) | run_len;   // both < 2^16: per-field maxima by two reductions
+  {
+    uint32_t a = run_imp, bl = run_len;
+    for (int d = 32; d >= 1; d >>= 1) {
+      const uint32_t oa = __shfl_xor(a, d, 64), ob = __shfl_xor(bl, d, 64);
+      a = a > oa ? a : oa; bl = bl > ob ? bl : ob;
+    }
+    rmax = (a << 16) | bl;
+  }
   if (lane == 0) {
     TrialRes r;
     r.state = state;
@@ -2401,6 +2419,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     r.cyc_fallback = cyc_fb;
     r.saved_syms = sbase;
     r.saved_flags = saved_flags;
+    r.reads_max = rmax;
     A.res[t] = r;
   }
 }
