@@ -36,7 +36,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n_streams, seed, ctx):
+def cpu_baseline(n_streams, seed, ctx, workload="c4"):
     """Time the real reference binary on a bounded sample of the workload (1 thread), and check that
     the library's .atz of the same sample is byte-identical to the reference's (parity at the bench
     configuration: same generator, seed and options, 3 sweep pipes)."""
@@ -45,12 +45,12 @@ def cpu_baseline(n_streams, seed, ctx):
     ref = os.path.join(ROOT, "oracle", "_ref", "uncomp")
     if not os.path.exists(ref):
         return None
-    data = datagen.gen_c4(seed=seed, n_streams=n_streams)
+    data = datagen.CONFIGS[workload](seed=seed, n_streams=n_streams)
     d = tempfile.mkdtemp(prefix="atzcpu")
     p = os.path.join(d, "sample.bin")
     with open(p, "wb") as f:
         f.write(data)
-    cmd = [ref, "-i", p, "-o", p + ".atz", "--notest"]
+    cmd = [ref, "-i", p, "-o", p + ".atz", "--notest"] + (["--brute-window"] if workload == "c5" else [])
     try:
         cmd = ["taskset", "-c", "0"] + cmd if subprocess.run(["which", "taskset"], capture_output=True).returncode == 0 else cmd
         t0 = time.perf_counter()
@@ -75,7 +75,8 @@ def cpu_baseline(n_streams, seed, ctx):
     return {"value": round(len(data) / 1e6 / dt, 4), "unit": "MB/s", "cores": 1, "kind": "reference",
             "atz_identical_to_reference": same, "atz_sha256": ref_sha[:16],
             "sample": "%d-stream prefix config of the same generator (%.1f MB, seed %d), oracle/_ref/uncomp --notest, "
-                      "%.1f s wall" % (n_streams, len(data) / 1e6, seed, dt)}
+                      "%.1f s wall" % (n_streams, len(data) / 1e6, seed, dt)
+                      + (" --brute-window" if workload == "c5" else "")}
 
 
 def hip_copy(dst, src, n):
@@ -132,6 +133,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-recon", action="store_true", help="skip the reconstruct (-r / verify) measurement")
     ap.add_argument("--cache", default=os.environ.get("ATZ_BENCH_CACHE", "/tmp/atz_bench_cache"))
+    ap.add_argument("--workload", choices=("c4", "c5"), default="c4",
+                    help="c4: the metric's workload (BASELINE configs[3]); c5: configs[4], the same generator with "
+                         "windowBits U10-15 and --brute-window (a measurement beside the metric, not its value)")
     ap.add_argument("--mode", choices=("shards", "file"), default="shards",
                     help="shards: every rank precompresses its own 1 GB file (weak scaling, no data-path "
                          "collective); file: ONE 1 GB file split over the ranks (antiz_amd.shard: all-gather "
@@ -158,9 +162,10 @@ def main():
     import antiz_amd
     from antiz_amd import datagen
 
-    seed = 4 + rank if args.mode == "shards" else 4
+    base = 4 if args.workload == "c4" else 5
+    seed = base + rank if args.mode == "shards" else base
     t0 = time.time()
-    path = datagen.cached("c4", args.cache, seed=seed, n_streams=args.streams)
+    path = datagen.cached(args.workload, args.cache, seed=seed, n_streams=args.streams)
     with open(path, "rb") as f:
         data = f.read()
     log("rank %d: workload %s (%.1f MB) ready in %.1fs" % (rank, os.path.basename(path), len(data) / 1e6, time.time() - t0))
@@ -169,7 +174,7 @@ def main():
     dev = host.to("cuda", non_blocking=False)
     torch.cuda.synchronize()
 
-    ctx = antiz_amd.Context(device=local)
+    ctx = antiz_amd.Context(device=local, brute_window=args.workload == "c5")
     group = None
 
     def step():
@@ -242,7 +247,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.cpu_sample_streams, seed, ctx)
+        cpu = cpu_baseline(args.cpu_sample_streams, seed, ctx, args.workload)
 
     if rank == 0:
         out = {
@@ -257,10 +262,13 @@ def main():
             "scaling": "weak" if args.mode == "shards" else "strong",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (antiz_amd.datagen C4, seed %s; text from a seeded 20k-word vocabulary)"
-                    % ("4+rank" if args.mode == "shards" else "4"),
+            "data": "synthetic (antiz_amd.datagen %s, seed %s; text from a seeded 20k-word vocabulary)"
+                    % (args.workload.upper(), ("%d+rank" if args.mode == "shards" else "%d") % base),
             "config": ({"workload": "C4: %d zlib streams (clevel U1-9, memLevel U1-9, w15), %.3f GB per GPU, "
-                                    "default thresholds" % (args.streams, len(data) / 1e9),
+                                    "default thresholds" % (args.streams, len(data) / 1e9)
+                                    if args.workload == "c4" else
+                                    "C5: %d zlib streams (clevel U1-9, memLevel U1-9, windowBits U10-15), %.3f GB "
+                                    "per GPU, --brute-window, default thresholds" % (args.streams, len(data) / 1e9),
                         "streams_per_gpu": args.streams, "bytes_per_gpu": len(data),
                         "parallelism": "stream-sharded dp%d" % world}
                        if args.mode == "shards" else

@@ -297,6 +297,28 @@ def test_bench_config_slice_matches_oracle(atz):
         assert sha(out) == sha(ref)
 
 
+def test_c5_brute_window_slice_matches_oracle(atz):
+    """BASELINE configs[4] (C5) as a parity case: the first 900 streams of `bench.py --workload c5`
+    (windowBits U10-15, seed 5) with --brute-window, so the sweep runs every header window and, for
+    streams left >= mismatch_tol short, the extra windows (main.cpp:590-600).  The scan table, each
+    stream's chosen (clevel, window, memLevel), ident and recomp, and the .atz bytes must equal the
+    oracle's."""
+    from antiz_amd import datagen
+    data = datagen.gen_c5(seed=5, n_streams=900, workers=4)
+    rc, ref, st_ref = _libs.ora_precompress(data, brute=1)
+    assert rc == 0
+    with atz.Context(brute_window=True) as c:
+        recs = c.scan(data)
+        assert [r[:4] for r in recs] == [(s["offset"], s["type"], s["comp_len"], s["infl_len"]) for s in st_ref["streams"]]
+        res, _ = c.sweep()
+        got = [(r["clevel"], r["window"], r["memlevel"], r["ident"], r["recomp"]) for r in res]
+        exp = [(s["clevel"], s["window"], s["memlevel"], s["ident"], s["recomp"]) for s in st_ref["streams"]]
+        assert got == exp
+        assert len({s["window"] for s in st_ref["streams"]}) == 6
+        out, st = c.precompress(data)
+        assert sha(out) == sha(ref)
+
+
 def test_reconstruct_rejects_crafted_atz(atz):
     """Size fields of an ATZ1 file are untrusted: counts and lengths that overflow, overlap or point
     past the file must give ATZ_E_FORMAT (the reference would abort or read out of bounds), never a
