@@ -1667,6 +1667,16 @@ static bool budget_free(atz_ctx* x, int kind, const Trial& t) {
   const uint32_t Bq = (uint32_t)(c_cfg_host(t.clevel) >> (kind == 1 ? 0 : 2));
   return x->depth_pin.as<uint32_t>()[10 * (size_t)t.stream + t.memlevel] <= Bq;
 }
+// Budget-free AND memLevel-free: a node at distance exactly MAX_DIST is walked when it is the hash
+// head (deflate_fast / deflate_slow test strstart - hash_head <= MAX_DIST) but not as a chain
+// successor (longest_match continues only while cur_match > strstart - MAX_DIST, Z/deflate.c:1227),
+// so whether it is visited depends on which other trigrams share its bucket, i.e. on the memLevel.
+// Replays across memLevels are therefore exact only for streams in which no candidate can sit at
+// that distance (n <= MAX_DIST); levels at one memLevel (level_dups) share the buckets and are not
+// affected.  (Found on the C5 workload: w13 streams of 13-16 KB.)
+static bool replay_free(atz_ctx* x, int kind, const Trial& t) {
+  return x->recs[t.stream].infl_len <= (1ull << t.window) - 262 && budget_free(x, kind, t);
+}
 
 // Cross-level duplicates.  Levels 7, 8 and 9 write the same zlib header (FLEVEL 3) and differ only in
 // good_length, max_lazy, nice_length and max_chain (Z/deflate.c:141-143).  When both levels are
@@ -1730,7 +1740,7 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
     const uint64_t n = x->recs[t.stream].infl_len;
     const uint64_t wsz = 1ull << t.window;
     if (n > wsz + (wsz - 262)) continue;                                  // the window may slide
-    const bool bf = budget_free(x, kind, t);
+    const bool bf = replay_free(x, kind, t);
     if (!bf && !checked) continue;
     StreamState& st = ss[t.stream];
     if (st.rp < 0) { st.rp = (int32_t)c->rp_pool.size(); c->rp_pool.emplace_back(); }
@@ -1931,7 +1941,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
             Trial& t = t2[k][j];
             t.mode &= ~64u;
             const RpEntry& e = c->rp_pool[ss[t.stream].rp][t.clevel - 1];
-            if (e.state == 2 && e.window == t.window) replay_from(t, e, budget_free(x, k, t));
+            if (e.state == 2 && e.window == t.window) replay_from(t, e, replay_free(x, k, t));
             tr[k][i2[k][j]].mode = t.mode;
             if (t.mode & 128) continue;
             const uint64_t n = x->recs[t.stream].infl_len;

@@ -2025,7 +2025,18 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         const uint32_t hl = holes[(ey >> 1) & (HOLE_SLOTS - 1)];
         bool exact = hl == 0 || hl - 1u < x - (ey >> 16);
         if (!exact && !((ey >> 12) & 1u)) {
-          if ((ex >> 23) <= 2) exact = true;
+          // Skipped nodes only shrink the visited set -- except at the MAX_DIST edge: deflate_fast
+          // walks its hash head at distance MAX_DIST (Z/deflate.c:1660) but later chain nodes only
+          // above it (Z/deflate.c:1227), so when holes above it made a hole the table's head, the
+          // node at exactly x - MAX_DIST can be examined by deflate_fast and not by the table walk.
+          // Such a node is resolved by the exact walk below.
+          const uint32_t q0 = x - maxd;
+          const uint32_t hb = tr.memlevel + 7u, hs = (hb + 2u) / 3u, hm = (1u << hb) - 1u;
+          const bool edge = x > maxd && q0 > Sx &&
+                            ((((uint32_t)in[q0] << (2u * hs)) ^ ((uint32_t)in[q0 + 1] << hs) ^ in[q0 + 2]) & hm) ==
+                            ((((uint32_t)in[x] << (2u * hs)) ^ ((uint32_t)in[x + 1] << hs) ^ in[x + 2]) & hm);
+          if (edge) exact = false;
+          else if ((ex >> 23) <= 2) exact = true;
           else {
             const uint32_t wpos = x - ((ex >> 8) & 0x7fffu);
             exact = wpos > Sx && ins_get(wpos);

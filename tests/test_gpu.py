@@ -319,6 +319,36 @@ def test_c5_brute_window_slice_matches_oracle(atz):
         assert sha(out) == sha(ref)
 
 
+MAXDIST_EDGE_SHA = "d75a2a586f840cd037952b7289852f11c4702d92dbefef4b6112824d68680f32"   # real reference
+
+
+def test_maxdist_edge_streams(atz):
+    """The MAX_DIST edge (tests/golden/maxdist_edge.bin, pinned by the real reference in
+    test_oracle.py): deflate_fast walks a hash head at distance exactly MAX_DIST but later chain nodes
+    only above it, so (a) a hole that is the table's head can hide such a node from the table walk
+    (w11 stream, levels 1-3), and (b) symbol replays across memLevels are not exact for streams
+    longer than MAX_DIST (w13/w14 streams).  One-shot deflates at every (clevel, memLevel) of each
+    stream's window against the oracle, and the ATZ1 bytes with and without --brute-window."""
+    import zlib
+    data = open(os.path.join(GOLD, "maxdist_edge.bin"), "rb").read()
+    with atz.Context() as c:
+        recs = c.scan(data)
+        assert len(recs) == 11
+        bad = []
+        for off, typ, cl, il in (r[:4] for r in recs):
+            d = zlib.decompress(data[off:off + cl])
+            w = 10 + typ // 4
+            for lv in range(1, 10):
+                for m in range(1, 10):
+                    if c.deflate(d, lv, w, m) != _libs.ora_deflate(d, lv, w, m)[0]:
+                        bad.append((off, lv, w, m))
+        assert not bad, bad[:10]
+    for brute in (False, True):
+        with atz.Context(brute_window=brute) as c:
+            out, _ = c.precompress(data)
+            assert sha(out) == MAXDIST_EDGE_SHA
+
+
 def test_reconstruct_rejects_crafted_atz(atz):
     """Size fields of an ATZ1 file are untrusted: counts and lengths that overflow, overlap or point
     past the file must give ATZ_E_FORMAT (the reference would abort or read out of bounds), never a

@@ -98,3 +98,18 @@ def test_live_reference_deflate_inflate_sample():
         assert (st == 0) == (rl == 1)
         if st == 0:
             assert prod == to
+
+
+MAXDIST_EDGE_SHA = "d75a2a586f840cd037952b7289852f11c4702d92dbefef4b6112824d68680f32"
+
+
+def test_maxdist_edge_fixture_pinned():
+    """tests/golden/maxdist_edge.bin: 11 streams of the C5 workload (windowBits 11, 13, 14; longer than
+    MAX_DIST) whose parses hinge on a hash head at distance exactly MAX_DIST (walked as a head, not as
+    a chain successor: Z/deflate.c:1227, 1660, 1766).  The expected ATZ1 SHA-256 was produced by the
+    real reference (oracle/_ref/uncomp, with and without --brute-window: the same bytes); the oracle
+    must agree."""
+    data = open(os.path.join(G.GOLD, "maxdist_edge.bin"), "rb").read()
+    for brute in (0, 1):
+        rc, out, _ = _libs.ora_precompress(data, brute=brute)
+        assert rc == 0 and hashlib.sha256(out).hexdigest() == MAXDIST_EDGE_SHA
