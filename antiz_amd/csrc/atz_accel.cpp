@@ -565,6 +565,7 @@ static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, con
                             bool arena_reset = true) {
   res.resize(jobs.size());
   if (jobs.empty()) return 0;
+  auto ti0 = std::chrono::steady_clock::now();
   if (int r = upload(c, c->d_jobs, jobs.data(), jobs.size() * sizeof(InfJob))) return r;
   if (int r = c->d_res.reserve(jobs.size() * sizeof(InfRes))) return r;
   if (int r = c->d_arena_used.reserve(64)) return r;
@@ -588,9 +589,14 @@ static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, con
                        c->d_arena_used.as<unsigned long long>(), arena_cap);
   kend(c);
   KCHECK("k_inflate");
+  const double ti_launch = ms_since(ti0);
   HIPCHK(hipMemcpyAsync(res.data(), c->d_res.p, n * sizeof(InfRes), hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
+  const double ti_sync = ms_since(ti0);
   kcollect(c);
+  if (timing_level() >= 2)
+    std::fprintf(stderr, "atz: inflate jobs %u: launched at %.2f ms, synced at %.2f ms, collected at %.2f ms\n", n,
+                 ti_launch, ti_sync, ms_since(ti0));
   if (small) {   // jobs whose far history was lost (arena full / slot overflowed): 32 KiB ring, no slot
     std::vector<InfJob> rj;
     std::vector<uint32_t> ri;
@@ -853,6 +859,7 @@ static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, Sca
       if (k >= 0) todo.push_back(j);
     }
     c->stats.n_continuations += todo.size();
+    TMARK("scan: cont select");
     for (int pass = 0; pass < 2 && !todo.empty(); pass++) {
       std::vector<Seg> segs;
       std::vector<uint8_t> meta;
@@ -878,9 +885,11 @@ static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, Sca
         cj.push_back(jb2);
         out = (out + 3) & ~3ull;
       }
+      TMARK("scan: cont segs");
       if (int r = upload(c, c->d_meta, meta.data(), meta.size())) return r;
       if (int r = upload(c, c->d_segs, segs.data(), segs.size() * sizeof(Seg))) return r;
       if (int r = c->d_virt.reserve(out + 4096)) return r;
+      TMARK("scan: cont upload+reserve");
       const uint32_t nseg = (uint32_t)segs.size();
       const uint32_t blocks = std::min<uint32_t>((nseg + 3) / 4, 65535u);
       kbeg(c, 3);
@@ -888,6 +897,7 @@ static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, Sca
                          c->d_virt.as<uint8_t>(), c->d_segs.as<Seg>(), nseg);
       kend(c);
       KCHECK("k_gather");
+      TMARK("scan: cont gather launch");
       std::vector<InfRes> cr;
       if (int r = run_inflate_jobs(c, c->d_virt.as<uint8_t>(), nullptr, cj, cr, S.arena_cap, false, false)) return r;
       if (timing_on()) {
@@ -1776,6 +1786,16 @@ static uint64_t round_budget_bytes() {
 }
 // The sweep of the streams c->streams on pipe c (per-kind x level counters: count, cycles
 // total/tree/emit/heap/fallback, parsed bytes, symbols, scan/send cycles, parse window phases).
+static size_t tail_active() {   // ATZ_TAIL_ACTIVE=n: rounds with fewer active streams use tail_target()
+  static long v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_TAIL_ACTIVE"); v = e ? std::max(0L, std::atol(e)) : 0; }
+  return (size_t)v;
+}
+static size_t tail_target() {   // ATZ_TAIL_TARGET=n: trials per round and pipe in the tail
+  static long v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_TAIL_TARGET"); v = e ? std::max(256L, std::atol(e)) : 4096; }
+  return (size_t)v;
+}
 static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss, size_t target) {
   auto t0 = std::chrono::steady_clock::now();
   std::vector<uint32_t> active;
@@ -1805,7 +1825,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       active.resize(chunk);
     }
     const auto tl0 = std::chrono::steady_clock::now();
-    const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, target / active.size()));
+    // the sweep's tail (few active streams) is latency-bound: every round costs about its slowest
+    // trial, so below tail_active() streams a round speculates deeper (tail_target() trials)
+    const size_t tgt = active.size() < tail_active() ? std::max(target, tail_target()) : target;
+    const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, tgt / active.size()));
     std::vector<std::pair<uint32_t, int>> need;
     for (int k = 0; k < 3; k++) tr[k].clear();
     // per stream, its trials of this round in list order: (kind, index in tr[kind])
@@ -2445,16 +2468,31 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
   std::vector<StreamState> ss;
   SweepRun R;
   SweepGuard guard{c, R};
-  if (int r = sweep_begin(c, d_file, ss, n_max, R)) return r;
   const uint32_t nch = (uint32_t)S.chunks.size();
   const uint32_t P = std::max<uint32_t>(1, std::min(scan_pieces(), nch));
   while (c->slabs.size() < P) c->slabs.emplace_back(new DBuf());
+  // The sweep's host set-up (per-record tables sized for every candidate, pipe threads) runs on a
+  // helper thread while the first piece's candidate inflates keep the GPU busy; with one piece
+  // nothing reaches the pipes before that piece is scanned anyway.  (It touches no state of the
+  // scan: c->recs, the scan buffers and the arena are the scan's; infl_off / adler are resized
+  // here before inflate_records reads them.)
+  int rc_begin = 0;
+  std::thread t_begin([&]() {
+    auto tsb = std::chrono::steady_clock::now();
+    rc_begin = sweep_begin(c, d_file, ss, n_max, R);
+    if (timing_on()) std::fprintf(stderr, "atz: sweep begin (%zu slots)       %9.2f ms\n", n_max, ms_since(tsb));
+  });
+  struct Join { std::thread& t; ~Join() { if (t.joinable()) t.join(); } } join_begin{t_begin};
   double scan_busy = ms_since(t0);
   for (uint32_t p = 0; p < P; p++) {
     auto tp = std::chrono::steady_clock::now();
     const uint32_t ja = (uint32_t)((uint64_t)nch * p / P), jb = (uint32_t)((uint64_t)nch * (p + 1) / P);
     const size_t r0 = c->recs.size();
     if (int r = scan_piece(c, h, d_file, S, ja, jb)) return r;
+    if (p == 0) {
+      t_begin.join();
+      if (rc_begin) return rc_begin;
+    }
     const size_t r1 = c->recs.size();
     if (int r = inflate_records(c, d_file, F, r0, r1, *c->slabs[p])) return r;
     if (int r = sweep_publish(c, R, r0, r1)) return r;
