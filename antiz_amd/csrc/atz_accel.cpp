@@ -1097,7 +1097,7 @@ static bool bucket_verify() {   // ATZ_BUCKETS_VERIFY=1 (read per call): check k
   const char* e = std::getenv("ATZ_BUCKETS_VERIFY");
   return e && std::atoi(e) != 0;
 }
-static constexpr uint32_t BSORT_MAX_NPAD = ((160u * 1024u - 256u - BSORT_CNT_BYTES) / 6u) & ~63u;   // LDS limit (256 B static)
+static constexpr uint32_t BSORT_MAX_NPAD = std::min<uint32_t>(65472u, ((160u * 1024u - 256u - BSORT_CNT_BYTES) / BSORT_BYTES_PER_POS) & ~63u);   // LDS limit (256 B static)
 static_assert(bsort_lds_bytes(BSORT_MAX_NPAD) + 256u <= 160u * 1024u && BSORT_MAX_NPAD < 65536u, "k_buckets_sort LDS class");
 // prefetch builds finished: fold their kernel times into the pipe's counters
 static int chains_prefetch_collect(Pipe* c) {

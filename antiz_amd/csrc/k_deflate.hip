@@ -385,10 +385,19 @@ __global__ __launch_bounds__(256) void k_buckets_pk(const uint8_t* __restrict__ 
 // digit-major, wave-minor order, and the waves scatter their tiles in order.  A final sweep over
 // the sorted order writes bpos (first entry of a hash flagged BUCKET_FIRST) and sidx.  The result
 // is the unique (hash, position) order, so it is identical to the other kernels' output.
-// LDS: 6 bytes per position + 2 bytes per (digit, wave); streams of < 64 Ki positions.
+// LDS: 2 (ATZ_BSORT_GLOBAL) or 6 bytes per position + 2 bytes per (digit, wave); streams of < 64 Ki positions.
+// ATZ_BSORT_GLOBAL=1 (default): only the hashes stay in LDS (2 bytes per position); the first pass
+// scatters into the sidx array (overwritten at the end) and the second straight into bpos, both in
+// HBM (L2-resident: 8 bytes per position), so two blocks fit a CU and a sort leaves LDS for the trial
+// blocks of the other pipes.  C4 A/B (2 runs each, one box): k_chains 338-362 -> 262-298 ms summed,
+// 1076-1116 -> 1105-1133 MB/s.  0: positions in LDS too (6 bytes per position, one block per CU).
+#ifndef ATZ_BSORT_GLOBAL
+#define ATZ_BSORT_GLOBAL 1
+#endif
 static constexpr uint32_t BSORT_THREADS = 1024, BSORT_W = BSORT_THREADS / 64;
 static constexpr uint32_t BSORT_CNT_BYTES = 256 * BSORT_W * 2;
-__host__ __device__ constexpr uint32_t bsort_lds_bytes(uint32_t npad) { return 6 * npad + BSORT_CNT_BYTES; }
+static constexpr uint32_t BSORT_BYTES_PER_POS = ATZ_BSORT_GLOBAL ? 2 : 6;
+__host__ __device__ constexpr uint32_t bsort_lds_bytes(uint32_t npad) { return BSORT_BYTES_PER_POS * npad + BSORT_CNT_BYTES; }
 // lanes of the wave (among `valid` ones) whose `bits`-bit digit equals this lane's
 __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, uint32_t bits) {
   uint64_t m = __ballot(valid);
@@ -417,9 +426,13 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
   const uint32_t hbits = jb.memlevel + 7, hmask = (1u << hbits) - 1, hshift = (hbits + 2) / 3;
   const uint32_t nh = n >= 3 ? n - 2 : 0;
   LDS uint16_t* H = (LDS uint16_t*)dyn_lds;   // hash of position p
+#if ATZ_BSORT_GLOBAL
+  LDS uint16_t* cnt = H + npad;               // [digit * BSORT_W + wave]: count, then output offset
+#else
   LDS uint16_t* A = H + npad;                 // positions after the low-digit pass
   LDS uint16_t* Bo = A + npad;                // positions in (hash, position) order
   LDS uint16_t* cnt = Bo + npad;              // [digit * BSORT_W + wave]: count, then output offset
+#endif
   for (uint32_t p = tid; p < nh; p += BSORT_THREADS)
     H[p] = (uint16_t)((((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask);
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -427,7 +440,7 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
   const uint32_t t0 = (uint32_t)wave * T < nh ? (uint32_t)wave * T : nh;
   const uint32_t t1 = t0 + T < nh ? t0 + T : nh;
   // one stable counting-sort pass: digit (H[p] >> shift) & (2^bits - 1) of p = src ? src[i] : i
-  auto pass = [&](const LDS uint16_t* src, LDS uint16_t* dst, uint32_t shift, uint32_t bits) {
+  auto pass = [&](auto src, auto dst, uint32_t shift, uint32_t bits) {
     const uint32_t dmask = (1u << bits) - 1;
     __syncthreads();   // H / the previous pass's dst written, its scatter done with cnt
     for (uint32_t i = tid; i < 256 * BSORT_W; i += BSORT_THREADS) cnt[i] = 0;
@@ -467,18 +480,27 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
       const uint64_t pm = digit_peers(d, valid, bits);
       const uint32_t base = valid ? (uint32_t)cnt[d * BSORT_W + wave] : 0u;
       if (valid) {
-        dst[base + (uint32_t)__popcll(pm & lt)] = (uint16_t)p;
+        dst[base + (uint32_t)__popcll(pm & lt)] = p;
         if ((pm & lt) == 0) cnt[d * BSORT_W + wave] = (uint16_t)(base + (uint32_t)__popcll(pm));
       }
     }
   };
   static_assert(256 * BSORT_W == 4 * BSORT_THREADS, "the scan takes 4 counters per thread");
+#if ATZ_BSORT_GLOBAL
   if (hbits <= 8) {
-    pass(nullptr, Bo, 0, hbits);
+    pass((const uint32_t*)nullptr, bpos, 0, hbits);
   } else {
-    pass(nullptr, A, 0, hbits - 8);
-    pass(A, Bo, hbits - 8, 8);
+    pass((const uint32_t*)nullptr, sidx, 0, hbits - 8);
+    pass((const uint32_t*)sidx, bpos, hbits - 8, 8);
   }
+#else
+  if (hbits <= 8) {
+    pass((const LDS uint16_t*)nullptr, Bo, 0, hbits);
+  } else {
+    pass((const LDS uint16_t*)nullptr, A, 0, hbits - 8);
+    pass((const LDS uint16_t*)A, Bo, hbits - 8, 8);
+  }
+#endif
   __syncthreads();
   // per wave, its contiguous tile [t0, t1) of the sorted order: bucket starts by ballot, and (when
   // asked) the deepest bucket, as the largest distance from an element back to its bucket's start
@@ -492,8 +514,14 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
   for (uint32_t i0 = t0; i0 < t1; i0 += 64) {
     const uint32_t i = i0 + (uint32_t)lane;
     const bool valid = i < t1;
+#if ATZ_BSORT_GLOBAL
+    // bpos[i - 1] may already carry its flag (written by the lane or wave that owns it)
+    const uint32_t p = valid ? bpos[i] & ~BUCKET_FIRST : 0u;
+    const bool first = valid && (i == 0 || H[bpos[i - 1] & ~BUCKET_FIRST] != H[p]);
+#else
     const uint32_t p = valid ? (uint32_t)Bo[i] : 0u;
     const bool first = valid && (i == 0 || H[Bo[i - 1]] != H[p]);
+#endif
     if (valid) {
       bpos[i] = p | (first ? BUCKET_FIRST : 0u);
       sidx[p] = i;
