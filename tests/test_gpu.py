@@ -504,3 +504,46 @@ def test_symbol_replay_matches_oracle(atz):
         assert st["n_trials_duplicate"] > 0, st   # skipped: same-level single-block replays, levels 7-9 twins
         assert sha(out) == sha(ref)
         assert c.reconstruct(out) == data
+
+
+CLI_CASES = [
+    ("c1", []),                                        # precompress + the default verify
+    ("c4s", ["--notest", "--chunksize", "65536"]),
+    ("c5s", ["--notest", "--brute-window", "-o", "out.atz"]),
+    ("c4s", ["--recomp-tresh", "16", "--shortcut-len", "256", "--mismatch-tol", "0"]),
+    ("missing", []),                                   # error path: input file not found
+]
+
+
+@pytest.mark.skipif(not os.path.exists(_libs.REF_UNCOMP), reason="reference build (oracle/_ref) not present")
+@pytest.mark.parametrize("inp,args", CLI_CASES, ids=lambda v: v if isinstance(v, str) else "_".join(v) or "default")
+def test_cli_matches_reference(atz, tmp_path, inp, args):
+    """The uncomp CLI (antiz_amd/csrc/uncomp.cpp) against the reference's own CLI
+    (oracle/_ref/uncomp, main.cpp:1066-1231) on the same input in twin directories: the same stdout,
+    exit code and output files (.atz, the .rec it leaves or deletes), then -r of the .atz."""
+    import subprocess
+    from antiz_amd import datagen, build
+    mine = os.path.join(os.path.dirname(build.LIB), "uncomp")
+    data = {"c1": lambda: datagen.gen_c1(), "c4s": lambda: datagen.gen_c4(seed=11, n_streams=150, workers=1),
+            "c5s": lambda: datagen.gen_c5(seed=12, n_streams=120, workers=1), "missing": lambda: None}[inp]()
+    runs = {}
+    for who, exe in (("ref", _libs.REF_UNCOMP), ("mine", mine)):
+        d = tmp_path / who
+        d.mkdir()
+        if data is not None:
+            (d / "in.bin").write_bytes(data)
+        r = subprocess.run([exe, "-i", "in.bin"] + args, cwd=d, capture_output=True, text=True, timeout=300)
+        files = {f: (d / f).read_bytes() for f in sorted(os.listdir(d))}
+        runs[who] = (r.returncode, r.stdout, files)
+        if data is not None:
+            atzname = "out.atz" if "-o" in args else "in.bin.atz"
+            r2 = subprocess.run([exe, "-i", atzname, "-r"], cwd=d, capture_output=True, text=True, timeout=300)
+            runs[who + "-r"] = (r2.returncode, r2.stdout, {f: (d / f).read_bytes() for f in sorted(os.listdir(d))})
+    for k in ("", "-r"):
+        if "ref" + k not in runs:
+            continue
+        rc_ref, out_ref, f_ref = runs["ref" + k]
+        rc_me, out_me, f_me = runs["mine" + k]
+        assert (rc_me, out_me) == (rc_ref, out_ref), (k, out_me, out_ref)
+        assert sorted(f_me) == sorted(f_ref), k
+        assert all(f_me[f] == f_ref[f] for f in f_ref), k
