@@ -136,6 +136,9 @@ def main():
     ap.add_argument("--workload", choices=("c4", "c5"), default="c4",
                     help="c4: the metric's workload (BASELINE configs[3]); c5: configs[4], the same generator with "
                          "windowBits U10-15 and --brute-window (a measurement beside the metric, not its value)")
+    ap.add_argument("--files-per-gpu", type=int, default=1,
+                    help="independent files in flight per GPU (one context and host thread each; shards mode). "
+                         "1 = the metric's workload; 2 measures the multi-file throughput mode (DESIGN s3.6)")
     ap.add_argument("--mode", choices=("shards", "file"), default="shards",
                     help="shards: every rank precompresses its own 1 GB file (weak scaling, no data-path "
                          "collective); file: ONE 1 GB file split over the ranks (antiz_amd.shard: all-gather "
@@ -164,6 +167,7 @@ def main():
 
     base = 4 if args.workload == "c4" else 5
     seed = base + rank if args.mode == "shards" else base
+    nf = max(1, args.files_per_gpu) if args.mode == "shards" else 1
     t0 = time.time()
     path = datagen.cached(args.workload, args.cache, seed=seed, n_streams=args.streams)
     with open(path, "rb") as f:
@@ -176,8 +180,38 @@ def main():
 
     ctx = antiz_amd.Context(device=local, brute_window=args.workload == "c5")
     group = None
+    # --files-per-gpu k > 1: k - 1 more independent files (seeds after every rank's), each with its own
+    # context, precompressed by their own host threads beside the first (ctypes drops the GIL)
+    extra = []
+    for k in range(1, nf):
+        p2 = datagen.cached(args.workload, args.cache, seed=base + world * k + rank, n_streams=args.streams)
+        with open(p2, "rb") as f:
+            d2 = f.read()
+        h2 = torch.frombuffer(bytearray(d2) + bytearray(4096), dtype=torch.uint8)
+        extra.append((antiz_amd.Context(device=local, brute_window=args.workload == "c5"), d2, h2.to("cuda")))
+    torch.cuda.synchronize()
+
+    def step_extra():
+        import threading
+        res = [None] * len(extra)
+        def run(i):
+            c2, d2, dv2 = extra[i]
+            res[i] = c2.precompress_device(dv2.data_ptr(), d2)
+        th = [threading.Thread(target=run, args=(i,)) for i in range(len(extra))]
+        for t in th:
+            t.start()
+        return th, res
 
     def step():
+        if extra:
+            th, _ = step_extra()
+            dptr, n, st = ctx.precompress_device(dev.data_ptr(), data)
+            for t in th:
+                t.join()
+            return n, st
+        return step1()
+
+    def step1():
         if args.mode == "file":
             from antiz_amd import shard
             if world == 1:
@@ -202,8 +236,8 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt, value, atz_sizes = aggregate(dt, n, len(data) if args.mode == "shards" else len(data) / world,
-                                     args.steps, world, red_dev)
+    shard_bytes = len(data) + sum(len(e[1]) for e in extra) if args.mode == "shards" else len(data) / world
+    dt, value, atz_sizes = aggregate(dt, n, shard_bytes, args.steps, world, red_dev)
     ms_per_step = dt * 1000.0 / args.steps
 
     last = stats[-1]
@@ -269,8 +303,8 @@ def main():
                                     if args.workload == "c4" else
                                     "C5: %d zlib streams (clevel U1-9, memLevel U1-9, windowBits U10-15), %.3f GB "
                                     "per GPU, --brute-window, default thresholds" % (args.streams, len(data) / 1e9),
-                        "streams_per_gpu": args.streams, "bytes_per_gpu": len(data),
-                        "parallelism": "stream-sharded dp%d" % world}
+                        "streams_per_gpu": args.streams * nf, "bytes_per_gpu": len(data) + sum(len(e[1]) for e in extra),
+                        "files_per_gpu": nf, "parallelism": "stream-sharded dp%d" % world}
                        if args.mode == "shards" else
                        {"workload": "C4: one file of %d zlib streams (clevel U1-9, memLevel U1-9, w15), %.3f GB, "
                                     "split over %d GPUs, default thresholds" % (args.streams, len(data) / 1e9, world),
@@ -283,6 +317,8 @@ def main():
         }
         print(json.dumps(out), flush=True)
     ctx.close()
+    for e in extra:
+        e[0].close()
     if world > 1:
         dist.destroy_process_group()
 
