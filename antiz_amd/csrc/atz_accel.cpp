@@ -28,6 +28,7 @@
 #include <memory>
 #include <new>
 #include <stdexcept>
+#include <atomic>
 #include <thread>
 #include <condition_variable>
 #include <mutex>
@@ -474,6 +475,7 @@ struct atz_ctx {
   std::vector<std::unique_ptr<Pipe>> pipes;
   std::vector<std::unique_ptr<DBuf>> slabs;   // inflated records, one allocation per scan piece
   size_t pipes_running = 1;
+  std::atomic<bool> sweep_abort{false};   // the pipes stop at their next round (a withdrawn speculative scan)
   // multi-GPU precompress of one file (atz_shard_*): this rank's state between the calls
   struct Shard {
     std::shared_ptr<struct ScanState> S;
@@ -805,7 +807,7 @@ static long scan_select(const ScanState& S, uint32_t j, uint64_t i0, std::vector
 
 // Chunks [ja, jb): candidate inflates (their outputs kept in the arena, which is reset: earlier
 // pieces' records were gathered out of it already) and speculative first continuations.
-static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, ScanState& S, uint32_t ja, uint32_t jb) {
+static int scan_candidates(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, ScanState& S, uint32_t ja, uint32_t jb) {
   auto tm_ = std::chrono::steady_clock::now();
   const std::vector<Chunk>& chunks = S.chunks;
   const size_t k0 = S.cbeg[ja], k1 = S.cbeg[jb];
@@ -844,6 +846,25 @@ static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, Sca
     for (size_t q = 0; q < vk.size(); q++) S.cres[vk[q]] = vr[q];
   }
   TMARK("scan: candidate inflate");
+  return 0;
+}
+
+// the pending candidate of each chunk of [ja, jb) for a selection from i = 0 (S.pend0); returns the
+// chunks that have one (their first continuation is needed)
+static std::vector<uint32_t> scan_pending(ScanState& S, uint32_t ja, uint32_t jb) {
+  std::vector<uint32_t> todo;
+  for (uint32_t j = ja; j < jb && j + 1 < S.chunks.size(); j++) {
+    const long k = scan_select(S, j, 0, nullptr);
+    S.pend0[j] = k;
+    if (k >= 0) todo.push_back(j);
+  }
+  return todo;
+}
+
+static int scan_continuations(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, ScanState& S, uint32_t ja, uint32_t jb) {
+  (void)h;
+  auto tm_ = std::chrono::steady_clock::now();
+  const std::vector<Chunk>& chunks = S.chunks;
   {
     // speculative first continuations: pending candidate of chunk j (selection from 0) + buffer
     // j+1, assembled in HBM by k_gather from file ranges and the chunks' buffer[0] bytes.  The first
@@ -852,12 +873,7 @@ static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, Sca
     // (k_inflate consumes exactly zlib's bits); one that runs out of input is decoded again with
     // the whole buffer.  (The duplicated byte almost always ends them within a few symbols.)
     static constexpr uint64_t CONT_PROBE = 65536;
-    std::vector<uint32_t> todo;
-    for (uint32_t j = ja; j < jb && j + 1 < chunks.size(); j++) {
-      const long k = scan_select(S, j, 0, nullptr);
-      S.pend0[j] = k;
-      if (k >= 0) todo.push_back(j);
-    }
+    std::vector<uint32_t> todo = scan_pending(S, ja, jb);
     c->stats.n_continuations += todo.size();
     TMARK("scan: cont select");
     for (int pass = 0; pass < 2 && !todo.empty(); pass++) {
@@ -923,9 +939,16 @@ static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, Sca
   return 0;
 }
 
+static int scan_inflate(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, ScanState& S, uint32_t ja, uint32_t jb) {
+  if (int r = scan_candidates(c, h, d_file, S, ja, jb)) return r;
+  return scan_continuations(c, h, d_file, S, ja, jb);
+}
+
 // The sequential replay of chunks [ja, jb) (main.cpp:205-246 over searchInfile's chunk sequence),
 // appending to c->recs; needs the candidate results and first continuations of those chunks.
-static int scan_replay(atz_ctx* c, const uint8_t* h, ScanState& S, uint32_t ja, uint32_t jb) {
+static int scan_replay(atz_ctx* c, const uint8_t* h, ScanState& S, uint32_t ja, uint32_t jb,
+                       std::vector<Rec>* recs_out = nullptr) {
+  std::vector<Rec>& recs = recs_out ? *recs_out : c->recs;
   auto tm_ = std::chrono::steady_clock::now();
   const std::vector<Chunk>& chunks = S.chunks;
   ScanPend& pd = S.pd;
@@ -937,7 +960,7 @@ static int scan_replay(atz_ctx* c, const uint8_t* h, ScanState& S, uint32_t ja, 
     for (uint32_t k = 1; k <= q.napp; k++) chunk_bytes(h, chunks[q.j0 + k], v);
   };
   // c->recs never reallocates while the sweep reads it (capacity = S.max_records())
-  auto room = [&]() { return c->recs.capacity() - c->recs.size() >= (S.cbeg[jb] - S.cbeg[ja]) + (jb - ja); };
+  auto room = [&]() { return recs.capacity() - recs.size() >= (S.cbeg[jb] - S.cbeg[ja]) + (jb - ja); };
   if (!room()) return ATZ_E_INTERNAL;
   for (uint32_t j = ja; j < jb; j++) {
     const Chunk& ch = chunks[j];
@@ -967,13 +990,13 @@ static int scan_replay(atz_ctx* c, const uint8_t* h, ScanState& S, uint32_t ja, 
         avail = ch.len; st = INF_ERROR;
       }
       if (st == INF_END) {
-        c->recs.push_back({pd.off, pd.in, pd.out, pd.type, 1});
+        recs.push_back({pd.off, pd.in, pd.out, pd.type, 1});
         i = ch.len - avail;
       }
       S.need_more = avail == 0;
     }
     if (!S.need_more) {
-      const long k = scan_select(S, j, i, &c->recs);
+      const long k = scan_select(S, j, i, &recs);
       if (k >= 0) {
         const ScanCand& cd = S.cands[k];
         S.need_more = true;
@@ -1818,6 +1841,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
   static size_t chunk = ~(size_t)0;   // ATZ_CHUNK=n: at most n streams per round (the rest wait their turn)
   if (chunk == ~(size_t)0) { const char* e = std::getenv("ATZ_CHUNK"); chunk = e ? (size_t)std::atoll(e) : 0; }
   while (take_inbox()) {
+    if (x->sweep_abort.load(std::memory_order_relaxed)) break;
     rounds++;
     std::vector<uint32_t> waiting;
     if (chunk && active.size() > chunk) {
@@ -2446,6 +2470,15 @@ static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::
 
 // ATZ_PIECES=k: the scan runs in k chunk ranges, each handed to the sweep as soon as its records
 // are inflated, so the sweep of the first pieces overlaps the scan of the rest (1: scan, then sweep)
+static bool spec_cont_on() {   // ATZ_SPEC_CONT=0: the scan waits for the first continuations
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_SPEC_CONT"); v = e ? std::atoi(e) : 1; }
+  return v != 0;
+}
+static bool spec_abort_test() {   // ATZ_SPEC_ABORT_TEST=1 (read per call): withdraw the speculative sweep
+  const char* e = std::getenv("ATZ_SPEC_ABORT_TEST");
+  return e && *e == '1';
+}
 static uint32_t scan_pieces() {
   static int v = -1;
   if (v < 0) { const char* e = std::getenv("ATZ_PIECES"); v = e ? std::max(1, std::atoi(e)) : 1; }
@@ -2484,7 +2517,56 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
   });
   struct Join { std::thread& t; ~Join() { if (t.joinable()) t.join(); } } join_begin{t_begin};
   double scan_busy = ms_since(t0);
-  for (uint32_t p = 0; p < P; p++) {
+  if (P == 1 && spec_cont_on()) {
+    // The first continuations of pending streams (each a decode of the stream from its header through
+    // the chunk boundary) are latency-bound: one small launch, 15-30 ms.  The records do not wait for
+    // it: they are replayed as if every continuation fails -- the refill repeats the chunk's last
+    // byte, which almost always ends a pending stream with a data error (main.cpp:207-216) -- and
+    // handed to the sweep; then the real continuations run beside the sweep's first rounds and the
+    // replay is repeated with them.  Identical records confirm the speculation; otherwise the sweep
+    // is withdrawn and restarted on the real records (ATZ_SPEC_ABORT_TEST=1 forces that path).
+    auto tm_ = std::chrono::steady_clock::now();
+    if (int r = scan_candidates(c, h, d_file, S, 0, nch)) return r;
+    for (uint32_t j : scan_pending(S, 0, nch)) {
+      InfRes e{};
+      e.status = INF_ERROR;
+      S.cont0[j] = e;
+    }
+    if (int r = scan_replay(c, h, S, 0, nch)) return r;
+    t_begin.join();
+    if (rc_begin) return rc_begin;
+    const size_t r1 = c->recs.size();
+    if (int r = inflate_records(c, d_file, F, 0, r1, *c->slabs[0])) return r;
+    if (int r = sweep_publish(c, R, 0, r1)) return r;
+    TMARK("scan: speculative records out");
+    if (int r = scan_continuations(c, h, d_file, S, 0, nch)) return r;
+    S.need_more = false;
+    S.pd = ScanPend{};
+    std::vector<Rec> check;
+    check.reserve(n_max);
+    if (int r = scan_replay(c, h, S, 0, nch, &check)) return r;
+    bool same = check.size() == r1;
+    for (size_t i = 0; same && i < r1; i++) {
+      const Rec &a = check[i], &b = c->recs[i];
+      same = a.offset == b.offset && a.comp_len == b.comp_len && a.infl_len == b.infl_len && a.type == b.type &&
+             a.flags == b.flags && a.arena_off == b.arena_off;
+    }
+    if (spec_abort_test()) same = false;
+    if (!same) {
+      c->sweep_abort.store(true);
+      sweep_close(c, R);
+      c->sweep_abort.store(false);
+      c->recs.assign(check.begin(), check.end());   // capacity n_max: no reallocation
+      if (int r = sweep_begin(c, d_file, ss, n_max, R)) return r;
+      const size_t r2 = c->recs.size();
+      if (int r = inflate_records(c, d_file, F, 0, r2, *c->slabs[0])) return r;
+      if (int r = sweep_publish(c, R, 0, r2)) return r;
+      if (timing_on()) std::fprintf(stderr, "atz: speculative scan withdrawn (%zu vs %zu records)\n", r1, r2);
+    }
+    TMARK("scan: continuations checked");
+    scan_busy += ms_since(t0) - scan_busy;
+  }
+  for (uint32_t p = 0; p < P && !(P == 1 && spec_cont_on()); p++) {
     auto tp = std::chrono::steady_clock::now();
     const uint32_t ja = (uint32_t)((uint64_t)nch * p / P), jb = (uint32_t)((uint64_t)nch * (p + 1) / P);
     const size_t r0 = c->recs.size();

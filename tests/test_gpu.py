@@ -547,3 +547,24 @@ def test_cli_matches_reference(atz, tmp_path, inp, args):
         assert (rc_me, out_me) == (rc_ref, out_ref), (k, out_me, out_ref)
         assert sorted(f_me) == sorted(f_ref), k
         assert all(f_me[f] == f_ref[f] for f in f_ref), k
+
+
+def test_speculative_scan_withdrawal(atz, monkeypatch):
+    """The scan hands its records to the sweep before the first continuations are decoded, assuming
+    each fails; the real ones then re-run the replay, and a different record list withdraws the sweep
+    and restarts it.  ATZ_SPEC_ABORT_TEST=1 takes that path on every call: the ATZ1 bytes must still
+    be the oracle's (golden chunk-boundary cases, and a 400-stream C4 slice over 3 pipes)."""
+    from antiz_amd import datagen
+    monkeypatch.setenv("ATZ_SPEC_ABORT_TEST", "1")
+    cases = {c["name"]: c for c in G.cases()}
+    for name in ("chunk_default", "chunk_4096", "chunk_777", "eof_multiple"):
+        case = cases[name]
+        with atz.Context(chunksize=case["opts"].get("chunksize", 524288)) as c:
+            out, _ = c.precompress(G.case_input(case))
+            assert sha(out) == case["atz_sha256"], name
+    data = datagen.gen_c4(seed=21, n_streams=400, workers=2)
+    rc, ref, _ = _libs.ora_precompress(data, chunksize=65536)
+    assert rc == 0
+    with atz.Context(chunksize=65536) as c:
+        out, st = c.precompress(data)
+        assert sha(out) == sha(ref) and st["n_continuations"] > 0
