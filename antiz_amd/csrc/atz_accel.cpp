@@ -476,6 +476,10 @@ struct atz_ctx {
   std::vector<std::unique_ptr<DBuf>> slabs;   // inflated records, one allocation per scan piece
   size_t pipes_running = 1;
   std::atomic<bool> sweep_abort{false};   // the pipes stop at their next round (a withdrawn speculative scan)
+  // precompress_dev's large per-call state, kept so its capacity survives the calls
+  std::shared_ptr<struct ScanState> scan_keep;
+  std::vector<StreamState> ss_keep;
+  std::vector<StreamDev> sd_keep;
   // multi-GPU precompress of one file (atz_shard_*): this rank's state between the calls
   struct Shard {
     std::shared_ptr<struct ScanState> S;
@@ -692,6 +696,13 @@ struct ScanState {
   bool need_more = false;
   ScanPend pd{};
   uint64_t arena_cap = 0;
+  // per-call scratch, kept with the context's ScanState so its capacity survives the calls (multi-MB
+  // buffers would otherwise be mapped, faulted in and unmapped on every precompress)
+  std::vector<uint64_t> pairs;
+  std::vector<InfJob> fjobs;
+  std::vector<size_t> fk;
+  std::vector<InfRes> fr;
+  std::vector<Rec> check;
   uint64_t max_records() const { return cands.size() + chunks.size() + 1; }
 };
 
@@ -721,7 +732,8 @@ static int scan_plan(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
   }
   // ---- all header pairs of the file, in file order (GPU: count pass, host prefix, write pass),
   // packed position << 5 | header type ----
-  std::vector<uint64_t> pairs;
+  std::vector<uint64_t>& pairs = S.pairs;
+  pairs.clear();
   {
     const uint64_t nb = std::max<uint64_t>(1, std::min<uint64_t>(8192, (F + 65535) / 65536));
     const uint64_t seg = ((F + nb - 1) / nb + 4095) & ~4095ull;
@@ -814,8 +826,12 @@ static int scan_candidates(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, 
   {
     // file-backed jobs (output kept in an arena slot), and materialized buffers for chunk starts
     // whose buffer[0] is not the file byte
-    std::vector<InfJob> fjobs, vjobs;
-    std::vector<size_t> fk, vk;
+    std::vector<InfJob>& fjobs = S.fjobs;
+    std::vector<size_t>& fk = S.fk;
+    fjobs.clear();
+    fk.clear();
+    std::vector<InfJob> vjobs;
+    std::vector<size_t> vk;
     std::vector<uint8_t> virt;
     fjobs.reserve(k1 - k0);
     fk.reserve(k1 - k0);
@@ -836,7 +852,8 @@ static int scan_candidates(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, 
         fk.push_back(k);
       }
     }
-    std::vector<InfRes> fr, vr;
+    std::vector<InfRes>& fr = S.fr;
+    std::vector<InfRes> vr;
     if (int r = run_inflate_jobs(c, d_file, nullptr, fjobs, fr, S.arena_cap)) return r;
     if (!vjobs.empty()) {
       if (int r = upload(c, c->d_virt, virt.data(), virt.size())) return r;
@@ -2494,12 +2511,15 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
   struct Drop { atz_ctx* c; ~Drop() { c->hfile = nullptr; } } drop{c};   // h is the caller's, valid for this call only
   c->stats.file_bytes = F;
   c->recs.clear();
-  ScanState S;
+  if (!c->scan_keep) c->scan_keep = std::make_shared<ScanState>();
+  ScanState& S = *c->scan_keep;
   if (int r = scan_plan(c, h, d_file, F, S)) return r;
   const size_t n_max = S.max_records();
   c->recs.reserve(n_max);
-  std::vector<StreamState> ss;
+  std::vector<StreamState>& ss = c->ss_keep;
   SweepRun R;
+  R.sd.swap(c->sd_keep);
+  struct KeepSd { SweepRun& R; atz_ctx* c; ~KeepSd() { R.sd.swap(c->sd_keep); } } keep_sd{R, c};
   SweepGuard guard{c, R};
   const uint32_t nch = (uint32_t)S.chunks.size();
   const uint32_t P = std::max<uint32_t>(1, std::min(scan_pieces(), nch));
@@ -2542,7 +2562,8 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
     if (int r = scan_continuations(c, h, d_file, S, 0, nch)) return r;
     S.need_more = false;
     S.pd = ScanPend{};
-    std::vector<Rec> check;
+    std::vector<Rec>& check = S.check;
+    check.clear();
     check.reserve(n_max);
     if (int r = scan_replay(c, h, S, 0, nch, &check)) return r;
     bool same = check.size() == r1;
@@ -3206,7 +3227,10 @@ int atz_precompress_device(atz_ctx_t* c, const uint8_t* d_file, const uint8_t* h
     (void)hipGetLastError();
     if (!c || !d_file || !h_file || !d_atz || !atz_len) return ATZ_E_ARG;
     uint64_t al = 0;
+    auto tc = std::chrono::steady_clock::now();
     if (int r = precompress_dev(c, d_file, h_file, len, &al, nullptr)) return r;
+    if (timing_on())
+      std::fprintf(stderr, "atz: precompress call %.2f ms (inside: %.2f ms)\n", ms_since(tc), c->stats.total_ms);
     *d_atz = c->d_atz.as<uint8_t>();
     *atz_len = al;
     if (stats) *stats = c->stats;
