@@ -6,16 +6,20 @@ clevel U{1..9} x memLevel U{1..9}, w15, ~10 KB compressed each, 0-64 B random ga
 A step = one full precompress (Phase 1 scan+inflate, Phase 3 parameter sweep, Phase 4 ATZ1 assembly)
 of that file, input already resident in HBM, ATZ1 output assembled in HBM.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the path shards by
-stream/file with no data-path exchange, so every rank precompresses its own 1 GB shard (seed 4 + rank;
-rank 0's shard is the single-GPU workload) -- weak scaling; the only collectives are the barrier and
-the max-over-ranks of the step time (plus an all_gather of per-rank ATZ sizes: the shard index).
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): by default ONE 1 GB
+file (config 4: "1 GB synthetic, 100k streams, stream-sharded across 8 x MI355X") is split over the
+ranks (--mode file, antiz_amd.shard): an all-gather of the scan results, a cost-balanced split of the
+streams, and a gather of the ATZ1 pieces to rank 0 over RCCL -- strong scaling.  --mode shards (every
+rank its own 1 GB file, seed 4 + rank: weak scaling) is a labelled secondary line.
 
 roofline: the dominant kernel (k_trial_*: deflate trials) -- achieved = algorithmic bytes
 (trial input read + compare read, summed over the launches) / the kernels' summed
-device time (HIP events recorded inside libatz_accel on its own stream), peak = MI355X HBM 8 TB/s.
+device time (HIP events recorded inside libatz_accel on its own stream), peak = MI355X HBM 8 TB/s;
+achieved_wall divides the same bytes by the step's wall time (the pipes' launches overlap).
 cpu_baseline: the REAL reference (oracle/_ref/uncomp, built from /root/reference) on a bounded
-sample of the same workload (first seed, fewer streams), 1 core, --notest.
+sample of the same workload (first seed, fewer streams), 1 core, --notest; the host CPU is named.
+host_to_host: atz_precompress from a host buffer to host ATZ1 bytes (H2D + D2H included), the path
+the uncomp CLI takes; reported beside the metric, never as its value.
 """
 import argparse
 import hashlib
@@ -34,6 +38,20 @@ HBM_PEAK_GBS = 8000.0
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_model():
+    """The host CPU the baseline runs on (/proc/cpuinfo), and the cores this process may use."""
+    name = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return name, len(os.sched_getaffinity(0))
 
 
 def cpu_baseline(n_streams, seed, ctx, workload="c4"):
@@ -72,7 +90,9 @@ def cpu_baseline(n_streams, seed, ctx, workload="c4"):
     same = hashlib.sha256(atz).hexdigest() == ref_sha
     if not same:
         log("PARITY FAILURE: the library's .atz of the cpu_baseline sample differs from the reference's")
+    model, visible = cpu_model()
     return {"value": round(len(data) / 1e6 / dt, 4), "unit": "MB/s", "cores": 1, "kind": "reference",
+            "cpu_model": model, "host_cpus_visible": visible,
             "atz_identical_to_reference": same, "atz_sha256": ref_sha[:16],
             "sample": "%d-stream prefix config of the same generator (%.1f MB, seed %d), oracle/_ref/uncomp --notest, "
                       "%.1f s wall" % (n_streams, len(data) / 1e6, seed, dt)
@@ -92,17 +112,18 @@ def pmc_traffic():
     """HBM traffic per k_trial launch from the newest committed PMC summary (profiles/r*_pmc_traffic.json:
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench, FETCH_SIZE doubled per the
     MI355X guide's gfx950 correction). rocprofv3 cannot run inside the timed process, so the counter
-    passes are their own runs of the same command; the file named here is the one used."""
+    passes are their own runs of the same command; the file named here is the one used, and its
+    "code_sha" (the commit the passes ran, when recorded) shows which code it measured."""
     import glob
     import re
     files = glob.glob(os.path.join(ROOT, "profiles", "r*_v*_pmc_traffic.json"))
     if not files:
-        return None, None
+        return None, None, None
     key = lambda p: tuple(int(x) for x in re.findall(r"r(\d+)_v(\d+)_", os.path.basename(p))[0])
     path = max(files, key=key)
     with open(path) as f:
         d = json.load(f)
-    return d["k_trial"]["traffic_per_launch"], os.path.relpath(path, ROOT)
+    return d["k_trial"]["traffic_per_launch"], os.path.relpath(path, ROOT), d.get("code_sha")
 
 
 def aggregate(dt, atz_len, shard_bytes, steps, world, device):
@@ -132,6 +153,7 @@ def main():
     ap.add_argument("--cpu-sample-streams", type=int, default=8000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-recon", action="store_true", help="skip the reconstruct (-r / verify) measurement")
+    ap.add_argument("--no-h2h", action="store_true", help="skip the host-to-host (atz_precompress) measurement")
     ap.add_argument("--cache", default=os.environ.get("ATZ_BENCH_CACHE", "/tmp/atz_bench_cache"))
     ap.add_argument("--workload", choices=("c4", "c5"), default="c4",
                     help="c4: the metric's workload (BASELINE configs[3]); c5: configs[4], the same generator with "
@@ -139,11 +161,14 @@ def main():
     ap.add_argument("--files-per-gpu", type=int, default=1,
                     help="independent files in flight per GPU (one context and host thread each; shards mode). "
                          "1 = the metric's workload; 2 measures the multi-file throughput mode (DESIGN s3.6)")
-    ap.add_argument("--mode", choices=("shards", "file"), default="shards",
-                    help="shards: every rank precompresses its own 1 GB file (weak scaling, no data-path "
-                         "collective); file: ONE 1 GB file split over the ranks (antiz_amd.shard: all-gather "
-                         "of scan results, RCCL gather of the ATZ1 pieces to rank 0; strong scaling)")
+    ap.add_argument("--mode", choices=("file", "shards"), default="file",
+                    help="file (default, the metric's config 4): ONE 1 GB file split over the ranks (antiz_amd.shard: "
+                         "all-gather of scan results, cost-balanced stream split, RCCL gather of the ATZ1 pieces to "
+                         "rank 0; strong scaling); shards: every rank precompresses its own 1 GB file (weak scaling, "
+                         "no data-path collective; a secondary line)")
     args = ap.parse_args()
+    if args.mode == "file" and args.files_per_gpu > 1:
+        ap.error("--files-per-gpu > 1 needs --mode shards (one file per step is split in file mode)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -245,10 +270,15 @@ def main():
     alg = last["k_trial_alg_bytes"]
     achieved = alg / ktime / 1e9 if ktime > 0 else 0.0
     launches = max(1, last["k_trial_launches"])
-    traffic, traffic_src = pmc_traffic()
+    traffic, traffic_src, traffic_sha = pmc_traffic()
+    achieved_wall = alg / (ms_per_step / 1000.0) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+            "achieved_wall": round(achieved_wall, 3), "frac_wall": round(achieved_wall / HBM_PEAK_GBS, 6),
+            "limiter": "not HBM: per-trial serial parse on the scalar + vector issue pipes and dependent LDS "
+                       "latency (DESIGN.md s3.5); the HBM fraction is reported because it is the graded roofline",
             "traffic_unit": "bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE)", "traffic_source": traffic_src,
+            "traffic_code_sha": traffic_sha,
             "kernel": "k_trial_{stored,fast,slow}", "launches": last["k_trial_launches"],
             "avg_launch_ms": round(last["k_trial_ms"] / launches, 4),
             "alg_bytes_per_launch": int(alg / launches)}
@@ -279,6 +309,24 @@ def main():
                  "identical": rl == len(data) and back.numpy().tobytes() == data}
         del hdev
 
+    # the product path as the CLI runs it: host buffer in, host ATZ1 bytes out (H2D + D2H included)
+    h2h = None
+    if world == 1 and not args.no_h2h:
+        import ctypes
+        L = antiz_amd.lib()
+        p, n, st = ctypes.POINTER(ctypes.c_uint8)(), ctypes.c_uint64(0), antiz_amd.Stats()
+        ts = []
+        for _ in range(2):   # the first call sizes the library's pinned staging
+            t1 = time.perf_counter()
+            rc = L.atz_precompress(ctx.h, data, len(data), ctypes.byref(p), ctypes.byref(n), ctypes.byref(st))
+            ts.append(time.perf_counter() - t1)
+            if rc != 0:
+                raise RuntimeError("atz_precompress failed: %d" % rc)
+            L.atz_free(p)
+        h2h = {"value": round(len(data) / 1e6 / ts[-1], 3), "unit": "MB/s", "ms": round(ts[-1] * 1000, 2),
+               "atz_bytes": n.value, "what": "atz_precompress: host file bytes -> host ATZ1 bytes (H2D of the input, "
+                                             "D2H of the ATZ1 included), the uncomp CLI's path; not the metric's value"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_sample_streams, seed, ctx, args.workload)
@@ -306,13 +354,19 @@ def main():
                         "streams_per_gpu": args.streams * nf, "bytes_per_gpu": len(data) + sum(len(e[1]) for e in extra),
                         "files_per_gpu": nf, "parallelism": "stream-sharded dp%d" % world}
                        if args.mode == "shards" else
-                       {"workload": "C4: one file of %d zlib streams (clevel U1-9, memLevel U1-9, w15), %.3f GB, "
-                                    "split over %d GPUs, default thresholds" % (args.streams, len(data) / 1e9, world),
-                        "file_bytes": len(data), "parallelism": "chunk-range sharded x%d + RCCL gather" % world}),
+                       {"workload": ("C4: one file of %d zlib streams (clevel U1-9, memLevel U1-9, w15)"
+                                     if args.workload == "c4" else
+                                     "C5: one file of %d zlib streams (clevel U1-9, memLevel U1-9, windowBits U10-15), "
+                                     "--brute-window") % args.streams
+                                    + ", %.3f GB, split over %d GPUs, default thresholds" % (len(data) / 1e9, world),
+                        "file_bytes": len(data),
+                        "parallelism": "one file: scan by chunk ranges, cost-balanced stream split x%d, RCCL gather"
+                                       % world}),
             "roofline": roof,
             "cpu_baseline": cpu,
             "atz_bytes_per_rank": atz_sizes,
             "reconstruct": recon,
+            "host_to_host": h2h,
             "detail": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in last.items()},
         }
         print(json.dumps(out), flush=True)

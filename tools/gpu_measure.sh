@@ -2,7 +2,10 @@
 # One GPU call: parity suite, default bench line (with CPU baseline), rocprofv3 kernel stats of one
 # step, and separate PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic.  Every GPU step has its
 # own time limit; the chain stops at the first failure.
-# usage: tools/gpu_measure.sh <tag> [stages...]   stages: test bench prof pmc (default: all)
+# usage: tools/gpu_measure.sh <tag> [stages...]
+#   stages: test bench prof pmc timing small (default: test bench prof pmc)
+#   timing: ATZ_TIMING=2 timeline of one C4 step; small: the same on a 12 500-stream file (one rank's
+#   share of C4 at 8 GPUs)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${1:-run}; shift
@@ -14,10 +17,16 @@ timeout -k 10 300 python3 -c "
 import sys; sys.path.insert(0,'.')
 from antiz_amd import datagen; print(datagen.cached('c4','/tmp/atz_bench_cache',seed=4,n_streams=100000))" > $O/gen.log 2>&1 || exit 1
 if has test; then
-  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/test.log 2>&1 || exit 2
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/test.log 2>&1 || exit 2
 fi
 if has bench; then
   timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || exit 3
+fi
+if has timing; then
+  ATZ_TIMING=2 timeout -k 10 200 python3 bench.py --steps 1 --warmup 1 --no-cpu --no-recon > $O/timing.json 2> $O/timing.err || exit 7
+fi
+if has small; then
+  ATZ_TIMING=2 timeout -k 10 200 python3 bench.py --streams 12500 --steps 2 --warmup 1 --no-cpu --no-recon > $O/small.json 2> $O/small.err || exit 8
 fi
 if has prof; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o p --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-recon > $O/prof.json 2> $O/prof.err || exit 4
