@@ -2094,153 +2094,169 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         }
         bad = !exact;
       }
-      const uint64_t badm = __ballot(bad);
-      const uint64_t Pc = badm ? P & ((1ull << __builtin_ctzll(badm)) - 1ull) : P;
-#if ATZ_STEP_SPLIT
-      t1 = STEP_CLOCK(); csec[1] += t1 - t0; t0 = t1;   // (diagnostics: node checks counted with steps)
-#endif
-      // ---- tally the committed nodes' symbols lane-parallel, in position order
-      {
-        const bool mine = (Pc >> lane) & 1ull;
-        const uint32_t o = (uint32_t)__popcll(Pc & lt);
-        const uint32_t T = (uint32_t)__popcll(Pc);
-        z.nsym += T;
-        uint32_t base = 0;
-        while (base < T) {
-          const uint32_t room = z.lbs - 1u - z.last_lit;
-          const uint32_t seg_end = T - base < room ? T : base + room;
-          if (mine && o >= base && o < seg_end) {
-            uint32_t v;
-            if (wt == 2) {
-              v = (D << 8) | (L - 3u);
-              __hip_atomic_fetch_add(&s.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              __hip_atomic_fetch_add(&s.dfreq2[(dist_code(D - 1u)) >> 1], 1u << (16 * ((dist_code(D - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-              v = ex & 0xffu;
-              __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // Bad nodes are resolved one at a time by an exact walk.  When the walk's length equals the
+      // table's (or both give a literal), the parse path is unchanged: the node keeps its place on
+      // the path (with the walk's distance) and the window goes on to its next bad node.  Only a
+      // different length ends the window there.
+      uint64_t badm = __ballot(bad);
+      uint64_t donem = 0;   // path nodes tallied so far
+      uint32_t Dx = D;      // this lane's match distance (an exact walk may replace the table's)
+      bool restart = false;
+      uint32_t qnext = qn;
+      for (;;) {
+        // ---- tally the committed nodes' symbols lane-parallel, in position order
+        const uint64_t Pc = (badm ? P & ((1ull << __builtin_ctzll(badm)) - 1ull) : P) & ~donem;
+        {
+          const bool mine = (Pc >> lane) & 1ull;
+          const uint32_t o = (uint32_t)__popcll(Pc & lt);
+          const uint32_t T = (uint32_t)__popcll(Pc);
+          z.nsym += T;
+          uint32_t base = 0;
+          while (base < T) {
+            const uint32_t room = z.lbs - 1u - z.last_lit;
+            const uint32_t seg_end = T - base < room ? T : base + room;
+            if (mine && o >= base && o < seg_end) {
+              uint32_t v;
+              if (wt == 2) {
+                v = (Dx << 8) | (L - 3u);
+                __hip_atomic_fetch_add(&s.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&s.dfreq2[(dist_code(Dx - 1u)) >> 1], 1u << (16 * ((dist_code(Dx - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              } else {
+                v = ex & 0xffu;
+                __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              }
+              syms[(saving ? sbase : 0u) + z.last_lit + (o - base)] = v;
             }
-            syms[(saving ? sbase : 0u) + z.last_lit + (o - base)] = v;
+            z.last_lit += seg_end - base;
+            if (z.last_lit == z.lbs - 1u) {   // flush after the node tallied last: strstart past its step
+              const uint64_t om = __ballot(mine && o == seg_end - 1u);
+              const int ol = (int)__builtin_ctzll(om);
+              const uint32_t fx = (uint32_t)__builtin_amdgcn_readlane((int)x, ol);
+              const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)L, ol);
+              z.p = fx + (fl ? fl : 1u);
+              z.S = S_iter(Sb, fx);
+              FLUSH(0);
+              state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+              if (state != ~0u) break;
+            }
+            base = seg_end;
           }
-          z.last_lit += seg_end - base;
-          if (z.last_lit == z.lbs - 1u) {   // flush after the node tallied last: strstart past its step
-            const uint64_t om = __ballot(mine && o == seg_end - 1u);
-            const int ol = (int)__builtin_ctzll(om);
-            const uint32_t fx = (uint32_t)__builtin_amdgcn_readlane((int)x, ol);
-            const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)L, ol);
-            z.p = fx + (fl ? fl : 1u);
-            z.S = S_iter(Sb, fx);
-            FLUSH(0);
-            state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
-            if (state != ~0u) break;
-          }
-          base = seg_end;
         }
+        donem |= Pc;
+        if (state != ~0u || !badm) break;
+        // ---- the first node that may differ: deflate_fast's longest_match over the INSERTED
+        // same-hash positions (Z/deflate.c:1148-1289): 64 bucket entries per step, lanes test
+        // insertion and compare bytes in parallel; the walk order is the lane order.
+        fallbacks++;
+        const uint64_t cf0 = STEP_CLOCK();
+        const int fln = __builtin_ctzll(badm);
+        const uint32_t f = wb + (uint32_t)fln;
+        const uint32_t Sf = S_iter(Sb, f);
+        const uint32_t la = n - f < LOOKMIN ? n - f : LOOKMIN;   // lookahead (>= 258 stands for more)
+        uint32_t ml = 0, ms = 0;
+        {
+          const uint32_t si = uni(sidx[f]);
+          bool done = (uni(bpos[si]) & BUCKET_FIRST) != 0;   // first of its bucket: no chain
+          bool head_done = false, hv = false, won = false;
+          uint32_t examined = 0, best = 2, win = 0;
+          const uint32_t limit = f > maxd ? f - maxd : 0u;   // later nodes only while > limit
+          const uint32_t cap = n - f < 258u ? n - f : 258u;
+          const uint32_t nicec = z.nice < la ? z.nice : la;   // <= cap
+          int32_t top = (int32_t)si - 1;
+          while (!done) {
+            const int32_t k = top - lane;
+            const uint32_t e = k >= 0 ? bpos[k] : BUCKET_FIRST;
+            const uint64_t fm = __ballot((e & BUCKET_FIRST) != 0);
+            const int flane = fm ? __ffsll((unsigned long long)fm) - 1 : 64;   // bucket's first entry: last node
+            const uint32_t qc = e & ~BUCKET_FIRST;
+            const bool insd = lane <= flane && k >= 0 && ins_get(qc);
+            const uint64_t im = __ballot(insd);
+            int head_lane = -1, from = 0;
+            if (!head_done) {
+              if (!im) {   // no inserted node in this chunk yet
+                if (flane < 64) break;
+                top -= 64;
+                continue;
+              }
+              head_lane = __ffsll((unsigned long long)im) - 1;
+              const uint32_t hh = (uint32_t)__builtin_amdgcn_readlane((int)qc, head_lane);
+              head_done = true;
+              hv = hh > Sf && f - hh <= maxd;   // zlib calls longest_match only then
+              if (!hv) break;
+              from = head_lane;
+            }
+            // the walk stops at the first inserted node <= limit (the head is always examined)
+            const uint64_t sm = __ballot(insd && lane >= from && lane != head_lane && qc <= limit);
+            const int slane = sm ? __ffsll((unsigned long long)sm) - 1 : 64;
+            bool cand = insd && lane >= from && lane < slane;
+            const uint32_t room = z.chain - examined;
+            cand = cand && (uint32_t)__popcll(__ballot(cand) & lt) < room;
+            const uint64_t cm = __ballot(cand);
+            examined += (uint32_t)__popcll(cm);
+            // match lengths capped at nice (16 bytes per round trip); the first candidate reaching
+            // nice ends the walk, so capped lengths decide the winner
+            uint32_t len = 0;
+            bool go = cand;
+            while (__ballot(go)) {
+              if (go) {
+                // 16 bytes per round trip: 5 aligned dword loads per side (stream bases are 256-byte aligned)
+                const uint32_t run = match16((const GLOBAL uint32_t*)in, qc + len, f + len, nullptr, 0);
+                const uint32_t left = nicec - len;
+                len += run < left ? run : left;
+                go = run == 16 && len < nicec;
+              }
+            }
+            const uint64_t nm = __ballot(cand && len >= nicec);
+            if (nm) {
+              const int wl = __ffsll((unsigned long long)nm) - 1;
+              win = (uint32_t)__builtin_amdgcn_readlane((int)qc, wl);
+              best = uni(common_len(in, win, f, nicec, cap, lane));   // full length of the winner
+              won = true;
+              break;
+            }
+            uint32_t mx = cand ? len : 0u;
+            for (int d = 32; d >= 1; d >>= 1) { const uint32_t o2 = __shfl_xor(mx, d, 64); mx = mx > o2 ? mx : o2; }
+            mx = uni(mx);
+            if (mx > best) {
+              const uint64_t xm = __ballot(cand && len == mx);
+              win = (uint32_t)__builtin_amdgcn_readlane((int)qc, __ffsll((unsigned long long)xm) - 1);
+              best = mx;
+              won = true;
+            }
+            done = examined >= z.chain || slane < 64 || flane < 64;
+            top -= 64;
+          }
+          if (hv && won) {
+            ml = best <= la ? best : la;
+            ms = win;
+          }
+        }
+        cyc_fb += STEP_CLOCK() - cf0;
+        const uint32_t twt = uni((uint32_t)__builtin_amdgcn_readlane((int)wt, fln));
+        const uint32_t tL = uni((uint32_t)__builtin_amdgcn_readlane((int)L, fln));
+        if (ml >= 3 ? (twt == 2 && tL == ml) : twt == 1) {   // same step: the path stands
+          if (ml >= 3 && lane == fln) Dx = f - ms;
+          badm &= badm - 1ull;
+          continue;
+        }
+        // the path changes at f: its exact step, then a new window after it
+        const uint32_t step = ml >= 3 ? ml : 1u;
+        span_set(f, f + step, [&](uint32_t p, uint32_t& y, uint32_t& Ly) { y = f; Ly = ml >= 3 ? ml : 0u; });
+        const bool full = tally1(ml >= 3 ? (((f - ms) << 8) | (ml - 3u)) : (uint32_t)in[f]);
+        if (full) {
+          z.p = f + step;
+          z.S = Sf;
+          FLUSH(0);
+          state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+        }
+        qnext = f + step;
+        restart = true;
+        break;
       }
       t1 = STEP_CLOCK(); csec[3] += t1 - t0;
       if (state != ~0u) break;
-      if (!badm) {
-        if (need) { state = TR_NEED_R; z.p = qn; break; }
-        q = qn;
-        continue;
-      }
-      // ---- the first node that may differ: deflate_fast's longest_match over the INSERTED
-      // same-hash positions (Z/deflate.c:1148-1289): 64 bucket entries per step, lanes test
-      // insertion and compare bytes in parallel; the walk order is the lane order.
-      fallbacks++;
-      const uint64_t cf0 = STEP_CLOCK();
-      const uint32_t f = wb + (uint32_t)__builtin_ctzll(badm);
-      const uint32_t Sf = S_iter(Sb, f);
-      const uint32_t la = n - f < LOOKMIN ? n - f : LOOKMIN;   // lookahead (>= 258 stands for more)
-      uint32_t ml = 0, ms = 0;
-      {
-        const uint32_t si = uni(sidx[f]);
-        bool done = (uni(bpos[si]) & BUCKET_FIRST) != 0;   // first of its bucket: no chain
-        bool head_done = false, hv = false, won = false;
-        uint32_t examined = 0, best = 2, win = 0;
-        const uint32_t limit = f > maxd ? f - maxd : 0u;   // later nodes only while > limit
-        const uint32_t cap = n - f < 258u ? n - f : 258u;
-        const uint32_t nicec = z.nice < la ? z.nice : la;   // <= cap
-        int32_t top = (int32_t)si - 1;
-        while (!done) {
-          const int32_t k = top - lane;
-          const uint32_t e = k >= 0 ? bpos[k] : BUCKET_FIRST;
-          const uint64_t fm = __ballot((e & BUCKET_FIRST) != 0);
-          const int flane = fm ? __ffsll((unsigned long long)fm) - 1 : 64;   // bucket's first entry: last node
-          const uint32_t qc = e & ~BUCKET_FIRST;
-          const bool insd = lane <= flane && k >= 0 && ins_get(qc);
-          const uint64_t im = __ballot(insd);
-          int head_lane = -1, from = 0;
-          if (!head_done) {
-            if (!im) {   // no inserted node in this chunk yet
-              if (flane < 64) break;
-              top -= 64;
-              continue;
-            }
-            head_lane = __ffsll((unsigned long long)im) - 1;
-            const uint32_t hh = (uint32_t)__builtin_amdgcn_readlane((int)qc, head_lane);
-            head_done = true;
-            hv = hh > Sf && f - hh <= maxd;   // zlib calls longest_match only then
-            if (!hv) break;
-            from = head_lane;
-          }
-          // the walk stops at the first inserted node <= limit (the head is always examined)
-          const uint64_t sm = __ballot(insd && lane >= from && lane != head_lane && qc <= limit);
-          const int slane = sm ? __ffsll((unsigned long long)sm) - 1 : 64;
-          bool cand = insd && lane >= from && lane < slane;
-          const uint32_t room = z.chain - examined;
-          cand = cand && (uint32_t)__popcll(__ballot(cand) & lt) < room;
-          const uint64_t cm = __ballot(cand);
-          examined += (uint32_t)__popcll(cm);
-          // match lengths capped at nice (16 bytes per round trip); the first candidate reaching
-          // nice ends the walk, so capped lengths decide the winner
-          uint32_t len = 0;
-          bool go = cand;
-          while (__ballot(go)) {
-            if (go) {
-              // 16 bytes per round trip: 5 aligned dword loads per side (stream bases are 256-byte aligned)
-              const uint32_t run = match16((const GLOBAL uint32_t*)in, qc + len, f + len, nullptr, 0);
-              const uint32_t left = nicec - len;
-              len += run < left ? run : left;
-              go = run == 16 && len < nicec;
-            }
-          }
-          const uint64_t nm = __ballot(cand && len >= nicec);
-          if (nm) {
-            const int wl = __ffsll((unsigned long long)nm) - 1;
-            win = (uint32_t)__builtin_amdgcn_readlane((int)qc, wl);
-            best = uni(common_len(in, win, f, nicec, cap, lane));   // full length of the winner
-            won = true;
-            break;
-          }
-          uint32_t mx = cand ? len : 0u;
-          for (int d = 32; d >= 1; d >>= 1) { const uint32_t o2 = __shfl_xor(mx, d, 64); mx = mx > o2 ? mx : o2; }
-          mx = uni(mx);
-          if (mx > best) {
-            const uint64_t xm = __ballot(cand && len == mx);
-            win = (uint32_t)__builtin_amdgcn_readlane((int)qc, __ffsll((unsigned long long)xm) - 1);
-            best = mx;
-            won = true;
-          }
-          done = examined >= z.chain || slane < 64 || flane < 64;
-          top -= 64;
-        }
-        if (hv && won) {
-          ml = best <= la ? best : la;
-          ms = win;
-        }
-      }
-      cyc_fb += STEP_CLOCK() - cf0;
-      const uint32_t step = ml >= 3 ? ml : 1u;
-      span_set(f, f + step, [&](uint32_t p, uint32_t& y, uint32_t& Ly) { y = f; Ly = ml >= 3 ? ml : 0u; });
-      const bool full = tally1(ml >= 3 ? (((f - ms) << 8) | (ml - 3u)) : (uint32_t)in[f]);
-      if (full) {
-        z.p = f + step;
-        z.S = Sf;
-        FLUSH(0);
-        state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
-        if (state != ~0u) break;
-      }
-      q = f + step;
+      if (!restart && need) { state = TR_NEED_R; z.p = qn; break; }
+      q = qnext;
     }
     if (state == ~0u) {
       z.p = n;
