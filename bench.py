@@ -236,15 +236,16 @@ def main():
             return n, st
         return step1()
 
+    last_out = [None]   # device pointer (int) or tensor holding the last step's ATZ1 on rank 0
+
     def step1():
-        if args.mode == "file":
+        if args.mode == "file" and world > 1:
             from antiz_amd import shard
-            if world == 1:
-                dptr, n, st = ctx.precompress_device(dev.data_ptr(), data)
-                return n, st
             out, n, st = shard.precompress_sharded(ctx, dev, data, group=group)
+            last_out[0] = out
             return n, st
         dptr, n, st = ctx.precompress_device(dev.data_ptr(), data)
+        last_out[0] = dptr
         return n, st
 
     for _ in range(args.warmup):
@@ -282,6 +283,24 @@ def main():
             "kernel": "k_trial_{stored,fast,slow}", "launches": last["k_trial_launches"],
             "avg_launch_ms": round(last["k_trial_ms"] / launches, 4),
             "alg_bytes_per_launch": int(alg / launches)}
+
+    # parity of the timed run's own output: the ATZ1 SHA-256 of the last step against the real reference's
+    # (tests/golden/full_configs.json: oracle/_ref/uncomp on the same generated file), full-size C4/C5 only
+    atz_check = None
+    if rank == 0 and args.streams == 100000 and last_out[0] is not None and (args.mode == "file" or not extra):
+        ref = json.load(open(os.path.join(ROOT, "tests", "golden", "full_configs.json"))).get(args.workload)
+        if ref and len(data) == ref["input_bytes"]:
+            h = torch.empty(n, dtype=torch.uint8)
+            if isinstance(last_out[0], int):
+                torch.cuda.synchronize()
+                hip_copy(h.data_ptr(), last_out[0], n)
+            else:
+                h.copy_(last_out[0][:n].cpu())
+            sha = hashlib.sha256(h.numpy().tobytes()).hexdigest()
+            atz_check = {"atz_sha256": sha[:16], "identical_to_reference": sha == ref["atz_sha256"],
+                         "reference": "oracle/_ref/uncomp on the same file (tests/golden/full_configs.json)"}
+            if sha != ref["atz_sha256"]:
+                log("PARITY FAILURE: the timed run's ATZ1 differs from the reference's")
 
     # reconstruct (-r, and precompress's default verify: main.cpp:869-950, 1173-1203) of the last ATZ1,
     # resident in HBM; not part of the metric: its own wall time, and the round trip checked
@@ -353,7 +372,7 @@ def main():
                                     "per GPU, --brute-window, default thresholds" % (args.streams, len(data) / 1e9),
                         "streams_per_gpu": args.streams * nf, "bytes_per_gpu": len(data) + sum(len(e[1]) for e in extra),
                         "files_per_gpu": nf, "parallelism": "stream-sharded dp%d" % world}
-                       if args.mode == "shards" else
+                       if args.mode == "shards" or world == 1 else
                        {"workload": ("C4: one file of %d zlib streams (clevel U1-9, memLevel U1-9, w15)"
                                      if args.workload == "c4" else
                                      "C5: one file of %d zlib streams (clevel U1-9, memLevel U1-9, windowBits U10-15), "
@@ -365,6 +384,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "atz_bytes_per_rank": atz_sizes,
+            "atz_parity": atz_check,
             "reconstruct": recon,
             "host_to_host": h2h,
             "detail": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in last.items()},

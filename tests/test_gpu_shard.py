@@ -90,3 +90,42 @@ def test_sharded_equals_single_gpu_and_oracle(sample, world, chunksize):
     assert hashlib.sha256(res[0][0]).hexdigest() == hashlib.sha256(one).hexdigest()
     assert sum(v[1] for v in res.values()) == st["n_streams"]     # the ranks' records partition the file's
     assert sum(v[2] for v in res.values()) == st["n_recomp"]
+
+
+def _cost_split(recs, world):
+    """The split atz_shard_sweep makes (atz_accel.cpp shard_records): contiguous record ranges of equal
+    estimated cost, (I_s + 1024) x mean trials of the header class."""
+    import bisect
+    t = [6, 15, 6, 20]
+    cum = [0]
+    for off, typ, cl, il, fl in recs:
+        cum.append(cum[-1] + (il + 1024) * t[typ & 3])
+    cuts = [0] + [bisect.bisect_left(cum, cum[-1] * q // world) for q in range(1, world)] + [len(recs)]
+    return [cuts[q + 1] - cuts[q] for q in range(world)]
+
+
+@pytest.fixture(scope="module")
+def clustered(tmp_path_factory):
+    """C4 streams followed by a cluster of C3's PNG-like Z_FILTERED streams (they match no trial, so
+    each runs its class's whole list): an equal split of the chunks would leave the ranks that hold the
+    cluster with most of the sweep; the cost-balanced split gives them fewer records."""
+    from antiz_amd import datagen
+    data = datagen.gen_c4(seed=43, n_streams=500) + datagen.gen_c3(seed=44, total=3_000_000)
+    path = str(tmp_path_factory.mktemp("shardc") / "mixed.bin")
+    with open(path, "wb") as f:
+        f.write(data)
+    rc, ref, _ = _libs.ora_precompress(data)
+    assert rc == 0
+    return path, data, ref
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sharded_cost_split_on_clustered_input(clustered, world):
+    import antiz_amd
+    path, data, ref = clustered
+    with antiz_amd.Context(device=0) as c:
+        recs = c.scan(data)
+    res = _run(world, path, 524288)
+    assert hashlib.sha256(res[0][0]).hexdigest() == hashlib.sha256(ref).hexdigest()
+    counts = [res[r][1] for r in range(world)]
+    assert counts == _cost_split(recs, world)
