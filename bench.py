@@ -194,7 +194,11 @@ def main():
     seed = base + rank if args.mode == "shards" else base
     nf = max(1, args.files_per_gpu) if args.mode == "shards" else 1
     t0 = time.time()
+    if args.mode == "file" and world > 1 and rank != 0:
+        dist.barrier()   # rank 0 generates the one shared file first (same seed, same cache path)
     path = datagen.cached(args.workload, args.cache, seed=seed, n_streams=args.streams)
+    if args.mode == "file" and world > 1 and rank == 0:
+        dist.barrier()
     with open(path, "rb") as f:
         data = f.read()
     log("rank %d: workload %s (%.1f MB) ready in %.1fs" % (rank, os.path.basename(path), len(data) / 1e6, time.time() - t0))
