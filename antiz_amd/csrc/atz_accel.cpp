@@ -410,13 +410,11 @@ struct Pipe {
   KTimer kt;
   atz_stats_t stats{};
   DBuf d_trials, d_tres, d_out, d_syms, d_R, d_mjobs, d_chains, d_diffjobs, d_diffpos, d_diffval, d_diffcnt, d_djobs;
-  ChainBufs cb[2];   // [0] builds on st, [1] prefetch builds on pst
-  // next-round bucket builds run ahead on their own stream while this round's trials run
+  ChainBufs cb;
+  // a second stream that stays idle: it only shifts how the process's GPU_MAX_HW_QUEUES (4) hardware
+  // queues are shared by the pipes' streams (two pipes then share a queue, which measured faster
+  // than every pipe on its own queue: DESIGN.md s3.6)
   hipStream_t pst = nullptr;
-  hipEvent_t pev = nullptr;
-  bool pev_pending = false;
-  hipEvent_t fev0 = nullptr, fev1 = nullptr;   // fast-level trials forked onto pst and joined back
-  KTimer pkt;
   uint64_t chain_used = 0, chain_cap = 0;
   std::vector<uint32_t> streams;   // the streams whose chain tables this pipe owns
   // symbol replay: saved sequences (bump arena, reset per sweep) and per-stream entries
@@ -437,11 +435,7 @@ struct Pipe {
   ~Pipe() {
     if (pst) { hipStreamSynchronize(pst); hipStreamDestroy(pst); }
     if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
-    if (pev) hipEventDestroy(pev);
-    if (fev0) hipEventDestroy(fev0);
-    if (fev1) hipEventDestroy(fev1);
     for (hipEvent_t e : kt.pool) hipEventDestroy(e);
-    for (hipEvent_t e : pkt.pool) hipEventDestroy(e);
   }
 };
 
@@ -1127,48 +1121,44 @@ static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F, size_t
 // sweep (8 bytes per position).  When a round would push the cache past its cap the cache is
 // dropped and the round's tables are rebuilt.
 static constexpr uint64_t CHAIN_CACHE_CAP = 48ull << 30;
-// ATZ_BUCKET_SORT=0: the older in-order bucket kernels for every job (A/B)
-static bool bucket_sort_on() {
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_BUCKET_SORT"); v = e ? std::atoi(e) : 1; }
-  return v != 0;
-}
 static bool bucket_verify() {   // ATZ_BUCKETS_VERIFY=1 (read per call): check k_buckets_sort against the others
   const char* e = std::getenv("ATZ_BUCKETS_VERIFY");
   return e && std::atoi(e) != 0;
 }
 static constexpr uint32_t BSORT_MAX_NPAD = std::min<uint32_t>(65472u, ((160u * 1024u - 256u - BSORT_CNT_BYTES) / BSORT_BYTES_PER_POS) & ~63u);   // LDS limit (256 B static)
 static_assert(bsort_lds_bytes(BSORT_MAX_NPAD) + 256u <= 160u * 1024u && BSORT_MAX_NPAD < 65536u, "k_buckets_sort LDS class");
-// prefetch builds finished: fold their kernel times into the pipe's counters
-static int chains_prefetch_collect(Pipe* c) {
-  if (!c->pev_pending) return 0;
-  HIPCHK(hipEventSynchronize(c->pev));
-  c->pev_pending = false;
-  std::swap(c->kt, c->pkt);
-  kcollect(c);
-  std::swap(c->kt, c->pkt);
-  return 0;
-}
-static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need, ChainBufs& B,
-                            bool prefetch);
-// Builds the missing tables of `need` on the pipe's stream (after any prefetch builds in flight).
+static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need, ChainBufs& B);
+// Builds the missing tables of `need` on the pipe's stream.
 static int ensure_chains(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need) {
-  if (c->pev_pending) HIPCHK(hipStreamWaitEvent(c->st, c->pev, 0));
-  return ensure_chains_on(x, c, need, c->cb[0], false);
+  return ensure_chains_on(x, c, need, c->cb);
 }
 // The deepest-bucket sizes (symbol replay's budget-free test) of pairs not known yet, without building
 // their tables (k_bucket_depth; streams < 64 Ki positions, larger ones are never budget-free): a pair
 // whose trials all turn out to be replays never needs its tables.  Runs on the pipe's stream.
-static int ensure_depths(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need) {
+// need_b[i]: the largest walk budget B of a trial on pair need[i] (budget-free: depth <= B).
+// memLevels with the same hash shift s = (memLevel + 9) / 3 -- {1, 2}, {3, 4, 5}, {6, 7, 8}, {9} --
+// hash a trigram to the same value (c0 << 2s) ^ (c1 << s) ^ c2 masked to memLevel + 7 bits, so a
+// smaller memLevel's buckets are unions of a larger one's and its depth is at least theirs: a pair
+// whose known lower bound already exceeds B cannot be budget-free and its depth is not computed
+// (it stays unknown, which budget_free reads as "not budget-free").
+static int ensure_depths(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need,
+                         const std::vector<uint32_t>& need_b) {
   if (!x->depth_pin.p) return 0;
   uint32_t* dp = x->depth_pin.as<uint32_t>();
   std::vector<ChainJob> byl[10];
   size_t tot = 0;
-  for (const auto& q : need) {
-    const uint32_t s = q.first;
-    const int m = q.second;
+  for (size_t qi = 0; qi < need.size(); qi++) {
+    const uint32_t s = need[qi].first;
+    const int m = need[qi].second;
     const size_t i = 10 * (size_t)s + (size_t)m;
     if (dp[i] != ~0u || x->recs[s].infl_len >= 65536) continue;
+    const int top = m <= 2 ? 2 : m <= 5 ? 5 : m <= 8 ? 8 : 9;
+    uint32_t lb = 0;
+    for (int m2 = m + 1; m2 <= top; m2++) {
+      const uint32_t d = dp[10 * (size_t)s + (size_t)m2];
+      if (d < 0xfffffffeu && d > lb) lb = d;
+    }
+    if (lb > need_b[qi]) continue;
     dp[i] = 0xfffffffeu;   // queued (the kernel overwrites it)
     ChainJob jb{};
     jb.infl_off = x->infl_off[s];
@@ -1195,20 +1185,6 @@ static int ensure_depths(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32
     KCHECK("k_bucket_depth");
   }
   for (const ChainJob& jb : all) c->stats.k_chains_alg_bytes += jb.n;
-  return 0;
-}
-// Speculative builds for the next round on the prefetch stream; skipped when they would need the
-// cache dropped or grown (both are only done between rounds, on the pipe's stream).
-static int chains_prefetch(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need) {
-  if (int r = chains_prefetch_collect(c)) return r;
-  std::swap(c->st, c->pst);
-  std::swap(c->kt, c->pkt);
-  int r = ensure_chains_on(x, c, need, c->cb[1], true);
-  std::swap(c->st, c->pst);
-  std::swap(c->kt, c->pkt);
-  if (r) return r;
-  HIPCHK(hipEventRecord(c->pev, c->pst));
-  c->pev_pending = true;
   return 0;
 }
 // The kernels of one set of bucket jobs, writing at chains + job.chain_off.
@@ -1247,13 +1223,9 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
     if (jobs.empty()) return 0;
   }
   // hash tables of memLevel <= 8 and streams < 64 Ki positions: LDS kernels; memLevel 9: HBM scratch
-  static int pk8 = -1;   // ATZ_PK8=1: memLevel 8 on packed 16-bit counters (2 blocks per CU; measured
-                         // 838 vs 852 MB/s on C4: its builds are faster but slow the concurrent trials)
-  if (pk8 < 0) { const char* e = std::getenv("ATZ_PK8"); pk8 = e ? std::atoi(e) : 0; }
-  std::vector<ChainJob> tiny, small, mid, big, eight;
+  std::vector<ChainJob> tiny, small, mid, big;
   for (const ChainJob& jb : jobs) {
     const uint32_t hs = 1u << (jb.memlevel + 7);
-    if (pk8 && hs == 32768 && jb.n < 65536) { eight.push_back(jb); continue; }
     (jb.n >= 65536 || hs > 32768 ? big : hs <= 4096 ? tiny : hs <= 16384 ? small : mid).push_back(jb);
   }
   {
@@ -1280,26 +1252,18 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
   std::vector<ChainJob> nine, rest;   // memLevel 9 with n < 64 Ki: packed LDS counters + HBM bases
   for (const ChainJob& jb : big) ((jb.memlevel == 9 && jb.n < 65536) ? nine : rest).push_back(jb);
   big.swap(rest);
-  if (!nine.empty() || !eight.empty()) {   // packed counters: memLevel 8 first, then 9
+  if (!nine.empty()) {   // memLevel 9 on packed 16-bit LDS counters
     const size_t nbs = 4096;   // HBM scratch slots for the bucket bases, reused in launch order
     if (int r = B.d_heads2.reserve(nbs * 65536 * 4)) return r;
-    std::vector<ChainJob> pk(eight);
-    pk.insert(pk.end(), nine.begin(), nine.end());
+    std::vector<ChainJob>& pk = nine;
     for (size_t k = 0; k < pk.size(); k++) pk[k].slot = (uint32_t)(k % nbs);
     if (int r = upload(c, B.d_cjobs3, pk.data(), pk.size() * sizeof(ChainJob))) return r;
     for (size_t b0 = 0; b0 < pk.size();) {
-      const bool is8 = b0 < eight.size();
-      const size_t end = is8 ? eight.size() : pk.size();
-      const size_t nb = std::min(nbs - b0 % nbs, end - b0);   // a launch never holds two jobs of one slot
+      const size_t nb = std::min(nbs - b0 % nbs, pk.size() - b0);   // a launch never holds two jobs of one slot
       kbeg(c, 2);
-      if (is8)
-        hipLaunchKernelGGL(k_buckets_pk<15>, dim3((uint32_t)nb), dim3(256), 0, c->st, INFL_BASE,
-                           B.d_cjobs3.as<ChainJob>() + b0, chains, B.d_heads2.as<uint32_t>(),
-                           (uint32_t)nb);
-      else
-        hipLaunchKernelGGL(k_buckets_pk<16>, dim3((uint32_t)nb), dim3(256), 0, c->st, INFL_BASE,
-                           B.d_cjobs3.as<ChainJob>() + b0, chains, B.d_heads2.as<uint32_t>(),
-                           (uint32_t)nb);
+      hipLaunchKernelGGL(k_buckets_pk<16>, dim3((uint32_t)nb), dim3(256), 0, c->st, INFL_BASE,
+                         B.d_cjobs3.as<ChainJob>() + b0, chains, B.d_heads2.as<uint32_t>(),
+                         (uint32_t)nb);
       kend(c);
       KCHECK("k_buckets_pk");
       b0 += nb;
@@ -1322,18 +1286,15 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
   return 0;
 }
 
-static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need, ChainBufs& B,
-                            bool prefetch) {
+static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need, ChainBufs& B) {
   auto words = [&](uint32_t s) { return 2 * ((x->recs[s].infl_len + 63) & ~63ull); };
   uint64_t add = 0;
   for (auto& q : need)
     if (x->chain_off[q.first][q.second] == ~0ull) add += words(q.first);
   if ((c->chain_used + add) * 4 > c->chain_cap) {   // drop this pipe's cache
-    if (prefetch) return 0;
     for (uint32_t s : c->streams) x->chain_off[s].fill(~0ull);
     c->chain_used = 0;
   }
-  if (prefetch && (c->chain_used + add) * 4 + 4096 > c->d_chains.n) return 0;
   std::vector<ChainJob> jobs;
   for (auto& q : need) {
     uint32_t s = q.first;
@@ -1361,7 +1322,6 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     if (cap < need_bytes) cap = need_bytes;
     if (hipMalloc(&np, cap) != hipSuccess) return ATZ_E_NOMEM;
     if (c->d_chains.p) {
-      if (int r = chains_prefetch_collect(c)) return r;
       HIPCHK(hipMemcpyAsync(np, c->d_chains.p, c->d_chains.n, hipMemcpyDeviceToDevice, c->st));
       HIPCHK(hipStreamSynchronize(c->st));
       (void)hipFree(c->d_chains.p);
@@ -1369,8 +1329,8 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     c->d_chains.p = np;
     c->d_chains.n = cap;
   }
-  if (int r = build_bucket_jobs(x, c, B, jobs, c->d_chains.as<uint32_t>(), bucket_sort_on(), x->depth_pin.as<uint32_t>())) return r;
-  if (bucket_verify() && bucket_sort_on()) {
+  if (int r = build_bucket_jobs(x, c, B, jobs, c->d_chains.as<uint32_t>(), true, x->depth_pin.as<uint32_t>())) return r;
+  if (bucket_verify()) {
     // diagnostics (ATZ_BUCKETS_VERIFY=1): the same jobs again on the in-order kernels, compared
     uint64_t tot = 0;
     std::vector<ChainJob> alt(jobs);
@@ -1401,15 +1361,8 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
 
 // Match-table prefix for a trial that may stop early: enough positions for the blocks that decide
 // the shortcut (~3 positions per symbol, lit_bufsize symbols per block); the rest on demand.
-static uint64_t match_prefix(uint64_t n, int memlevel) {
-  static uint64_t pmin = 1024, pmul4 = 8;   // 2 * lit_bufsize positions (measured on C4: 1.5x-6x)
-  static bool init = false;
-  if (!init) {   // ATZ_XLIM=min,mul*4 (tuning)
-    init = true;
-    if (const char* e = std::getenv("ATZ_XLIM")) std::sscanf(e, "%llu,%llu", (unsigned long long*)&pmin, (unsigned long long*)&pmul4);
-  }
-  uint64_t x = std::max<uint64_t>(pmin, (pmul4 << (memlevel + 6)) >> 2);
-  return std::min(n, x);
+static uint64_t match_prefix(uint64_t n, int memlevel) {   // 2 x lit_bufsize positions, at least 1024
+  return std::min(n, std::max<uint64_t>(1024, 2ull << (memlevel + 6)));
 }
 
 static uint32_t lazy_host(uint32_t level) {   // max_lazy of levels 7-9 (Z/deflate.c:141-143)
@@ -1434,16 +1387,8 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
     for (int k = 0; k < NC; k++) if (b <= cls[k]) return k;
     return NC;
   };
-  // launch groups: classes are merged into groups (one launch each, LDS of the group's largest class)
-  // so a round pays few launch tails; within a launch the longest walks go first (LPT)
-  static int groups = -1;   // ATZ_MATCH_GROUPS: 0 one launch per class, 1 two groups (<= 8 KiB, more), 2 one
-  if (groups < 0) { const char* e = std::getenv("ATZ_MATCH_GROUPS"); groups = e ? std::atoi(e) : 0; }   // C4: 0 847, 1 831, 2 834 MB/s
-  auto group_of = [&](int k) -> int {
-    if (k == NC) return NC;
-    if (groups == 0) return k;
-    if (groups == 1) return k <= 1 ? 1 : NC - 1;
-    return NC - 1;
-  };
+  // one launch per class; within a launch the longest walks go first (LPT)
+  auto group_of = [](int k) -> int { return k; };
   std::vector<MatchJob> mj;
   mj.reserve(mj0.size());
   size_t cnt[NC + 1] = {};
@@ -1490,34 +1435,13 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
 // Runs the trials tr[k] (k = 0 stored, 1 fast, 2 slow levels); res[k] receives their results.
 // Chain tables must exist.  Match tables are built for a prefix of each trial's positions; a
 // trial that parses past it (TR_NEED_R) gets the rest of its table and is run again.
-static bool split_kinds() {
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_SPLIT_KINDS"); v = e ? std::atoi(e) : 0; }   // off: 772 -> 735 MB/s on C4
-  return v != 0;
-}
-static bool chain_prefetch_on() {   // ATZ_CHAIN_PREFETCH=0 disables the next-round bucket builds
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_CHAIN_PREFETCH"); v = e ? std::atoi(e) : 0; }   // off: measured 739 -> 708 MB/s on C4 (bucket builds compete with the trials)
-  return v != 0;
-}
-static uint64_t full_tables_below() {   // ATZ_FULL_BELOW=n: rounds of <= n trials build whole match tables
-  static int64_t v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_FULL_BELOW"); v = e ? std::atoll(e) : 0; }
-  return (uint64_t)v;
-}
 static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
-                           std::vector<TrialRes>* res, const std::function<int()>& while_running, bool allow_defer);
-static bool defer_rerun() {   // ATZ_DEFER_RERUN=1: TR_NEED_R trials wait for the next round (measured
-  static int v = -1;          // 750 vs 855 MB/s on C4: the stream falls a round behind; off)
-  if (v < 0) { const char* e = std::getenv("ATZ_DEFER_RERUN"); v = e ? std::atoi(e) : 0; }
-  return v != 0;
-}
+                           std::vector<TrialRes>* res);
 // A launch lasts as long as its slowest wave, so the trials go in longest-expected-first order
 // (classic LPT): low memLevels mean many blocks (one tree build each), fast levels mean hole
 // fallbacks, and the work grows with the stream.  Results come back in the caller's order.
 static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
-                      std::vector<TrialRes>* res, const std::function<int()>& while_running = nullptr,
-                      bool allow_defer = false) {
+                      std::vector<TrialRes>* res) {
   std::vector<Trial> tp[3];
   std::vector<uint32_t> perm[3];
   std::vector<TrialRes> rp[3];
@@ -1535,7 +1459,7 @@ static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Tri
     tp[k].resize(n);
     for (size_t q = 0; q < n; q++) tp[k][q] = tr[k][perm[k][q]];
   }
-  if (int r = run_trials_impl(x, c, d_cmp, tp, so, rp, while_running, allow_defer)) return r;
+  if (int r = run_trials_impl(x, c, d_cmp, tp, so, rp)) return r;
   for (int k = 0; k < 3; k++) {
     res[k].resize(tr[k].size());
     for (size_t q = 0; q < tr[k].size(); q++) res[k][perm[k][q]] = rp[k][q];
@@ -1543,8 +1467,7 @@ static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Tri
   return 0;
 }
 static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
-                           std::vector<TrialRes>* res, const std::function<int()>& while_running, bool allow_defer) {
-  const bool full = tr[0].size() + tr[1].size() + tr[2].size() <= full_tables_below();
+                           std::vector<TrialRes>* res) {
   uint64_t r_tot = 0;
   std::vector<MatchJob> mj;
   for (int k = 0; k < 3; k++)
@@ -1560,7 +1483,7 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
       if ((t.mode & 24) == 8) { t.r_off = 0; t.x_lim = n; continue; }   // unchecked replays: no match table
       t.r_off = r_tot;
       r_tot += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
-      t.x_lim = ((t.mode & 3) || full) ? n : match_prefix(n, t.memlevel);
+      t.x_lim = (t.mode & 3) ? n : match_prefix(n, t.memlevel);
       MatchJob m{};
       m.infl_off = x->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
       m.p0 = 0; m.p1 = t.x_lim; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
@@ -1588,48 +1511,21 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
     KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
     return 0;
   };
-  // ATZ_SPLIT_KINDS=1: fast-level trials on the pipe's second stream, concurrently with the
-  // slow-level launch (overlapping the two tails; measured slower, so off by default)
-  bool forked = false;
-  auto launch_kind = [&](int k, const Trial* h, size_t cnt, size_t base) -> int {
-    if (k != 1 || !split_kinds()) return launch(k, h, cnt, base);
-    HIPCHK(hipEventRecord(c->fev0, c->st));
-    HIPCHK(hipStreamWaitEvent(c->pst, c->fev0, 0));
-    std::swap(c->st, c->pst);
-    const int r = launch(k, h, cnt, base);
-    std::swap(c->st, c->pst);
-    forked = true;
-    return r;
-  };
-  auto join = [&]() -> int {
-    if (!forked) return 0;
-    HIPCHK(hipEventRecord(c->fev1, c->pst));
-    HIPCHK(hipStreamWaitEvent(c->st, c->fev1, 0));
-    forked = false;
-    return 0;
-  };
   size_t base = 0;
   size_t bases[3];
   for (int k = 0; k < 3; k++) {
     bases[k] = base;
     res[k].resize(tr[k].size());
     if (tr[k].empty()) continue;
-    if (int r = launch_kind(k, tr[k].data(), tr[k].size(), base)) return r;
+    if (int r = launch(k, tr[k].data(), tr[k].size(), base)) return r;
     base += tr[k].size();
   }
-  if (int r = join()) return r;
   for (int k = 0; k < 3; k++)
     if (!tr[k].empty())
       HIPCHK(hipMemcpyAsync(res[k].data(), c->d_tres.as<TrialRes>() + bases[k], tr[k].size() * sizeof(TrialRes),
                             hipMemcpyDeviceToHost, c->st));
-  if (while_running)
-    if (int r = while_running()) return r;
   HIPCHK(hipStreamSynchronize(c->st));
   kcollect(c);
-  // Trials that parsed past their table prefix (TR_NEED_R) are rerun below with the rest of their
-  // table.  ATZ_DEFER_RERUN=1 instead hands them back to the sweep, which reschedules them in its
-  // next round with the whole table (slower: their stream falls a round behind).
-  if (defer_rerun() && allow_defer) return 0;
   // second pass: complete the match tables of the trials that need them and run those again
   std::vector<Trial> again[3];
   std::vector<size_t> where[3];
@@ -1653,11 +1549,10 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
   std::vector<TrialRes> rr[3];
   for (int k = 1; k < 3; k++) {
     if (again[k].empty()) continue;
-    if (int r = launch_kind(k, again[k].data(), again[k].size(), base)) return r;
+    if (int r = launch(k, again[k].data(), again[k].size(), base)) return r;
     rr[k].resize(again[k].size());
     base += again[k].size();
   }
-  if (int r = join()) return r;
   {
     size_t b2 = base;
     for (int k = 2; k >= 1; k--) b2 -= again[k].size();
@@ -1818,24 +1713,10 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
   }
 }
 
-// ATZ_ROUND_GB=g: match tables + output scratch of one round, over all pipes (default 24 GB)
-static uint64_t round_budget_bytes() {
-  static int64_t v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_ROUND_GB"); v = (int64_t)((e ? std::max(1.0, std::atof(e)) : 24.0) * (1ull << 30)); }
-  return (uint64_t)v;
-}
+// match tables + output scratch of one round, over all pipes
+static constexpr uint64_t ROUND_BUDGET_BYTES = 24ull << 30;
 // The sweep of the streams c->streams on pipe c (per-kind x level counters: count, cycles
 // total/tree/emit/heap/fallback, parsed bytes, symbols, scan/send cycles, parse window phases).
-static size_t tail_active() {   // ATZ_TAIL_ACTIVE=n: rounds with fewer active streams use tail_target()
-  static long v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_TAIL_ACTIVE"); v = e ? std::max(0L, std::atol(e)) : 0; }
-  return (size_t)v;
-}
-static size_t tail_target() {   // ATZ_TAIL_TARGET=n: trials per round and pipe in the tail
-  static long v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_TAIL_TARGET"); v = e ? std::max(256L, std::atol(e)) : 4096; }
-  return (size_t)v;
-}
 static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss, size_t target) {
   auto t0 = std::chrono::steady_clock::now();
   std::vector<uint32_t> active;
@@ -1855,22 +1736,14 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
   // stops at its j-th trial discards the results of the later ones), K sized so a round fills the
   // GPU.  Results are applied per stream strictly in list order, so the outcome is the
   // reference's sequential one; the speculation only changes how much work runs per launch.
-  static size_t chunk = ~(size_t)0;   // ATZ_CHUNK=n: at most n streams per round (the rest wait their turn)
-  if (chunk == ~(size_t)0) { const char* e = std::getenv("ATZ_CHUNK"); chunk = e ? (size_t)std::atoll(e) : 0; }
   while (take_inbox()) {
     if (x->sweep_abort.load(std::memory_order_relaxed)) break;
     rounds++;
     std::vector<uint32_t> waiting;
-    if (chunk && active.size() > chunk) {
-      waiting.assign(active.begin() + chunk, active.end());
-      active.resize(chunk);
-    }
     const auto tl0 = std::chrono::steady_clock::now();
-    // the sweep's tail (few active streams) is latency-bound: every round costs about its slowest
-    // trial, so below tail_active() streams a round speculates deeper (tail_target() trials)
-    const size_t tgt = active.size() < tail_active() ? std::max(target, tail_target()) : target;
-    const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, tgt / active.size()));
+    const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, target / active.size()));
     std::vector<std::pair<uint32_t, int>> need;
+    std::vector<uint32_t> need_b;   // per need entry: the trial's walk budget (replay's budget-free test)
     for (int k = 0; k < 3; k++) tr[k].clear();
     // per stream, its trials of this round in list order: (kind, index in tr[kind])
     // flat: stream a's trials are mine[mbeg[a] .. mbeg[a + 1])
@@ -1878,7 +1751,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     std::vector<uint32_t> mbeg(active.size() + 1);
     mine.reserve(active.size() * K);
     uint64_t out_tot = 0, sym_tot = 0, round_bytes = 0;
-    const uint64_t round_budget = round_budget_bytes() / x->pipes_running;
+    const uint64_t round_budget = ROUND_BUDGET_BYTES / x->pipes_running;
     for (size_t a = 0; a < active.size(); a++) {
       mbeg[a] = (uint32_t)mine.size();
       const uint32_t s = active[a];
@@ -1903,7 +1776,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         t.sym_off = sym_tot; sym_tot += (1ull << (m + 6)) + 64;
         round_bytes += 8 * (x->recs[s].infl_len + 320) + t.out_cap + 4 * ((1ull << (m + 6)) + 64);
         int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
-        if (kind) need.push_back({s, m});
+        if (kind) {
+          need.push_back({s, m});
+          need_b.push_back((uint32_t)(c_cfg_host((uint32_t)cl) >> (kind == 1 ? 0 : 2)));
+        }
         mine.push_back({kind, (uint32_t)tr[kind].size()});
         tr[kind].push_back(t);
       }
@@ -1914,7 +1790,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     // replays first (they need the pairs' bucket depths only), then the tables the other trials read
     std::vector<std::array<uint32_t, 4>> savers;   // (kind, index in tr[kind], rp_pool entry, level - 1)
     if (replay_on() && x->depth_pin.p) {
-      if (int r = ensure_depths(x, c, need)) return r;
+      if (int r = ensure_depths(x, c, need, need_b)) return r;
       HIPCHK(hipStreamSynchronize(c->st));
       if (dedup_on()) level_dups(x, ss, tr[2]);
       for (int k = 1; k < 3; k++) plan_replay(x, c, ss, k, tr[k], savers);
@@ -1945,20 +1821,6 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       }
     if (int r = c->d_out.reserve(out_tot + 4096)) return r;
     if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
-    // while the trials run: the bucket tables the next round will likely need (each stream's next
-    // K list entries, as if it goes on) are built on the prefetch stream
-    auto prefetch = [&]() -> int {
-      if (!chain_prefetch_on()) return 0;
-      std::vector<std::pair<uint32_t, int>> nx;
-      for (size_t a = 0; a < active.size(); a++) {
-        const StreamState& st = ss[active[a]];
-        for (uint32_t j = K; j < 2 * K && st.idx + j < st.list->size(); j++) {
-          const uint32_t pp = (*st.list)[st.idx + j];
-          if ((pp >> 16) != 0 && x->chain_off[active[a]][pp & 0xff] == ~0ull) nx.push_back({active[a], (int)(pp & 0xff)});
-        }
-      }
-      return nx.empty() ? 0 : chains_prefetch(x, c, nx);
-    };
     auto finish_savers = [&]() {   // a complete saved sequence serves the stream's later trials at that level
       for (const auto& sv : savers) {
         const TrialRes& r = trres[sv[0]][sv[1]];
@@ -1978,7 +1840,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     for (int k = 1; k < 3; k++)
       for (const Trial& t : tr[k]) { waiting_trials |= (t.mode & 64) != 0; dups |= (t.mode & 128) != 0; }
     if (!waiting_trials && !dups) {
-      if (int r = run_trials(x, c, d_file, tr, so, trres, prefetch, true)) return r;
+      if (int r = run_trials(x, c, d_file, tr, so, trres)) return r;
       finish_savers();
     } else {
       std::vector<Trial> t1[3], t2[3];
@@ -1993,7 +1855,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
           (w ? i2 : i1)[k].push_back(q);
         }
       }
-      if (int r = run_trials(x, c, d_file, t1, so, r1, prefetch, true)) return r;
+      if (int r = run_trials(x, c, d_file, t1, so, r1)) return r;
       for (int k = 0; k < 3; k++)
         for (size_t j = 0; j < i1[k].size(); j++) trres[k][i1[k][j]] = r1[k][j];
       finish_savers();
@@ -2017,7 +1879,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
             t3[k].push_back(t);
             i3[k].push_back(i2[k][j]);
           }
-        if (int r = run_trials(x, c, d_file, t3, so, r2, nullptr, true)) return r;
+        if (int r = run_trials(x, c, d_file, t3, so, r2)) return r;
         for (int k = 1; k < 3; k++)
           for (size_t j = 0; j < i3[k].size(); j++) trres[k][i3[k][j]] = r2[k][j];
       }
@@ -2047,7 +1909,8 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         const TrialRes& r = trres[k][q];
         const uint64_t C = x->recs[tr[k][q].stream].comp_len;
         c->stats.trial_parsed_bytes += r.parsed;
-        c->stats.n_fast_fallbacks += r.fallbacks;
+        c->stats.n_fast_fallbacks += r.fallbacks & 0xffffffffull;
+        c->stats.n_fast_restarts += r.fallbacks >> 32;
         c->stats.trial_cyc_total += r.cyc_total; c->stats.trial_cyc_tree += r.cyc_tree;
         c->stats.trial_cyc_emit += r.cyc_emit; c->stats.trial_blocks += r.blocks;
         c->stats.trial_cyc_heap += r.cyc_heap; c->stats.trial_cyc_fallback += r.cyc_fallback;
@@ -2069,10 +1932,11 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         const Trial& t = tr[top[i].second.first][top[i].second.second];
         const TrialRes& r = trres[top[i].second.first][top[i].second.second];
         std::fprintf(stderr, "atz: round %llu slow trial: stream %u I=%llu c%u w%u m%u state %u cyc %.1fM syms %llu blocks %llu "
-                     "fallbacks %llu tree %.1fM emit %.1fM\n", (unsigned long long)rounds, t.stream,
+                     "fallbacks %llu tree %.1fM emit %.1fM (heap %.1fM scan %.1fM send %.1fM fb %.1fM)\n", (unsigned long long)rounds, t.stream,
                      (unsigned long long)x->recs[t.stream].infl_len, t.clevel, t.window, t.memlevel, r.state,
                      r.cyc_total / 1e6, (unsigned long long)r.symbols, (unsigned long long)r.blocks,
-                     (unsigned long long)r.fallbacks, r.cyc_tree / 1e6, r.cyc_emit / 1e6);
+                     (unsigned long long)(r.fallbacks & 0xffffffffull), r.cyc_tree / 1e6, r.cyc_emit / 1e6, r.cyc_heap / 1e6,
+                     r.cyc_scan / 1e6, r.cyc_send / 1e6, r.cyc_fallback / 1e6);
       }
     }
     // apply the reference's sequential rule per stream, in list order
@@ -2169,7 +2033,6 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     active.swap(next);
     c->t_apply += ms_since(tc);
   }
-  if (int r = chains_prefetch_collect(c)) return r;
   c->stats.n_trials += ntr; c->stats.n_trials_shortcut += nsc; c->stats.n_rounds = rounds; c->stats.n_hazard += nhz;
   c->stats.n_trials_speculative += nspec;
   c->stats.sweep_ms = ms_since(t0);
@@ -2183,16 +2046,9 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
     std::unique_ptr<Pipe> p(new Pipe());
     p->id = (int)c->pipes.size();
     if (hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
-    // the second stream only for the (off by default) prefetch / split-kind modes: an idle stream
-    // still holds one of the process's GPU_MAX_HW_QUEUES (4) hardware queues, and a pipe whose
-    // stream shares a queue with another pipe's is serialised behind it
-    static int pst = -1;   // ATZ_PST=1: create it anyway (A/B of the hardware-queue mapping)
-    if (pst < 0) { const char* e = std::getenv("ATZ_PST"); pst = e ? std::atoi(e) : 1; }
-    if ((pst || chain_prefetch_on() || split_kinds()) &&
-        hipStreamCreateWithFlags(&p->pst, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
-    if (hipEventCreateWithFlags(&p->pev, hipEventDisableTiming) != hipSuccess) return ATZ_E_HIP;
-    if (hipEventCreateWithFlags(&p->fev0, hipEventDisableTiming) != hipSuccess) return ATZ_E_HIP;
-    if (hipEventCreateWithFlags(&p->fev1, hipEventDisableTiming) != hipSuccess) return ATZ_E_HIP;
+    // the idle second stream (see Pipe::pst): with it two pipes share a hardware queue and their
+    // kernels run back to back, so fewer LDS-heavy kernels co-run (measured faster)
+    if (hipStreamCreateWithFlags(&p->pst, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
     c->pipes.push_back(std::move(p));
   }
   return 0;
@@ -2327,7 +2183,7 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
     t.k_match_launches += q.k_match_launches;
     t.k_trial_alg_bytes += q.k_trial_alg_bytes; t.k_chains_alg_bytes += q.k_chains_alg_bytes;
     t.trial_parsed_bytes += q.trial_parsed_bytes; t.k_match_positions += q.k_match_positions;
-    t.n_trials_rerun += q.n_trials_rerun; t.n_fast_fallbacks += q.n_fast_fallbacks;
+    t.n_trials_rerun += q.n_trials_rerun; t.n_fast_fallbacks += q.n_fast_fallbacks; t.n_fast_restarts += q.n_fast_restarts;
     t.trial_cyc_total += q.trial_cyc_total; t.trial_cyc_tree += q.trial_cyc_tree; t.trial_cyc_emit += q.trial_cyc_emit;
     t.trial_blocks += q.trial_blocks; t.trial_cyc_heap += q.trial_cyc_heap; t.trial_cyc_fallback += q.trial_cyc_fallback;
     t.trial_symbols += q.trial_symbols; t.n_trials_replayed += q.n_trials_replayed; t.n_replay_checked += q.n_replay_checked;
@@ -2485,8 +2341,6 @@ static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::
   return 0;
 }
 
-// ATZ_PIECES=k: the scan runs in k chunk ranges, each handed to the sweep as soon as its records
-// are inflated, so the sweep of the first pieces overlaps the scan of the rest (1: scan, then sweep)
 static bool spec_cont_on() {   // ATZ_SPEC_CONT=0: the scan waits for the first continuations
   static int v = -1;
   if (v < 0) { const char* e = std::getenv("ATZ_SPEC_CONT"); v = e ? std::atoi(e) : 1; }
@@ -2495,11 +2349,6 @@ static bool spec_cont_on() {   // ATZ_SPEC_CONT=0: the scan waits for the first 
 static bool spec_abort_test() {   // ATZ_SPEC_ABORT_TEST=1 (read per call): withdraw the speculative sweep
   const char* e = std::getenv("ATZ_SPEC_ABORT_TEST");
   return e && *e == '1';
-}
-static uint32_t scan_pieces() {
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_PIECES"); v = e ? std::max(1, std::atoi(e)) : 1; }
-  return (uint32_t)v;
 }
 
 static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, uint64_t F, uint64_t* atz_len,
@@ -2522,7 +2371,10 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
   struct KeepSd { SweepRun& R; atz_ctx* c; ~KeepSd() { R.sd.swap(c->sd_keep); } } keep_sd{R, c};
   SweepGuard guard{c, R};
   const uint32_t nch = (uint32_t)S.chunks.size();
-  const uint32_t P = std::max<uint32_t>(1, std::min(scan_pieces(), nch));
+  // The scan runs as one piece: handing the sweep early records of a partial scan (several chunk
+  // ranges, measured 2 pieces 840 vs 1025 MB/s) left late streams' round chains running on a half-empty
+  // GPU.  The piece loop below stays for ATZ_SPEC_CONT=0 (scan, then sweep).
+  const uint32_t P = 1;
   while (c->slabs.size() < P) c->slabs.emplace_back(new DBuf());
   // The sweep's host set-up (per-record tables sized for every candidate, pipe threads) runs on a
   // helper thread while the first piece's candidate inflates keep the GPU busy; with one piece
@@ -2644,7 +2496,7 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
   HIPCHK(hipStreamSynchronize(c->st));   // tables (context stream) before the pipe's kernels
   Pipe* p = c->pipes[0].get();
   if (int r = c->d_tmp.reserve(4096)) return r;   // zero-length "file" for the compare side
-  const uint64_t budget = round_budget_bytes();
+  const uint64_t budget = ROUND_BUDGET_BYTES;
   for (size_t s0 = 0; s0 < n;) {
     // a batch: streams until the scratch estimate passes the budget (at least one)
     size_t s1 = s0;

@@ -87,6 +87,7 @@ struct TrialRes {
   uint64_t symbols;     // diagnostic: symbols tallied
   uint64_t parsed;      // input positions consumed when the trial stopped
   uint64_t fallbacks;   // fast levels: steps that walked the chain because a skipped position was on it
+                        // (low 32 bits), of which walks whose result changed the parse path (high 32)
   uint64_t cyc_total, cyc_tree, cyc_emit, blocks;   // diagnostics: shader clocks in the trial / tree
                                                     // construction / block emission, blocks flushed
   uint64_t cyc_heap, cyc_fallback;                  // tree heap steps (ATZ_STEP_CLOCKS) / fast-level exact walks

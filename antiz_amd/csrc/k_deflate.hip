@@ -2006,6 +2006,9 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       uint64_t t1 = STEP_CLOCK(); csec[0] += t1 - t0; t0 = t1;
       // ---- the table's step at x = wb + lane: wt 0 none (x >= n), 1 literal, 2 match, 3 needs R >= x_lim
       const uint32_t x = wb + lane;
+      // x's bucket index, loaded now and read only by the node checks and the exact walks below (its
+      // latency hides behind the window's own work instead of opening a walk)
+      const uint32_t sxl = x < n ? sidx[x] : 0u;
       uint32_t wt = 0, L = 0, D = 0, ex = 0, ey = 0, Sx = Sb;
       if (x < n) {
         if (x >= xlim) wt = 3;
@@ -2075,7 +2078,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           // one, at most `chain` of them) was inserted -- deflate_fast's chain then starts with
           // the same nodes and spends the same budget on them
           const uint32_t lo = x - (ey >> 16);
-          const int32_t si = (int32_t)sidx[x];
+          const int32_t si = (int32_t)sxl;
           bool ok = true, stop = false;
           for (int32_t k = si - 1; ok && !stop && k > si - 1 - (int32_t)z.chain; k -= 4) {
             uint32_t e4[4];
@@ -2155,27 +2158,32 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         const uint32_t la = n - f < LOOKMIN ? n - f : LOOKMIN;   // lookahead (>= 258 stands for more)
         uint32_t ml = 0, ms = 0;
         {
-          const uint32_t si = uni(sidx[f]);
-          bool done = (uni(bpos[si]) & BUCKET_FIRST) != 0;   // first of its bucket: no chain
+          const uint32_t si = uni((uint32_t)__builtin_amdgcn_readlane((int)sxl, fln));
+          bool done = false;
           bool head_done = false, hv = false, won = false;
           uint32_t examined = 0, best = 2, win = 0;
           const uint32_t limit = f > maxd ? f - maxd : 0u;   // later nodes only while > limit
           const uint32_t cap = n - f < 258u ? n - f : 258u;
           const uint32_t nicec = z.nice < la ? z.nice : la;   // <= cap
-          int32_t top = (int32_t)si - 1;
+          // lane l reads bucket entry top - l; the first chunk starts at f's own entry (lane 0), whose
+          // first-of-bucket flag says whether f has a chain at all
+          int32_t top = (int32_t)si;
+          int skip = 1;
           while (!done) {
             const int32_t k = top - lane;
             const uint32_t e = k >= 0 ? bpos[k] : BUCKET_FIRST;
-            const uint64_t fm = __ballot((e & BUCKET_FIRST) != 0);
+            if (skip && (uni((uint32_t)__builtin_amdgcn_readlane((int)e, 0)) & BUCKET_FIRST)) break;   // first of its bucket: no chain
+            const uint64_t fm = __ballot((e & BUCKET_FIRST) != 0 && lane >= skip);
             const int flane = fm ? __ffsll((unsigned long long)fm) - 1 : 64;   // bucket's first entry: last node
             const uint32_t qc = e & ~BUCKET_FIRST;
-            const bool insd = lane <= flane && k >= 0 && ins_get(qc);
+            const bool insd = lane >= skip && lane <= flane && k >= 0 && ins_get(qc);
             const uint64_t im = __ballot(insd);
             int head_lane = -1, from = 0;
             if (!head_done) {
               if (!im) {   // no inserted node in this chunk yet
                 if (flane < 64) break;
                 top -= 64;
+                skip = 0;
                 continue;
               }
               head_lane = __ffsll((unsigned long long)im) - 1;
@@ -2225,6 +2233,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
             }
             done = examined >= z.chain || slane < 64 || flane < 64;
             top -= 64;
+            skip = 0;
           }
           if (hv && won) {
             ml = best <= la ? best : la;
@@ -2240,6 +2249,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           continue;
         }
         // the path changes at f: its exact step, then a new window after it
+        fallbacks += 1ull << 32;   // diagnostics: walks that changed the path (high half)
         const uint32_t step = ml >= 3 ? ml : 1u;
         span_set(f, f + step, [&](uint32_t p, uint32_t& y, uint32_t& Ly) { y = f; Ly = ml >= 3 ? ml : 0u; });
         const bool full = tally1(ml >= 3 ? (((f - ms) << 8) | (ml - 3u)) : (uint32_t)in[f]);

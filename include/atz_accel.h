@@ -79,6 +79,7 @@ typedef struct {
     uint64_t n_trials_replayed;                          /* trials that replayed a saved symbol sequence */
     uint64_t n_replay_checked;                           /* replays offered under a match-table check (passed or not) */
     uint64_t n_trials_duplicate;                         /* replays whose output equals their saver's: not launched */
+    uint64_t n_fast_restarts;                            /* fast-level exact walks that changed the parse path */
 } atz_stats_t;
 
 enum {

@@ -1,0 +1,57 @@
+"""The library's remaining run-time switches change how the sweep is scheduled, never its result.
+
+Each one is read once per process, so every setting runs in its own subprocess on the same input:
+the ATZ1 bytes must equal the oracle's (the reference's algorithm, oracle/) for each of them.
+  ATZ_REPLAY   0 no symbol replay, 2 save sequences but never replay, 3 replays between budget-free
+               trials only (default 1: DESIGN.md s3.5)
+  ATZ_DEDUP    0 launch duplicate trials anyway (default 1)
+  ATZ_PIPES    sweep pipes, 1..8 (default 3)
+  ATZ_TARGET   trials per round and pipe (speculation depth; default 4096)
+  ATZ_SPEC_CONT 0: the scan waits for the first chunk-boundary continuations (default 1: speculative)
+"""
+import hashlib
+import os
+import subprocess
+import sys
+
+import pytest
+
+import _libs
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SETTINGS = [{"ATZ_REPLAY": "0"}, {"ATZ_REPLAY": "2"}, {"ATZ_REPLAY": "3"}, {"ATZ_DEDUP": "0"},
+            {"ATZ_PIPES": "1"}, {"ATZ_PIPES": "5"}, {"ATZ_TARGET": "256"}, {"ATZ_TARGET": "65536"},
+            {"ATZ_SPEC_CONT": "0"}, {"ATZ_REPLAY": "0", "ATZ_DEDUP": "0", "ATZ_PIPES": "2", "ATZ_SPEC_CONT": "0"}]
+
+RUN = r"""
+import hashlib, sys
+sys.path.insert(0, %r)
+import antiz_amd
+data = open(sys.argv[1], "rb").read()
+with antiz_amd.Context(chunksize=int(sys.argv[2]), device=0) as c:
+    out, st = c.precompress(data)
+print(hashlib.sha256(out).hexdigest())
+""" % ROOT
+
+
+@pytest.fixture(scope="module")
+def sample(tmp_path_factory):
+    from antiz_amd import datagen
+    data = datagen.gen_c4(seed=51, n_streams=700)   # ~7 MB, chunk-boundary streams at 65536
+    path = str(tmp_path_factory.mktemp("knobs") / "c4k.bin")
+    with open(path, "wb") as f:
+        f.write(data)
+    rc, ref, _ = _libs.ora_precompress(data, chunksize=65536)
+    assert rc == 0
+    return path, hashlib.sha256(ref).hexdigest()
+
+
+@pytest.mark.parametrize("env", SETTINGS, ids=lambda e: ",".join("%s=%s" % kv for kv in e.items()))
+def test_switch_keeps_the_atz_bytes(sample, env):
+    path, want = sample
+    r = subprocess.run([sys.executable, "-c", RUN, path, "65536"], env=dict(os.environ, **env),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == want
