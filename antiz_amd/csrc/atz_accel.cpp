@@ -1432,6 +1432,21 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
   return 0;
 }
 
+// Trials with small blocks (memLevel <= 2: lit_bufsize <= 256 symbols) run on the multi-wave kernels
+// (C4, same box, 2 runs each: 1302-1363 vs 1250-1264 MB/s without; the 12 500-stream file 574-593 vs
+// 484-498)
+// (k_trial_{fast,slow}_mw: one parse wave, MW_F flusher waves; k_deflate.hip MWSlot).  Their symbols
+// stay in HBM for the whole stream (the flushers read each block at its own offset).
+static uint32_t mw_max_memlevel() {   // ATZ_MW=m: multi-wave up to memLevel m (0: none; tests/test_gpu_knobs.py)
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_MW"); v = e ? std::max(0, std::min(9, std::atoi(e))) : 2; }
+  return (uint32_t)v;
+}
+static bool mw_trial(int kind, uint32_t memlevel) { return kind != 0 && memlevel <= mw_max_memlevel(); }
+static uint64_t sym_words(int kind, uint32_t memlevel, uint64_t n) {   // symbol buffer of a trial (u32 units)
+  return (mw_trial(kind, memlevel) ? n + 64 : 0) + (1ull << (memlevel + 6)) + 64;
+}
+
 // Runs the trials tr[k] (k = 0 stored, 1 fast, 2 slow levels); res[k] receives their results.
 // Chain tables must exist.  Match tables are built for a prefix of each trial's positions; a
 // trial that parses past it (TR_NEED_R) gets the rest of its table and is run again.
@@ -1455,7 +1470,11 @@ static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Tri
                (uint64_t)((t.mode & 8) ? 1 : 4);   // replays skip the match walks
       perm[k][q] = (uint32_t)q;
     }
-    std::stable_sort(perm[k].begin(), perm[k].end(), [&](uint32_t a, uint32_t b) { return key[a] > key[b]; });
+    // multi-wave trials first (one launch of their own), each group longest first
+    std::stable_sort(perm[k].begin(), perm[k].end(), [&](uint32_t a, uint32_t b) {
+      const bool ma = mw_trial(k, tr[k][a].memlevel), mb = mw_trial(k, tr[k][b].memlevel);
+      return ma != mb ? ma : key[a] > key[b];
+    });
     tp[k].resize(n);
     for (size_t q = 0; q < n; q++) tp[k][q] = tr[k][perm[k][q]];
   }
@@ -1494,7 +1513,7 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
   const size_t tot_trials = tr[0].size() + tr[1].size() + tr[2].size();
   if (int r = c->d_trials.reserve(2 * tot_trials * sizeof(Trial) + 64)) return r;
   if (int r = c->d_tres.reserve(2 * tot_trials * sizeof(TrialRes) + 64)) return r;
-  auto launch = [&](int k, const Trial* h, size_t cnt, size_t base) -> int {
+  auto launch1 = [&](int k, const Trial* h, size_t cnt, size_t base, bool mw) -> int {
     HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + base, h, cnt * sizeof(Trial), hipMemcpyHostToDevice, c->st));
     SweepArgs A;
     A.file = d_cmp; A.infl = INFL_BASE; A.chains = c->d_chains.as<uint32_t>();
@@ -1502,13 +1521,25 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
     A.streams = x->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
     A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
     A.adler = x->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)cnt;
-    dim3 g((uint32_t)cnt), b(64);
+    dim3 g((uint32_t)cnt), b(mw ? MW_THREADS : 64);
     kbeg(c, 0);
     if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
+    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw, g, b, 0, c->st, A);
     else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, 0, c->st, A);
+    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, 0, c->st, A);
     else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
     kend(c);
     KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
+    return 0;
+  };
+  // the multi-wave trials lead each kind's list (run_trials orders them so): one launch each
+  auto launch = [&](int k, const Trial* h, size_t cnt, size_t base) -> int {
+    size_t m = 0;
+    while (m < cnt && mw_trial(k, h[m].memlevel)) m++;
+    if (m)
+      if (int r = launch1(k, h, m, base, true)) return r;
+    if (cnt > m)
+      if (int r = launch1(k, h + m, cnt - m, base + m, false)) return r;
     return 0;
   };
   size_t base = 0;
@@ -1773,9 +1804,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         if (st.idx + j == st.full_at) t.mode |= 2;   // host-only bit: whole match table up front
         t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
-        t.sym_off = sym_tot; sym_tot += (1ull << (m + 6)) + 64;
-        round_bytes += 8 * (x->recs[s].infl_len + 320) + t.out_cap + 4 * ((1ull << (m + 6)) + 64);
         int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
+        const uint64_t sw = sym_words(kind, (uint32_t)m, x->recs[s].infl_len);
+        t.sym_off = sym_tot; sym_tot += sw;
+        round_bytes += 8 * (x->recs[s].infl_len + 320) + t.out_cap + 4 * sw;
         if (kind) {
           need.push_back({s, m});
           need_b.push_back((uint32_t)(c_cfg_host((uint32_t)cl) >> (kind == 1 ? 0 : 2)));
@@ -2503,7 +2535,7 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
     uint64_t bytes = 0;
     while (s1 < n && (s1 == s0 || bytes <= budget)) {
       const int m = (int)(params[s1] & 0xff);
-      bytes += 9 * len[s1] + 4 * (1ull << (m + 6)) + 4096;
+      bytes += 9 * len[s1] + 4 * sym_words(1, (uint32_t)m, len[s1]) + 4096;
       s1++;
     }
     c->chain_off.assign(n, {});
@@ -2525,8 +2557,8 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
       t.stream = (uint32_t)s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 1;
       t.best_ident = 0; t.out_off = out_tot; t.out_cap = bound(len[s], w, m) + 64;
       out_tot += (t.out_cap + 255) & ~255ull;
-      t.sym_off = sym_tot; sym_tot += 1ull << (m + 6);
       const int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
+      t.sym_off = sym_tot; sym_tot += sym_words(kind, (uint32_t)m, len[s]);
       if (kind) t.chain_off = c->chain_off[s][m];
       tr[kind].push_back(t);
       idx[kind].push_back((uint32_t)s);

@@ -871,15 +871,21 @@ struct BitOut {
 };
 
 static constexpr uint32_t STAGE_WORDS = 196;   // 64 * SYM_PER_LANE * 48 / 32 + 2 (+ pad)
-struct TrialShared {
-  BitOut b;              // output / compare state of the trial (in LDS: the flush helpers take it by LDS reference)
-  uint32_t lfreq2[(NLC + 1) / 2];   // block frequencies, two 16-bit counts per word (symbol 2i low)
+struct BlockFreq {       // a block's symbol frequencies, two 16-bit counts per word (symbol 2i low)
+  uint32_t lfreq2[(NLC + 1) / 2];
   uint32_t dfreq2[NDC / 2];
+};
+struct TreeCodes {       // the three trees of the block being flushed
   uint16_t lcode[NLC]; uint8_t llen[NLC + 2];
   uint16_t dcode[NDC]; uint8_t dlen[NDC + 2];
   uint16_t bcode[NBLC]; uint8_t blen[NBLC + 2];
   uint32_t bfreq[NBLC];
   TreeWork w;
+};
+struct TrialShared {
+  BitOut b;              // output / compare state of the trial (in LDS: the flush helpers take it by LDS reference)
+  BlockFreq f;           // the block being parsed
+  TreeCodes k;
   // the bit-packing staging words (STAGE_WORDS) live in the match-table ring's LDS: they are only
   // used while a block is emitted, when the parse is paused (like TreeScratch during build_tree)
 };
@@ -898,6 +904,61 @@ struct TrialSharedSlow {
 };
 static_assert(sizeof(TreeScratch) <= RING_SLOW * sizeof(uint64_t), "tree scratch overlays the ring");
 static_assert(STAGE_WORDS * 4 <= RING_SLOW * sizeof(uint64_t), "emission staging overlays the ring");
+
+// Multi-wave trials (small blocks: memLevel <= MW_MAX_MEMLEVEL, host side).  A block of lit_bufsize
+// = 2^(memLevel + 6) symbols is flushed every ~128-256 positions, and the flush -- three Huffman trees
+// with zlib's serial heap, then the block's bits -- costs more than parsing it, so such a trial is
+// bound by its flushes (a stream's 90 block trees at memLevel 1 took most of a tail round).  Wave 0
+// parses as a single-wave trial does and hands each finished block (its frequencies and bounds; the
+// symbols stay in HBM) to flusher wave 1 + (block mod MW_F); the flushers build their blocks' trees
+// side by side and emit them strictly in block order, each block appending to the one bit output
+// and comparing it with the original.  A flusher that decides the trial (the early-exit gates, or
+// the final gates after the last block) raises `stop`; the parser checks it at every hand-over.
+static constexpr int MW_F = 3;   // flusher waves per multi-wave trial
+struct MWSlot {                  // a finished block waiting for its flusher
+  BlockFreq f;
+  int64_t block_start;
+  uint64_t p, S;
+  uint32_t last_lit, sbase, last, seq;   // seq: block index + 1 while the slot holds a block, 0 when free
+};
+struct MWFlusher {
+  TreeCodes k;
+  TreeScratch sc;                // gen_bitlen scratch, then the emission staging
+  uint64_t cyc_tree, cyc_emit;   // diagnostics
+};
+struct MWCtl {
+  uint32_t next_emit;   // index of the next block to emit
+  uint32_t stop;        // the trial is decided (state), or the parser gave up (TR_NEED_R)
+  uint32_t parse_done, nblocks;
+  uint32_t state, hazard;
+};
+struct MWPart {
+  MWSlot slot[MW_F];
+  MWFlusher fl[MW_F];
+  MWCtl ctl;
+};
+struct TrialSharedFastMW {
+  TrialShared t;
+  uint64_t ring[512];
+  uint32_t ins[BITMAP_BITS / 32];
+  uint32_t holes[HOLE_SLOTS];
+  MWPart mw;
+};
+struct TrialSharedSlowMW {
+  TrialShared t;
+  uint64_t ring[RING_SLOW];
+  MWPart mw;
+};
+static_assert(sizeof(TrialSharedFastMW) <= 64 * 1024 && sizeof(TrialSharedSlowMW) <= 64 * 1024, "static LDS of a block");
+template <typename T> struct HasMW { static constexpr bool value = false; };
+template <> struct HasMW<TrialSharedFastMW> { static constexpr bool value = true; };
+template <> struct HasMW<TrialSharedSlowMW> { static constexpr bool value = true; };
+__device__ __forceinline__ uint32_t ld_acq(const LDS uint32_t& x) {
+  return uni(__hip_atomic_load(&x, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void st_rel(LDS uint32_t& x, uint32_t v, int lane) {
+  if (lane == 0) __hip_atomic_store(&x, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 struct SweepArgs {
   const uint8_t* file;          // original compressed bytes
@@ -1358,7 +1419,7 @@ __device__ __forceinline__ void emit_lane_bits(LDS BitOut& b, LDS uint32_t* stag
 // (v only in the run's first chunk, where prevlen != v), REPZ_3_10+3 or REPZ_11_138+7.  So every
 // element finds its run (ballot masks of run starts; max_code + 1 is zlib's guard) and a chunk's
 // first element contributes the chunk: send = its bits in element order, else its bl_tree counts.
-__device__ void rle_tree(LDS BitOut& b, LDS TrialShared& s, LDS uint32_t* stage, const LDS uint8_t* ln, int max_code, bool send,
+__device__ void rle_tree(LDS BitOut& b, LDS TreeCodes& s, LDS uint32_t* stage, const LDS uint8_t* ln, int max_code, bool send,
                          int lane) {
   const int N = max_code + 1;   // elements; position N acts as a run start (the guard)
   const int G = N / 64 + 1;     // groups covering 0..N (N <= 286: at most 5)
@@ -1437,7 +1498,7 @@ __device__ void rle_tree(LDS BitOut& b, LDS TrialShared& s, LDS uint32_t* stage,
 // tested after every step: a bailed trial stops inside its first block instead of emitting all of
 // it.  Returns true when the trial is decided (the caller re-evaluates early_exit).
 template <typename C16, typename C8>
-__device__ bool compress_block(LDS BitOut& b, LDS TrialShared& s, LDS uint32_t* stage, const GLOBAL uint32_t* syms, uint32_t nsym,
+__device__ bool compress_block(LDS BitOut& b, LDS uint32_t* stage, const GLOBAL uint32_t* syms, uint32_t nsym,
                                C16 lc, C8 ll, C16 dc, C8 dl, const SweepOpts& o, uint64_t best_ident,
                                bool full_needed, int lane) {
   // the symbols were stored by other lanes during the parse: order those HBM stores before the reads
@@ -1530,21 +1591,77 @@ __device__ inline uint32_t common_len(const uint8_t* in, uint64_t a, uint64_t b,
   return cap;
 }
 
-// _tr_flush_block (Z/trees.c:907-1004) + FLUSH_BLOCK_ONLY bookkeeping
-// The parse state is passed by value so that it never leaves registers (a reference to it here
-// would put the whole parse state in scratch memory).  Returns the overlay-hazard bit.
-__device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch& sc, LDS BitOut& b, const GLOBAL uint32_t* syms,
-                                             const GLOBAL uint8_t* in,
-                                             int64_t block_start, uint64_t p, uint64_t S, uint32_t last_lit,
-                                             uint32_t level, uint32_t lbs, int last, SweepOpts opt,
-                                             uint64_t best_ident, bool full_needed, int lane) {
+// _tr_flush_block (Z/trees.c:907-1004), in two parts: the trees of a block (from its frequencies
+// alone) and its emission (in block order: it appends to the trial's bit output).  A single-wave
+// trial runs both back to back (flush_block); a multi-wave trial builds the trees of several blocks
+// at once on its flusher waves and emits them in order (trial_flusher).
+struct BlockPlan {
+  uint64_t opt_lenb, static_lenb;
+  int lmax, dmax, max_blindex;
+};
+__device__ __noinline__ BlockPlan block_trees(const LDS BlockFreq& f, LDS TreeCodes& s, LDS TreeScratch& sc, LDS BitOut& b,
+                                              uint32_t level, uint64_t stored_len, int lane) {
+  level = uni(level);
+  stored_len = uni(stored_len);
+  BlockPlan pl{};
+  uint64_t opt_len = 0, static_len = 0;
+  if (level > 0) {
+    // literal/length tree
+    for (int i = lane; i < NLC; i += 64) sc.freq[i] = (uint16_t)(f.lfreq2[i >> 1] >> (16 * (i & 1)));
+    TreeRes r = build_tree(s.w, sc, s.llen, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
+                           b.cyc_heap, lane);
+    pl.lmax = (int)uni((uint32_t)r.max_code);
+    opt_len += uni(r.d_opt);
+    static_len += uni(r.d_static);
+    gen_codes(s.w, pl.lmax, s.lcode, s.llen, lane);
+    for (int i = pl.lmax + 1 + lane; i < NLC + 2; i += 64) s.llen[i] = 0;
+    // distance tree
+    for (int i = lane; i < NDC; i += 64) sc.freq[i] = (uint16_t)(f.dfreq2[i >> 1] >> (16 * (i & 1)));
+    r = build_tree(s.w, sc, s.dlen, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
+                   b.cyc_heap, lane);
+    pl.dmax = (int)uni((uint32_t)r.max_code);
+    opt_len += uni(r.d_opt);
+    static_len += uni(r.d_static);
+    gen_codes(s.w, pl.dmax, s.dcode, s.dlen, lane);
+    for (int i = pl.dmax + 1 + lane; i < NDC + 2; i += 64) s.dlen[i] = 0;
+    // bit length tree
+    for (int i = lane; i < NBLC; i += 64) s.bfreq[i] = 0;
+    const uint64_t cs0 = STEP_CLOCK();
+    rle_tree(b, s, nullptr, s.llen, pl.lmax, false, lane);
+    rle_tree(b, s, nullptr, s.dlen, pl.dmax, false, lane);
+    b.cyc_scan += STEP_CLOCK() - cs0;
+    for (int i = lane; i < NBLC; i += 64) sc.freq[i] = (uint16_t)s.bfreq[i];
+    r = build_tree(s.w, sc, s.blen, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, b.cyc_heap, lane);
+    const int bmax = (int)uni((uint32_t)r.max_code);
+    opt_len += uni(r.d_opt);
+    gen_codes(s.w, bmax, s.bcode, s.blen, lane);
+    for (int i = bmax + 1 + lane; i < NBLC + 2; i += 64) s.blen[i] = 0;
+    int mb;
+    for (mb = NBLC - 1; mb >= 3; mb--)
+      if (s.blen[bl_order((uint32_t)mb)] != 0) break;
+    pl.max_blindex = mb;
+    opt_len += 3 * ((uint64_t)mb + 1) + 5 + 5 + 4;
+    pl.opt_lenb = (opt_len + 3 + 7) >> 3;
+    pl.static_lenb = (static_len + 3 + 7) >> 3;
+    if (pl.static_lenb <= pl.opt_lenb) pl.opt_lenb = pl.static_lenb;
+  } else {
+    pl.opt_lenb = pl.static_lenb = stored_len + 5;
+  }
+  return pl;
+}
+
+// The block's bits, compared with the original as they are written.  Returns the overlay-hazard bit.
+__device__ __noinline__ uint32_t block_emit(LDS TreeCodes& s, LDS uint32_t* stage, LDS BitOut& b, const GLOBAL uint32_t* syms,
+                                            const GLOBAL uint8_t* in, int64_t block_start, uint64_t p, uint64_t S,
+                                            uint32_t last_lit, uint32_t lbs, int last, SweepOpts opt, uint64_t best_ident,
+                                            bool full_needed, uint64_t opt_lenb, uint64_t static_lenb, int lmax, int dmax,
+                                            int max_blindex, int lane) {
   syms = uni_ptr(syms);
   in = uni_ptr(in);
   block_start = (int64_t)uni((uint64_t)block_start);
   p = uni(p);
   S = uni(S);
   last_lit = uni(last_lit);
-  level = uni(level);
   lbs = uni(lbs);
   last = (int)uni((uint32_t)last);
   opt.recomp_tresh = uni(opt.recomp_tresh);
@@ -1553,56 +1670,15 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
   opt.mismatch_tol = uni(opt.mismatch_tol);
   best_ident = uni(best_ident);
   full_needed = uni((uint32_t)full_needed) != 0;
+  opt_lenb = uni(opt_lenb);
+  static_lenb = uni(static_lenb);
+  lmax = (int)uni((uint32_t)lmax);
+  dmax = (int)uni((uint32_t)dmax);
+  max_blindex = (int)uni((uint32_t)max_blindex);
   uint32_t hazard = 0;
-  LDS uint32_t* const stage = (LDS uint32_t*)&sc;   // emission staging overlays the tree scratch
-  const uint64_t c0 = clock64();
   const bool bufok = block_start >= (int64_t)S;
   const uint64_t stored_len = (uint64_t)((int64_t)p - block_start);
-  uint64_t opt_len = 0, static_len = 0, opt_lenb, static_lenb;
-  int lmax = 0, dmax = 0, max_blindex = 0;
-  if (level > 0) {
-    // literal/length tree
-    for (int i = lane; i < NLC; i += 64) sc.freq[i] = (uint16_t)(s.lfreq2[i >> 1] >> (16 * (i & 1)));
-    TreeRes r = build_tree(s.w, sc, s.llen, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
-                           b.cyc_heap, lane);
-    lmax = (int)uni((uint32_t)r.max_code);
-    opt_len += uni(r.d_opt);
-    static_len += uni(r.d_static);
-    gen_codes(s.w, lmax, s.lcode, s.llen, lane);
-    for (int i = lmax + 1 + lane; i < NLC + 2; i += 64) s.llen[i] = 0;
-    // distance tree
-    for (int i = lane; i < NDC; i += 64) sc.freq[i] = (uint16_t)(s.dfreq2[i >> 1] >> (16 * (i & 1)));
-    r = build_tree(s.w, sc, s.dlen, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
-                   b.cyc_heap, lane);
-    dmax = (int)uni((uint32_t)r.max_code);
-    opt_len += uni(r.d_opt);
-    static_len += uni(r.d_static);
-    gen_codes(s.w, dmax, s.dcode, s.dlen, lane);
-    for (int i = dmax + 1 + lane; i < NDC + 2; i += 64) s.dlen[i] = 0;
-    // bit length tree
-    for (int i = lane; i < NBLC; i += 64) s.bfreq[i] = 0;
-    const uint64_t cs0 = STEP_CLOCK();
-    rle_tree(b, s, stage, s.llen, lmax, false, lane);
-    rle_tree(b, s, stage, s.dlen, dmax, false, lane);
-    b.cyc_scan += STEP_CLOCK() - cs0;
-    for (int i = lane; i < NBLC; i += 64) sc.freq[i] = (uint16_t)s.bfreq[i];
-    r = build_tree(s.w, sc, s.blen, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, b.cyc_heap, lane);
-    const int bmax = (int)uni((uint32_t)r.max_code);
-    opt_len += uni(r.d_opt);
-    gen_codes(s.w, bmax, s.bcode, s.blen, lane);
-    for (int i = bmax + 1 + lane; i < NBLC + 2; i += 64) s.blen[i] = 0;
-    for (max_blindex = NBLC - 1; max_blindex >= 3; max_blindex--)
-      if (s.blen[bl_order((uint32_t)max_blindex)] != 0) break;
-    opt_len += 3 * ((uint64_t)max_blindex + 1) + 5 + 5 + 4;
-    opt_lenb = (opt_len + 3 + 7) >> 3;
-    static_lenb = (static_len + 3 + 7) >> 3;
-    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
-  } else {
-    opt_lenb = static_lenb = stored_len + 5;
-  }
   const uint64_t blk_start_bytes = b.pos;
-  const uint64_t c1 = clock64();
-  b.cyc_tree += c1 - c0;
   b.blocks++;
   if (stored_len + 4 <= opt_lenb && bufok) {
     put_bits(b, stage, (uint32_t)last, 3, lane);
@@ -1626,7 +1702,7 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
     }
   } else if (static_lenb == opt_lenb) {
     put_bits(b, stage, (1u << 1) + (uint32_t)last, 3, lane);
-    compress_block(b, s, stage, syms, last_lit, (const CONSTANT uint16_t*)c_t.st_lcode, (const CONSTANT uint8_t*)c_t.st_llen,
+    compress_block(b, stage, syms, last_lit, (const CONSTANT uint16_t*)c_t.st_lcode, (const CONSTANT uint8_t*)c_t.st_llen,
                    (const CONSTANT uint16_t*)c_t.st_dcode, (const CONSTANT uint8_t*)c_t.st_dlen, opt, best_ident,
                    full_needed, lane);
   } else {
@@ -1641,18 +1717,36 @@ __device__ __noinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch
     rle_tree(b, s, stage, s.dlen, dcodes - 1, true, lane);
     b.cyc_send += STEP_CLOCK() - cs0;
     flush_bits_bytes(b, stage, lane);
-    compress_block(b, s, stage, syms, last_lit, (const LDS uint16_t*)s.lcode, (const LDS uint8_t*)s.llen,
+    compress_block(b, stage, syms, last_lit, (const LDS uint16_t*)s.lcode, (const LDS uint8_t*)s.llen,
                    (const LDS uint16_t*)s.dcode, (const LDS uint8_t*)s.dlen, opt, best_ident, full_needed, lane);
   }
   // 1.2.8 pending_buf/d_buf overlay condition (conservative, cf. oracle/ora_deflate.c)
   if (b.pos - blk_start_bytes > (uint64_t)lbs + 2ull * last_lit && last_lit) hazard = 1;
-  // init_block
-  for (int i = lane; i < (NLC + 1) / 2; i += 64) s.lfreq2[i] = 0;
-  for (int i = lane; i < NDC / 2; i += 64) s.dfreq2[i] = 0;
-  if (lane == 0) s.lfreq2[128] = 1;   // END_BLOCK (symbol 256: low half)
   if (last) windup(b, stage, lane);
-  b.cyc_emit += clock64() - c1;
   return hazard;
+}
+
+__device__ __forceinline__ void init_block(LDS BlockFreq& f, int lane) {   // Z/trees.c:409-425
+  for (int i = lane; i < (NLC + 1) / 2; i += 64) f.lfreq2[i] = 0;
+  for (int i = lane; i < NDC / 2; i += 64) f.dfreq2[i] = 0;
+  if (lane == 0) f.lfreq2[128] = 1;   // END_BLOCK (symbol 256: low half)
+}
+
+// _tr_flush_block + FLUSH_BLOCK_ONLY bookkeeping on one wave: trees, emission, init_block.  The emission
+// staging overlays the tree scratch.  Returns the overlay-hazard bit.
+__device__ __forceinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScratch& sc, LDS BitOut& b, const GLOBAL uint32_t* syms,
+                                                const GLOBAL uint8_t* in, int64_t block_start, uint64_t p, uint64_t S,
+                                                uint32_t last_lit, uint32_t level, uint32_t lbs, int last, const SweepOpts& opt,
+                                                uint64_t best_ident, bool full_needed, int lane) {
+  const uint64_t c0 = clock64();
+  const BlockPlan pl = block_trees(s.f, s.k, sc, b, level, (uint64_t)((int64_t)p - block_start), lane);
+  const uint64_t c1 = clock64();
+  b.cyc_tree += c1 - c0;
+  const uint32_t hz = block_emit(s.k, (LDS uint32_t*)&sc, b, syms, in, block_start, p, S, last_lit, lbs, last, opt, best_ident,
+                                 full_needed, pl.opt_lenb, pl.static_lenb, pl.lmax, pl.dmax, pl.max_blindex, lane);
+  init_block(s.f, lane);
+  b.cyc_emit += clock64() - c1;
+  return hz;
 }
 
 // The parse path through a window of 64 lanes (lane i = position wb + i).  Lane i's node kind:
@@ -1720,8 +1814,80 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t cnt, uint64_t lt, uin
   return o;
 }
 
+// One flusher wave of a multi-wave trial: blocks f, f + MW_F, f + 2 MW_F, ... (see MWSlot).
+__device__ void trial_flusher(const SweepArgs& A, LDS TrialShared& s, LDS MWPart& mw, const Trial& tr,
+                              const GLOBAL uint32_t* syms, const GLOBAL uint8_t* in, uint32_t level, uint32_t lbs,
+                              bool full_needed, int f, int lane) {
+  LDS BitOut& b = s.b;
+  LDS MWFlusher& me = mw.fl[f];
+  LDS MWSlot& sl = mw.slot[f];
+  LDS MWCtl& ctl = mw.ctl;
+  LDS uint32_t* const stage = (LDS uint32_t*)&me.sc;
+  for (uint32_t k = (uint32_t)f;; k += MW_F) {
+    bool have = false;
+    for (;;) {   // block k arrives in slot f
+      if (ld_acq(ctl.stop)) break;
+      if (ld_acq(sl.seq) == k + 1) { have = true; break; }
+      if (ld_acq(ctl.parse_done) && k >= ld_acq(ctl.nblocks)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!have) break;
+    const int64_t bs = (int64_t)uni((uint64_t)sl.block_start);
+    const uint64_t p = uni(sl.p), S = uni(sl.S);
+    const uint32_t last_lit = uni(sl.last_lit), sbase = uni(sl.sbase);
+    const int last = (int)uni(sl.last);
+    const uint64_t c0 = clock64();
+    const BlockPlan pl = block_trees(sl.f, me.k, me.sc, b, level, (uint64_t)((int64_t)p - bs), lane);
+    st_rel(sl.seq, 0u, lane);   // the parser may refill the slot
+    const uint64_t c1 = clock64();
+    bool turn = false;
+    for (;;) {   // emission in block order
+      if (ld_acq(ctl.stop)) break;
+      if (ld_acq(ctl.next_emit) == k) { turn = true; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!turn) break;
+    const uint64_t c2 = clock64();
+    const uint32_t hz = uni(block_emit(me.k, stage, b, syms + sbase, in, bs, p, S, last_lit, lbs, last, A.o, tr.best_ident,
+                                       full_needed, pl.opt_lenb, pl.static_lenb, pl.lmax, pl.dmax, pl.max_blindex, lane));
+    if (hz && lane == 0) __hip_atomic_fetch_or(&ctl.hazard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    uint32_t st = ~0u;
+    if (last) {
+      // adler32 trailer and the final gates (main.cpp:632-681), as a single-wave trial ends
+      const uint32_t ad = A.adler[tr.stream];
+      const uint32_t be = ((ad >> 24) & 0xff) | ((ad >> 8) & 0xff00) | ((ad << 8) & 0xff0000) | (ad << 24);
+      put_bits(b, stage, be, 32, lane);
+      flush_bits_bytes(b, stage, lane);
+      if (uni((uint32_t)b.overflow)) st = TR_OVERFLOW;
+      else if (full_needed) st = TR_FULL;
+      else {
+        const uint64_t thr = A.o.shortcut_len - A.o.recomp_tresh;
+        const uint64_t L = uni(b.pos), clen = uni(b.clen);
+        const int64_t dd = (int64_t)(L - clen);
+        const uint64_t ad2 = (uint64_t)(dd < 0 ? -dd : dd);
+        if (uni(b.shortcut) && uni(b.eq_sc) < thr) st = TR_SHORTCUT;
+        else if (ad2 > A.o.sizediff_tresh) st = TR_SIZEDIFF;
+        else st = TR_FULL;
+      }
+    } else {
+      st = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+    }
+    if (lane == 0) { me.cyc_tree += c1 - c0; me.cyc_emit += clock64() - c2; }
+    if (st != ~0u) {
+      if (lane == 0) ctl.state = st;
+      st_rel(ctl.stop, 1u, lane);
+    }
+    st_rel(ctl.next_emit, k + 1, lane);
+    if (st != ~0u) break;
+  }
+}
+
+static constexpr uint32_t TR_DECIDED = 0xfffffffeu;   // parser-side: a flusher decided the trial (MWCtl::state)
+
 template <int KIND, typename SH>
 __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
+  constexpr bool MW = HasMW<SH>::value;
+  const int wave = MW ? (int)(threadIdx.x >> 6) : 0;
   LDS TrialShared& s = *(LDS TrialShared*)&shm.t;
   LDS uint32_t* const stg = (LDS uint32_t*)shm.ring;   // emission staging (overlays the ring)
   const uint32_t t = blockIdx.x;
@@ -1741,10 +1907,12 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   z.match_start = 0; z.prev_match = 0; z.match_length = 2; z.prev_length = 2; z.match_available = 0;
   z.last_lit = 0; z.nsym = 0;
   LDS BitOut& b = s.b;
-  b.out = (GLOBAL uint8_t*)(A.out + tr.out_off); b.cap = tr.out_cap; b.pos = 0; b.bb = 0; b.bc = 0;
-  b.orig = (const GLOBAL uint8_t*)(A.file + sd.orig_off); b.clen = sd.comp_len;
-  b.shortcut = sd.comp_len > A.o.shortcut_len ? A.o.shortcut_len : 0;
-  b.eq_all = 0; b.eq_sc = 0; b.overflow = 0;
+  if (wave == 0) {
+    b.out = (GLOBAL uint8_t*)(A.out + tr.out_off); b.cap = tr.out_cap; b.pos = 0; b.bb = 0; b.bc = 0;
+    b.orig = (const GLOBAL uint8_t*)(A.file + sd.orig_off); b.clen = sd.comp_len;
+    b.shortcut = sd.comp_len > A.o.shortcut_len ? A.o.shortcut_len : 0;
+    b.eq_all = 0; b.eq_sc = 0; b.overflow = 0;
+  }
   // fast and slow levels: a saving trial writes its whole symbol sequence at rp_syms (block k's
   // symbols at sbase, the count of symbols in the blocks before it); a replaying trial reads one
   const bool saving = KIND != 0 && (tr.mode & 4);
@@ -1777,7 +1945,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   // a saving slow trial records the match-table entries its parse reads (rp_tab, cleared first)
   const bool rec = KIND == 2 && saving && (tr.mode & 32);
   GLOBAL uint64_t* const rtab = (GLOBAL uint64_t*)(uintptr_t)tr.rp_tab;
-  if (rec) {
+  if (rec && wave == 0) {
     for (uint32_t p = (uint32_t)lane; p < sd.infl_len; p += 64) rtab[p] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the clears land before the records
   }
@@ -1785,25 +1953,41 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   uint32_t saved_flags = 0;
   uint32_t run_len = 0, run_imp = 0;   // slow parses: longest match length any of its reads saw, longest
                                        // prev_length a lazy read improved (per lane, reduced at the end)
-  b.cyc_tree = b.cyc_emit = b.blocks = 0;
-  b.cyc_heap = b.cyc_scan = b.cyc_send = 0;
+  if (wave == 0) {
+    b.cyc_tree = b.cyc_emit = b.blocks = 0;
+    b.cyc_heap = b.cyc_scan = b.cyc_send = 0;
+  }
   const uint64_t cstart = clock64();
-  for (int i = lane; i < (NLC + 1) / 2; i += 64) s.lfreq2[i] = 0;
-  for (int i = lane; i < NDC / 2; i += 64) s.dfreq2[i] = 0;
-  if (lane == 0) s.lfreq2[128] = 1;   // END_BLOCK
+  if (wave == 0) init_block(s.f, lane);
   uint32_t hazard = 0;
   // Symbols and block statistics are tallied straight into HBM (syms) and LDS (lfreq / dfreq).
   uint32_t state = ~0u;
   uint64_t fallbacks = 0, cyc_fb = 0;
   uint64_t csec[4] = {0, 0, 0, 0};   // diagnostics (ATZ_STEP_CLOCKS)
   // zlib header (Z/deflate.c:738-759)
-  {
+  if (wave == 0) {
     uint32_t header = (8u + ((uint32_t)(tr.window - 8) << 4)) << 8;
     uint32_t lf = z.level < 2 ? 0 : z.level < 6 ? 1 : z.level == 6 ? 2 : 3;
     header |= lf << 6;
     header += 31 - (header % 31);
     put_bits(b, stg, ((header >> 8) & 0xff) | ((header & 0xff) << 8), 16, lane);   // < 32 bits: no staging
   }
+  uint32_t nblk = 0;   // multi-wave: blocks handed to the flushers
+  if constexpr (MW) {
+    LDS MWPart& mw = *(LDS MWPart*)&shm.mw;
+    if (wave == 0) {
+      if (lane < MW_F) { mw.slot[lane].seq = 0; mw.fl[lane].cyc_tree = 0; mw.fl[lane].cyc_emit = 0; }
+      if (lane == 0) {
+        mw.ctl.next_emit = 0; mw.ctl.stop = 0; mw.ctl.parse_done = 0; mw.ctl.nblocks = 0;
+        mw.ctl.state = ~0u; mw.ctl.hazard = 0;
+      }
+    }
+    __syncthreads();
+    if (wave != 0)
+      trial_flusher(A, s, mw, tr, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, z.level, z.lbs, full_needed,
+                    wave - 1, lane);
+  }
+  if (wave == 0) {   // (the parse; every wave of a single-wave trial)
   // fast and slow kinds: match-table entries of the positions around the parse window in an LDS
   // ring; window slides (fill_window at the top of an iteration when lookahead < MIN_LOOKAHEAD)
   // are a function of the iteration position, so any lane can evaluate them.
@@ -1829,6 +2013,32 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   uint32_t hi = 0;
   uint64_t pf = 0;
   if (KIND != 0 && n && !replay) pf = Rt[lane];
+  // multi-wave: hand the finished block to its flusher; false when the trial is already decided
+  auto publish = [&](int last) -> bool {
+    if constexpr (MW) {
+      LDS MWPart& mw = *(LDS MWPart*)&shm.mw;
+      const uint32_t f = nblk % (uint32_t)MW_F;
+      LDS MWSlot& sl = mw.slot[f];
+      for (;;) {
+        if (ld_acq(mw.ctl.stop)) return false;
+        if (ld_acq(sl.seq) == 0) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      for (int i = lane; i < (NLC + 1) / 2; i += 64) sl.f.lfreq2[i] = s.f.lfreq2[i];
+      for (int i = lane; i < NDC / 2; i += 64) sl.f.dfreq2[i] = s.f.dfreq2[i];
+      if (lane == 0) {
+        sl.block_start = (int64_t)z.block_start; sl.p = z.p; sl.S = z.S;
+        sl.last_lit = z.last_lit; sl.sbase = sbase; sl.last = (uint32_t)last;
+      }
+      st_rel(sl.seq, nblk + 1, lane);   // after the wave's symbol stores and the slot writes
+      nblk++;
+      init_block(s.f, lane);
+      sbase += z.last_lit;
+      z.last_lit = 0;
+      z.block_start = z.p;
+    }
+    return true;
+  };
   auto FLUSH = [&](int last) {
     hazard |= uni(flush_block(s, *(LDS TreeScratch*)shm.ring, b, (const GLOBAL uint32_t*)syms + ((saving || replay) ? sbase : 0u),
                               (const GLOBAL uint8_t*)in, (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last,
@@ -1843,6 +2053,15 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       }
     }
   };
+  // a block is full: flush it (single wave) or hand it over (multi-wave); returns the early-exit state
+  auto FLUSH0 = [&]() -> uint32_t {
+    if constexpr (MW) {
+      return publish(0) ? ~0u : TR_DECIDED;
+    } else {
+      FLUSH(0);
+      return uni(early_exit(b, A.o, tr.best_ident, full_needed));
+    }
+  };
   if constexpr (KIND == 0) {
     // deflate_stored (Z/deflate.c:1564-1619)
     uint64_t max_block = 0xffff;
@@ -1855,13 +2074,11 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       if (z.p == 0 || z.p >= max_start) {
         z.lookahead = z.p - max_start;
         z.p = max_start;
-        FLUSH(0);
-        state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+        state = FLUSH0();
         if (state != ~0u) break;
       }
       if (z.p - z.block_start >= z.maxdist) {
-        FLUSH(0);
-        state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+        state = FLUSH0();
         if (state != ~0u) break;
       }
     }
@@ -1902,18 +2119,17 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         if ((uint32_t)lane >= base && (uint32_t)lane < seg_end) {
           if (v >> 8) {
             const uint32_t lc = 257u + len_code(v & 0xffu), dc = dist_code((v >> 8) - 1u);
-            __hip_atomic_fetch_add(&s.lfreq2[lc >> 1], 1u << (16 * (lc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&s.dfreq2[dc >> 1], 1u << (16 * (dc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.f.lfreq2[lc >> 1], 1u << (16 * (lc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.f.dfreq2[dc >> 1], 1u << (16 * (dc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           } else {
-            __hip_atomic_fetch_add(&s.lfreq2[v >> 1], 1u << (16 * (v & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.f.lfreq2[v >> 1], 1u << (16 * (v & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
         }
         z.last_lit += seg_end - base;
         z.nsym += seg_end - base;
         if (z.last_lit == z.lbs - 1u && !(endlit && k + seg_end == nsv)) {
           z.p = pos + (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)seg_end - 1);
-          FLUSH(0);
-          state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+          state = FLUSH0();
           if (state != ~0u) break;
         }
         base = seg_end;
@@ -1979,12 +2195,12 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     // one symbol, tallied by the scalar unit; returns true when the block is full
     auto tally1 = [&](uint32_t v) -> bool {
       if (lane == 0) {
-        syms[(saving ? sbase : 0u) + z.last_lit] = v;
+        syms[(saving || MW ? sbase : 0u) + z.last_lit] = v;
         if (v >> 8) {
-          __hip_atomic_fetch_add(&s.lfreq2[(257u + len_code(v & 0xffu)) >> 1], 1u << (16 * ((257u + len_code(v & 0xffu)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          __hip_atomic_fetch_add(&s.dfreq2[(dist_code((v >> 8) - 1u)) >> 1], 1u << (16 * ((dist_code((v >> 8) - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&s.f.lfreq2[(257u + len_code(v & 0xffu)) >> 1], 1u << (16 * ((257u + len_code(v & 0xffu)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&s.f.dfreq2[(dist_code((v >> 8) - 1u)) >> 1], 1u << (16 * ((dist_code((v >> 8) - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else {
-          __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
       z.last_lit++;
@@ -2122,13 +2338,13 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
               uint32_t v;
               if (wt == 2) {
                 v = (Dx << 8) | (L - 3u);
-                __hip_atomic_fetch_add(&s.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(&s.dfreq2[(dist_code(Dx - 1u)) >> 1], 1u << (16 * ((dist_code(Dx - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&s.f.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&s.f.dfreq2[(dist_code(Dx - 1u)) >> 1], 1u << (16 * ((dist_code(Dx - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
               } else {
                 v = ex & 0xffu;
-                __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
               }
-              syms[(saving ? sbase : 0u) + z.last_lit + (o - base)] = v;
+              syms[(saving || MW ? sbase : 0u) + z.last_lit + (o - base)] = v;
             }
             z.last_lit += seg_end - base;
             if (z.last_lit == z.lbs - 1u) {   // flush after the node tallied last: strstart past its step
@@ -2138,8 +2354,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
               const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)L, ol);
               z.p = fx + (fl ? fl : 1u);
               z.S = S_iter(Sb, fx);
-              FLUSH(0);
-              state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+              state = FLUSH0();
               if (state != ~0u) break;
             }
             base = seg_end;
@@ -2256,8 +2471,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         if (full) {
           z.p = f + step;
           z.S = Sf;
-          FLUSH(0);
-          state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+          state = FLUSH0();
         }
         qnext = f + step;
         restart = true;
@@ -2381,12 +2595,12 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           else v = 0x80000000u | (D << 8) | (L - 3u);
           if (v & 0x80000000u) {
             v &= 0x7fffffffu;
-            __hip_atomic_fetch_add(&s.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&s.dfreq2[(dist_code(D - 1u)) >> 1], 1u << (16 * ((dist_code(D - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.f.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.f.dfreq2[(dist_code(D - 1u)) >> 1], 1u << (16 * ((dist_code(D - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           } else {
-            __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
-          syms[(saving ? sbase : 0u) + z.last_lit + (o + k - base)] = v;
+          syms[(saving || MW ? sbase : 0u) + z.last_lit + (o + k - base)] = v;
         }
         z.last_lit += seg_end - base;
         if (z.last_lit == z.lbs - 1u) {
@@ -2405,8 +2619,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           const int ol = (int)__builtin_ctzll(om);
           z.p = (uint32_t)__builtin_amdgcn_readlane((int)fp, ol);
           z.S = S_iter(Sb, (uint32_t)__builtin_amdgcn_readlane((int)fit, ol));
-          FLUSH(0);
-          state = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+          state = FLUSH0();
           if (state != ~0u) break;
         }
         base = seg_end;
@@ -2424,8 +2637,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
         const uint32_t v = prevb;
         saved_flags |= 2;
         if (lane == 0) {
-          syms[(saving ? sbase : 0u) + z.last_lit] = v;
-          __hip_atomic_fetch_add(&s.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          syms[(saving || MW ? sbase : 0u) + z.last_lit] = v;
+          __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         z.last_lit++;
         z.nsym++;
@@ -2434,7 +2647,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       z.S = S_iter(Sb, n);
     }
   }
-  if (state == ~0u) {
+  if (MW && state == ~0u) {
+    saved_flags |= 1;   // every symbol tallied: a saving trial's sequence is complete
+    if (!publish(1)) state = TR_DECIDED;   // the final gates run on the last block's flusher
+  } else if (state == ~0u) {
     saved_flags |= 1;   // every symbol tallied: a saving trial's sequence is complete
     FLUSH(1);
     // adler32 trailer
@@ -2453,6 +2669,25 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       if (b.shortcut && b.eq_sc < thr) state = TR_SHORTCUT;
       else if (ad2 > A.o.sizediff_tresh) state = TR_SIZEDIFF;
       else state = TR_FULL;
+    }
+  }
+  if constexpr (MW) {   // no more blocks: flushers waiting past the last one stop; TR_NEED_R abandons the rest
+    LDS MWCtl& ctl = (*(LDS MWPart*)&shm.mw).ctl;
+    if (lane == 0) ctl.nblocks = nblk;
+    st_rel(ctl.parse_done, 1u, lane);
+    if (state == TR_NEED_R) st_rel(ctl.stop, 1u, lane);
+  }
+  }   // wave 0
+  if constexpr (MW) {
+    __syncthreads();   // every flusher has stopped
+    if (wave != 0) return;
+    LDS MWPart& mw = *(LDS MWPart*)&shm.mw;
+    const uint32_t cs = uni(mw.ctl.state);
+    // a flusher's decision stands (it is final); TR_NEED_R only when none was reached
+    if (state != TR_NEED_R || cs != ~0u) state = cs;
+    hazard |= uni(mw.ctl.hazard);
+    if (lane == 0) {
+      for (int f = 0; f < MW_F; f++) { b.cyc_tree += mw.fl[f].cyc_tree; b.cyc_emit += mw.fl[f].cyc_emit; }
     }
   }
   uint32_t rmax = (run_imp << 16) | run_len;   // both < 2^16: per-field maxima by two reductions
@@ -2504,6 +2739,16 @@ __global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_fast(SweepArgs A
 __global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_slow(SweepArgs A) {
   __shared__ TrialSharedSlow shm;
   trial_body<2>(A, shm, threadIdx.x);
+}
+// multi-wave trials (small blocks): wave 0 parses, waves 1..MW_F flush
+static constexpr uint32_t MW_THREADS = 64 * (1 + MW_F);
+__global__ __launch_bounds__(MW_THREADS, TRIAL_SLOW_WAVES) void k_trial_fast_mw(SweepArgs A) {
+  __shared__ TrialSharedFastMW shm;
+  trial_body<1>(A, shm, (int)(threadIdx.x & 63));
+}
+__global__ __launch_bounds__(MW_THREADS, TRIAL_SLOW_WAVES) void k_trial_slow_mw(SweepArgs A) {
+  __shared__ TrialSharedSlowMW shm;
+  trial_body<2>(A, shm, (int)(threadIdx.x & 63));
 }
 
 }  // namespace atz
