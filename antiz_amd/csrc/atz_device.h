@@ -112,4 +112,20 @@ struct SweepOpts {
   uint64_t recomp_tresh, sizediff_tresh, shortcut_len, mismatch_tol;
 };
 
+// Inclusive prefix sum over the 64 lanes of a wave (every lane active), on DPP: a Hillis-Steele scan
+// inside each row of 16 lanes (row_shr 1, 2, 4, 8), then the rows' totals carried by row_bcast:15
+// (into rows 1 and 3) and row_bcast:31 (into rows 2 and 3).  Six VALU adds; no LDS-crossbar
+// permutes, unlike a __shfl_up ladder.  A lane whose DPP source is outside its row (or whose row is
+// masked off) adds the `old` operand, 0.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);   // row_bcast:15, rows 1 and 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);   // row_bcast:31, rows 2 and 3
+  return (uint32_t)x;
+}
+
 }  // namespace atz

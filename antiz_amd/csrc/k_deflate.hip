@@ -1388,29 +1388,6 @@ __device__ __forceinline__ void stage_or(LDS uint32_t* stage, uint32_t off, uint
   if ((uint32_t)(lo >> 32)) __atomic_fetch_or(&stage[wi + 1], (uint32_t)(lo >> 32), __ATOMIC_RELAXED);
   if (hi) __atomic_fetch_or(&stage[wi + 2], hi, __ATOMIC_RELAXED);
 }
-// Appends one bit string per lane (v, nb bits; lane order) to the output: bit offsets by a wave
-// prefix sum, words assembled in the staging buffer with LDS atomics (as in compress_block).
-__device__ __forceinline__ void emit_lane_bits(LDS BitOut& b, LDS uint32_t* stage, uint64_t v, uint32_t nb, int lane) {
-  uint32_t incl = nb;
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += t;
-  }
-  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  if (total == 0) return;
-  for (int i = lane; i < (int)STAGE_WORDS; i += 64) stage[i] = 0;
-  const uint32_t bc = uni(b.bc);
-  if (lane == 0) { stage[0] = (uint32_t)b.bb; stage[1] = (uint32_t)(b.bb >> 32); }
-  stage_or(stage, bc + incl - nb, v, nb);
-  const uint32_t all = bc + total;
-  const uint32_t full = all >> 3;
-  emit_bytes_from_stage(b, stage, full, lane);
-  const uint32_t rem = all & 7;
-  const uint32_t lastw = stage[full >> 2];
-  b.bb = rem ? ((lastw >> (8 * (full & 3))) & 0xff) & ((1u << rem) - 1) : 0;
-  b.bc = rem;
-}
-
 // scan_tree / send_tree (Z/trees.c:705-799), lane-parallel.  zlib walks the code lengths
 // ln[0..max_code] once, cutting each run of equal lengths into chunks; the cut points depend only
 // on the run: a run of v != 0 is cut after 7, then every 6 elements (max_count 7, then 6 while the
@@ -1419,8 +1396,10 @@ __device__ __forceinline__ void emit_lane_bits(LDS BitOut& b, LDS uint32_t* stag
 // (v only in the run's first chunk, where prevlen != v), REPZ_3_10+3 or REPZ_11_138+7.  So every
 // element finds its run (ballot masks of run starts; max_code + 1 is zlib's guard) and a chunk's
 // first element contributes the chunk: send = its bits in element order, else its bl_tree counts.
-__device__ void rle_tree(LDS BitOut& b, LDS TreeCodes& s, LDS uint32_t* stage, const LDS uint8_t* ln, int max_code, bool send,
-                         int lane) {
+// send: the chunks' bits go into the staging words at bit offset `off` on (in element order); returns
+// the offset after them.
+__device__ uint32_t rle_tree(LDS TreeCodes& s, LDS uint32_t* stage, const LDS uint8_t* ln, int max_code, bool send,
+                             uint32_t off, int lane) {
   const int N = max_code + 1;   // elements; position N acts as a run start (the guard)
   const int G = N / 64 + 1;     // groups covering 0..N (N <= 286: at most 5)
   uint64_t M[5];
@@ -1490,8 +1469,13 @@ __device__ void rle_tree(LDS BitOut& b, LDS TreeCodes& s, LDS uint32_t* stage, c
         }
       }
     }
-    if (send) emit_lane_bits(b, stage, v64, nb, lane);
+    if (send) {
+      const uint32_t incl = wave_incl_scan(nb);
+      stage_or(stage, off + incl - nb, v64, nb);
+      off += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
   }
+  return off;
 }
 
 // The trial's outcome gates (early_exit) are monotone in the output emitted so far, so they are
@@ -1514,11 +1498,7 @@ __device__ bool compress_block(LDS BitOut& b, LDS uint32_t* stage, const GLOBAL 
     sym_bits((uint32_t)(sp >> 32), k0 + 1 < nsym, k0 + 1 == nsym, lc, ll, dc, dl, v1, n1);
     const uint32_t nb = n0 + n1;
     // exclusive prefix sum of bit lengths
-    uint32_t incl = nb;
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t t = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += t;
-    }
+    const uint32_t incl = wave_incl_scan(nb);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (total == 0) break;
     // stage words: word 0..1 seeded with the pending bits
@@ -1627,8 +1607,8 @@ __device__ __noinline__ BlockPlan block_trees(const LDS BlockFreq& f, LDS TreeCo
     // bit length tree
     for (int i = lane; i < NBLC; i += 64) s.bfreq[i] = 0;
     const uint64_t cs0 = STEP_CLOCK();
-    rle_tree(b, s, nullptr, s.llen, pl.lmax, false, lane);
-    rle_tree(b, s, nullptr, s.dlen, pl.dmax, false, lane);
+    rle_tree(s, nullptr, s.llen, pl.lmax, false, 0, lane);
+    rle_tree(s, nullptr, s.dlen, pl.dmax, false, 0, lane);
     b.cyc_scan += STEP_CLOCK() - cs0;
     for (int i = lane; i < NBLC; i += 64) sc.freq[i] = (uint16_t)s.bfreq[i];
     r = build_tree(s.w, sc, s.blen, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, b.cyc_heap, lane);
@@ -1701,22 +1681,42 @@ __device__ __noinline__ uint32_t block_emit(LDS TreeCodes& s, LDS uint32_t* stag
       if (!full_needed && early_exit(b, opt, best_ident, false) != ~0u) break;
     }
   } else if (static_lenb == opt_lenb) {
-    put_bits(b, stage, (1u << 1) + (uint32_t)last, 3, lane);
+    // the 3 header bits join the pending bits (fewer than 32 at a block start): compress_block writes them
+    const uint32_t bc0 = uni(b.bc);
+    b.bb = uni(b.bb) | ((uint64_t)((1u << 1) + (uint32_t)last) << bc0);
+    b.bc = bc0 + 3;
     compress_block(b, stage, syms, last_lit, (const CONSTANT uint16_t*)c_t.st_lcode, (const CONSTANT uint8_t*)c_t.st_llen,
                    (const CONSTANT uint16_t*)c_t.st_dcode, (const CONSTANT uint8_t*)c_t.st_dlen, opt, best_ident,
                    full_needed, lane);
   } else {
     int lcodes = lmax + 1, dcodes = dmax + 1, blcodes = max_blindex + 1;
-    put_bits(b, stage, (2u << 1) + (uint32_t)last, 3, lane);
-    put_bits(b, stage, (uint32_t)(lcodes - 257), 5, lane);
-    put_bits(b, stage, (uint32_t)(dcodes - 1), 5, lane);
-    put_bits(b, stage, (uint32_t)(blcodes - 4), 4, lane);
-    for (int r = 0; r < blcodes; r++) put_bits(b, stage, s.blen[bl_order((uint32_t)r)], 3, lane);
+    // The whole block header -- BTYPE, HLIT / HDIST / HCLEN, the bit-length codes' lengths and the
+    // run-length coded literal and distance code lengths (send_all_trees, Z/trees.c:836-860) -- is
+    // assembled in the staging words behind the pending bits (fewer than 32 at a block start; at most
+    // ~4.6 kbit in all) and written and compared in one pass.
     const uint64_t cs0 = STEP_CLOCK();
-    rle_tree(b, s, stage, s.llen, lcodes - 1, true, lane);
-    rle_tree(b, s, stage, s.dlen, dcodes - 1, true, lane);
+    for (int i = lane; i < (int)STAGE_WORDS; i += 64) stage[i] = 0;
+    const uint32_t bc0 = uni(b.bc);
+    const uint64_t bb0 = uni(b.bb);
+    if (lane == 0) { stage[0] = (uint32_t)bb0; stage[1] = (uint32_t)(bb0 >> 32); }
+    uint32_t off = bc0;
+    if (lane == 0)
+      stage_or(stage, off, (uint64_t)((2u << 1) + (uint32_t)last) | ((uint64_t)(lcodes - 257) << 3) |
+                               ((uint64_t)(dcodes - 1) << 8) | ((uint64_t)(blcodes - 4) << 13), 17);
+    off += 17;
+    if (lane < blcodes) stage_or(stage, off + 3u * (uint32_t)lane, s.blen[bl_order((uint32_t)lane)], 3);
+    off += 3u * (uint32_t)blcodes;
+    off = rle_tree(s, stage, s.llen, lcodes - 1, true, off, lane);
+    off = rle_tree(s, stage, s.dlen, dcodes - 1, true, off, lane);
+    {
+      const uint32_t full = off >> 3;
+      emit_bytes_from_stage(b, stage, full, lane);
+      const uint32_t rem = off & 7;
+      const uint32_t lastw = stage[full >> 2];
+      b.bb = rem ? ((lastw >> (8 * (full & 3))) & 0xff) & ((1u << rem) - 1) : 0;
+      b.bc = rem;
+    }
     b.cyc_send += STEP_CLOCK() - cs0;
-    flush_bits_bytes(b, stage, lane);
     compress_block(b, stage, syms, last_lit, (const LDS uint16_t*)s.lcode, (const LDS uint8_t*)s.llen,
                    (const LDS uint16_t*)s.dcode, (const LDS uint8_t*)s.dlen, opt, best_ident, full_needed, lane);
   }
@@ -2105,11 +2105,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
       const bool valid = (uint32_t)lane < cnt;
       const uint32_t v = valid ? sv[k + (uint32_t)lane] : 0u;
       const uint32_t len = valid ? ((v >> 8) ? (v & 0xffu) + 3u : 1u) : 0u;
-      uint32_t incl = len;
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t2 = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += t2;
-      }
+      const uint32_t incl = wave_incl_scan(len);
       const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       if (xlim < n && pos + tot + 2u > xlim) { state = TR_NEED_R; z.p = pos; break; }
       uint32_t base = 0;
