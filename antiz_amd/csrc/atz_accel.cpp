@@ -1125,7 +1125,7 @@ static bool bucket_verify() {   // ATZ_BUCKETS_VERIFY=1 (read per call): check k
   const char* e = std::getenv("ATZ_BUCKETS_VERIFY");
   return e && std::atoi(e) != 0;
 }
-static constexpr uint32_t BSORT_MAX_NPAD = std::min<uint32_t>(65472u, ((160u * 1024u - 256u - BSORT_CNT_BYTES) / BSORT_BYTES_PER_POS) & ~63u);   // LDS limit (256 B static)
+static constexpr uint32_t BSORT_MAX_NPAD = std::min<uint32_t>(65472u, ((160u * 1024u - 256u - BSORT_CNT_BYTES) / 2u) & ~63u);   // LDS limit (256 B static)
 static_assert(bsort_lds_bytes(BSORT_MAX_NPAD) + 256u <= 160u * 1024u && BSORT_MAX_NPAD < 65536u, "k_buckets_sort LDS class");
 static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need, ChainBufs& B);
 // Builds the missing tables of `need` on the pipe's stream.
@@ -1210,8 +1210,12 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
       for (int k = 0; k < NC; k++) {
         const size_t cnt = beg[k + 1] - beg[k];
         if (!cnt) continue;
+        // a wave keeps its tile in registers: bsort_chunks(class) batches of 64 positions
+        static_assert(bsort_chunks(4096) == 4 && bsort_chunks(20480) == 20 && bsort_chunks(BSORT_MAX_NPAD) == 64, "classes");
+        auto kern = k == 0 ? k_buckets_sort<4> : k == 1 ? k_buckets_sort<8> : k == 2 ? k_buckets_sort<12>
+                  : k == 3 ? k_buckets_sort<16> : k == 4 ? k_buckets_sort<20> : k_buckets_sort<64>;
         kbeg(c, 2);
-        hipLaunchKernelGGL(k_buckets_sort, dim3((uint32_t)cnt), dim3(BSORT_THREADS), bsort_lds_bytes(cls[k]), c->st,
+        hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(BSORT_THREADS), bsort_lds_bytes(cls[k]), c->st,
                            INFL_BASE, B.d_cjobs2.as<ChainJob>() + beg[k], chains,
                            (uint32_t)cnt, depth);
         kend(c);
@@ -1348,12 +1352,23 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
       const uint64_t npad = (alt[k].n + 63) & ~63ull, nh = alt[k].n >= 3 ? alt[k].n - 2 : 0;
       const uint32_t* a = h1.data() + alt[k].chain_off;
       const uint32_t* b2 = h2.data() + alt[k].chain_off;
-      for (uint64_t i = 0; i < nh; i++)
+      uint64_t start = 0, deepest = 0;
+      for (uint64_t i = 0; i < nh; i++) {
         if (a[i] != b2[i] || a[npad + i] != b2[npad + i]) {
           std::fprintf(stderr, "atz: bucket mismatch: job %zu n %llu m %u at %llu\n", k, (unsigned long long)alt[k].n,
                        alt[k].memlevel, (unsigned long long)i);
           return ATZ_E_INTERNAL;
         }
+        if (b2[npad + i] & BUCKET_FIRST) start = i;
+        deepest = std::max(deepest, i - start);
+      }
+      const uint32_t dsort = x->depth_pin.p ? x->depth_pin.as<uint32_t>()[jobs[k].dslot] : 0u;
+      // the deepest bucket k_buckets_sort reported (symbol replay's test; ~0: a job past its LDS limit)
+      if (x->depth_pin.p && nh && dsort != ~0u && dsort != deepest) {
+        std::fprintf(stderr, "atz: deepest bucket mismatch: job %zu n %llu m %u: %u vs %llu\n", k,
+                     (unsigned long long)alt[k].n, alt[k].memlevel, dsort, (unsigned long long)deepest);
+        return ATZ_E_INTERNAL;
+      }
     }
   }
   return 0;
@@ -2517,6 +2532,10 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
     if (len[s] >= (1ull << 31)) return ATZ_E_ARG;   // trial kernels keep 32-bit positions
     c->recs[s].infl_len = len[s];
   }
+  // k_buckets_sort reports each (stream, memLevel)'s deepest bucket at 10 s + m: sized for these streams
+  // (a buffer left by an earlier call on fewer streams would be overrun)
+  if (int r = c->depth_pin.reserve(n * 40 + 64)) return r;
+  std::memset(c->depth_pin.p, 0xff, n * 40);
   if (!adl.empty()) {
     c->adler = adl;
     if (int r = upload(c, c->d_adler, c->adler.data(), n * 4)) return r;

@@ -375,29 +375,26 @@ __global__ __launch_bounds__(256) void k_buckets_pk(const uint8_t* __restrict__ 
   }
 }
 
-// k_buckets_sort: the same bucket arrays by a stable LSD radix sort of the positions by hash, all of
-// it in LDS and on every wave of the block (the kernels above assign positions in order on one
-// wave, which left a 128 KiB-LDS block's CU mostly idle).  Positions are sorted as u16 by their
-// hash (H[p], kept in LDS): one pass per <= 8-bit digit (hash_bits = memLevel + 7: one pass for
-// memLevel 1, two above), each pass a stable counting sort -- every wave owns a contiguous tile of
-// the input order and counts its digits per batch of 64 (lanes sharing a digit found with one
-// ballot per digit bit), an exclusive scan over (digit, wave) gives each wave's output ranges in
-// digit-major, wave-minor order, and the waves scatter their tiles in order.  A final sweep over
-// the sorted order writes bpos (first entry of a hash flagged BUCKET_FIRST) and sidx.  The result
-// is the unique (hash, position) order, so it is identical to the other kernels' output.
-// LDS: 2 (ATZ_BSORT_GLOBAL) or 6 bytes per position + 2 bytes per (digit, wave); streams of < 64 Ki positions.
-// ATZ_BSORT_GLOBAL=1 (default): only the hashes stay in LDS (2 bytes per position); the first pass
-// scatters into the sidx array (overwritten at the end) and the second straight into bpos, both in
-// HBM (L2-resident: 8 bytes per position), so two blocks fit a CU and a sort leaves LDS for the trial
-// blocks of the other pipes.  C4 A/B (2 runs each, one box): k_chains 338-362 -> 262-298 ms summed,
-// 1076-1116 -> 1105-1133 MB/s.  0: positions in LDS too (6 bytes per position, one block per CU).
-#ifndef ATZ_BSORT_GLOBAL
-#define ATZ_BSORT_GLOBAL 1
-#endif
+// k_buckets_sort: the same bucket arrays by a stable LSD radix sort of the positions by hash, on every
+// wave of the block (the kernels above assign positions in order on one wave, which left a 128 KiB-LDS
+// block's CU mostly idle).  One pass per <= 8-bit digit (hash_bits = memLevel + 7: one pass for
+// memLevel 1, two above), each pass a stable counting sort: every wave owns a contiguous tile of the
+// current order and holds it in registers as (hash << 16 | position), 64 positions per VGPR; it counts
+// its digits per batch of 64 (lanes sharing a digit found with one ballot per digit bit), an exclusive
+// scan over (digit, wave) gives each wave's output ranges in digit-major, wave-minor order, and the
+// waves scatter their tiles' positions into one u16 array in LDS.  Before the next pass every wave
+// reloads its tile of that array (re-reading each position's 3 input bytes for its hash), so the
+// scatter can overwrite it.  The sorted tile then writes bpos (first entry of a hash flagged
+// BUCKET_FIRST) and scatters the inverse permutation into the same LDS array, which is copied out as
+// sidx.  So HBM sees exactly one coalesced write of bpos and one of sidx (8 bytes per position); an
+// earlier version scattered both arrays through HBM/L2 and wrote 2.8 GB per launch.  The result is the
+// unique (hash, position) order, identical to the other kernels' output.
+// LDS: 2 bytes per position + 2 bytes per (digit, wave); streams of < 64 Ki positions.  MAXC: batches
+// of 64 positions per wave (the tile a wave keeps in registers), from the host's size class.
 static constexpr uint32_t BSORT_THREADS = 1024, BSORT_W = BSORT_THREADS / 64;
 static constexpr uint32_t BSORT_CNT_BYTES = 256 * BSORT_W * 2;
-static constexpr uint32_t BSORT_BYTES_PER_POS = ATZ_BSORT_GLOBAL ? 2 : 6;
-__host__ __device__ constexpr uint32_t bsort_lds_bytes(uint32_t npad) { return BSORT_BYTES_PER_POS * npad + BSORT_CNT_BYTES; }
+__host__ __device__ constexpr uint32_t bsort_lds_bytes(uint32_t npad) { return 2 * npad + BSORT_CNT_BYTES; }
+__host__ __device__ constexpr uint32_t bsort_chunks(uint32_t npad) { return (npad + BSORT_THREADS - 1) / BSORT_THREADS; }
 // lanes of the wave (among `valid` ones) whose `bits`-bit digit equals this lane's
 __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, uint32_t bits) {
   uint64_t m = __ballot(valid);
@@ -408,15 +405,20 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, uint32_t
   }
   return m;
 }
-__global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* __restrict__ infl,
-                                                              const ChainJob* __restrict__ jobs,
-                                                              uint32_t* __restrict__ chains, uint32_t njobs,
-                                                              uint32_t* __restrict__ depth_out) {
+__device__ __forceinline__ uint32_t bhash(const uint8_t* in, uint32_t p, uint32_t hs, uint32_t hm) {
+  return ((((uint32_t)in[p] << (2 * hs)) ^ ((uint32_t)in[p + 1] << hs) ^ in[p + 2]) & hm);
+}
+template <uint32_t MAXC>
+__global__ __launch_bounds__(BSORT_THREADS, MAXC <= 20 ? 8 : 4) void k_buckets_sort(
+    const uint8_t* __restrict__ infl, const ChainJob* __restrict__ jobs, uint32_t* __restrict__ chains,
+    uint32_t njobs, uint32_t* __restrict__ depth_out) {
   extern __shared__ uint32_t dyn_lds[];
   __shared__ uint32_t wtot[BSORT_W];
+  __shared__ uint32_t dmax;
   const uint32_t j = blockIdx.x;
   if (j >= njobs) return;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: the tile loops branch on scalars
   const ChainJob jb = jobs[j];
   const uint8_t* in = infl + jb.infl_off;
   const uint32_t n = (uint32_t)jb.n;
@@ -425,31 +427,50 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
   uint32_t* bpos = sidx + npad;
   const uint32_t hbits = jb.memlevel + 7, hmask = (1u << hbits) - 1, hshift = (hbits + 2) / 3;
   const uint32_t nh = n >= 3 ? n - 2 : 0;
-  LDS uint16_t* H = (LDS uint16_t*)dyn_lds;   // hash of position p
-#if ATZ_BSORT_GLOBAL
-  LDS uint16_t* cnt = H + npad;               // [digit * BSORT_W + wave]: count, then output offset
-#else
-  LDS uint16_t* A = H + npad;                 // positions after the low-digit pass
-  LDS uint16_t* Bo = A + npad;                // positions in (hash, position) order
-  LDS uint16_t* cnt = Bo + npad;              // [digit * BSORT_W + wave]: count, then output offset
-#endif
-  for (uint32_t p = tid; p < nh; p += BSORT_THREADS)
-    H[p] = (uint16_t)((((uint32_t)in[p] << (2 * hshift)) ^ ((uint32_t)in[p + 1] << hshift) ^ in[p + 2]) & hmask);
+  LDS uint16_t* Y = (LDS uint16_t*)dyn_lds;   // positions in the current order; at the end sidx
+  LDS uint16_t* cnt = Y + npad;               // [digit * BSORT_W + wave]: count, then output offset
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  const uint32_t T = ((nh + BSORT_W - 1) / BSORT_W + 63) & ~63u;   // input tile of a wave
+  const uint32_t T = ((nh + BSORT_W - 1) / BSORT_W + 63) & ~63u;   // tile of a wave (<= 64 * MAXC)
   const uint32_t t0 = (uint32_t)wave * T < nh ? (uint32_t)wave * T : nh;
   const uint32_t t1 = t0 + T < nh ? t0 + T : nh;
-  // one stable counting-sort pass: digit (H[p] >> shift) & (2^bits - 1) of p = src ? src[i] : i
-  auto pass = [&](auto src, auto dst, uint32_t shift, uint32_t bits) {
+  // The tile: hash << 16 | position per batch, or (MAXC > 16, the larger classes) two positions per
+  // register with the hashes re-read from the input when needed.  The batch loops stay rolled: the
+  // tile is indexed in registers (s_set_gpr_idx); unrolled, the compiler interleaved the batches and
+  // spilled.
+  constexpr bool PK = MAXC > 16;
+  uint32_t v[PK ? (MAXC + 1) / 2 : MAXC];
+  auto setv = [&](uint32_t c, uint32_t h, uint32_t p) {
+    if constexpr (PK) { if (c & 1) v[c >> 1] |= p << 16; else v[c >> 1] = p; } else v[c] = (h << 16) | p;
+  };
+  auto posv = [&](uint32_t c) -> uint32_t { return PK ? (v[c >> 1] >> (16 * (c & 1))) & 0xffffu : v[c] & 0xffffu; };
+  auto hashv = [&](uint32_t c) -> uint32_t { return PK ? bhash(in, posv(c), hshift, hmask) : v[c] >> 16; };
+  // the tile in input order, or (reload) the wave's tile of the order in Y; every batch is assigned
+#pragma unroll 1
+  for (uint32_t c = 0; c < MAXC; c++) {
+    const uint32_t i = t0 + 64 * c + (uint32_t)lane;
+    setv(c, PK || i >= t1 ? 0u : bhash(in, i, hshift, hmask), i < t1 ? i : 0u);
+  }
+  auto reload = [&]() {
+    __syncthreads();   // Y complete
+#pragma unroll 1
+    for (uint32_t c = 0; c < MAXC; c++) {
+      const uint32_t i = t0 + 64 * c + (uint32_t)lane;
+      const uint32_t p = i < t1 ? (uint32_t)Y[i] : 0u;
+      setv(c, PK || i >= t1 ? 0u : bhash(in, p, hshift, hmask), p);
+    }
+  };
+  // one stable counting-sort pass on digit (hash >> shift) & (2^bits - 1): tile -> Y
+  auto pass = [&](uint32_t shift, uint32_t bits) {
     const uint32_t dmask = (1u << bits) - 1;
-    __syncthreads();   // H / the previous pass's dst written, its scatter done with cnt
+    __syncthreads();   // every wave holds its tile (Y may be overwritten), cnt free
     for (uint32_t i = tid; i < 256 * BSORT_W; i += BSORT_THREADS) cnt[i] = 0;
     __syncthreads();
-    for (uint32_t i0 = t0; i0 < t1; i0 += 64) {
-      const uint32_t i = i0 + (uint32_t)lane;
+#pragma unroll 1
+    for (uint32_t c = 0; c < MAXC; c++) {
+      if (t0 + 64 * c >= t1) break;
+      const uint32_t i = t0 + 64 * c + (uint32_t)lane;
       const bool valid = i < t1;
-      const uint32_t p = valid ? (src ? (uint32_t)src[i] : i) : 0u;
-      const uint32_t d = valid ? ((uint32_t)H[p] >> shift) & dmask : 0u;
+      const uint32_t d = (hashv(c) >> shift) & dmask;
       const uint64_t pm = digit_peers(d, valid, bits);
       if (valid && (pm & lt) == 0) cnt[d * BSORT_W + wave] += (uint16_t)__popcll(pm);
     }
@@ -459,73 +480,59 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
     uint32_t c4[4], s = 0;
 #pragma unroll
     for (int u = 0; u < 4; u++) { c4[u] = cnt[b4 + u]; s += c4[u]; }
-    uint32_t incl = s;
-    for (int dd = 1; dd < 64; dd <<= 1) {
-      const uint32_t t = __shfl_up(incl, dd, 64);
-      if (lane >= dd) incl += t;
-    }
+    const uint32_t incl = wave_incl_scan(s);
     if (lane == 63) wtot[wave] = incl;
     __syncthreads();
-    uint32_t off = 0;
-    for (int w = 0; w < wave; w++) off += wtot[w];
+    // the totals of the waves before this one, lane-parallel
+    const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(lane < wave ? wtot[lane] : 0u), 63);
     uint32_t e = off + incl - s;
 #pragma unroll
     for (int u = 0; u < 4; u++) { cnt[b4 + u] = (uint16_t)e; e += c4[u]; }
     __syncthreads();
-    for (uint32_t i0 = t0; i0 < t1; i0 += 64) {
-      const uint32_t i = i0 + (uint32_t)lane;
+#pragma unroll 1
+    for (uint32_t c = 0; c < MAXC; c++) {
+      if (t0 + 64 * c >= t1) break;
+      const uint32_t i = t0 + 64 * c + (uint32_t)lane;
       const bool valid = i < t1;
-      const uint32_t p = valid ? (src ? (uint32_t)src[i] : i) : 0u;
-      const uint32_t d = valid ? ((uint32_t)H[p] >> shift) & dmask : 0u;
+      const uint32_t d = (hashv(c) >> shift) & dmask;
       const uint64_t pm = digit_peers(d, valid, bits);
       const uint32_t base = valid ? (uint32_t)cnt[d * BSORT_W + wave] : 0u;
       if (valid) {
-        dst[base + (uint32_t)__popcll(pm & lt)] = p;
+        Y[base + (uint32_t)__popcll(pm & lt)] = (uint16_t)posv(c);
         if ((pm & lt) == 0) cnt[d * BSORT_W + wave] = (uint16_t)(base + (uint32_t)__popcll(pm));
       }
     }
   };
   static_assert(256 * BSORT_W == 4 * BSORT_THREADS, "the scan takes 4 counters per thread");
-#if ATZ_BSORT_GLOBAL
   if (hbits <= 8) {
-    pass((const uint32_t*)nullptr, bpos, 0, hbits);
+    pass(0, hbits);
   } else {
-    pass((const uint32_t*)nullptr, sidx, 0, hbits - 8);
-    pass((const uint32_t*)sidx, bpos, hbits - 8, 8);
+    pass(0, hbits - 8);
+    reload();
+    pass(hbits - 8, 8);
   }
-#else
-  if (hbits <= 8) {
-    pass((const LDS uint16_t*)nullptr, Bo, 0, hbits);
-  } else {
-    pass((const LDS uint16_t*)nullptr, A, 0, hbits - 8);
-    pass((const LDS uint16_t*)A, Bo, hbits - 8, 8);
-  }
-#endif
-  __syncthreads();
-  // per wave, its contiguous tile [t0, t1) of the sorted order: bucket starts by ballot, and (when
-  // asked) the deepest bucket, as the largest distance from an element back to its bucket's start
-  // (carried across chunks and, after one barrier, across the waves' tiles)
-  __shared__ uint32_t dmax;
+  reload();
+  // per wave, its contiguous tile [t0, t1) of the sorted order: bucket starts from the neighbour's hash,
+  // and (when asked) the deepest bucket, as the largest distance from an element back to its bucket's
+  // start (carried across batches and, after one barrier, across the waves' tiles)
   uint32_t* const last_start = wtot;   // free after the last pass's scan
   if (tid == 0) dmax = 0;
-  uint32_t carry = 0, mine = 0;   // start of the bucket open at the tile's current chunk (0: before the tile)
+  uint32_t carry = 0, mine = 0;   // start of the bucket open at the tile's current batch (0: before the tile)
   bool before = true;              // no start seen yet in this tile
   uint32_t lead = 0;               // elements of the tile before its first start (belong to an earlier bucket)
-  for (uint32_t i0 = t0; i0 < t1; i0 += 64) {
+  uint32_t hprev = t0 > 0 && t0 < t1 ? bhash(in, (uint32_t)Y[t0 - 1], hshift, hmask) : ~0u;   // element t0 - 1
+#pragma unroll 1
+  for (uint32_t c = 0; c < MAXC; c++) {
+    if (t0 + 64 * c >= t1) break;
+    const uint32_t i0 = t0 + 64 * c;
     const uint32_t i = i0 + (uint32_t)lane;
     const bool valid = i < t1;
-#if ATZ_BSORT_GLOBAL
-    // bpos[i - 1] may already carry its flag (written by the lane or wave that owns it)
-    const uint32_t p = valid ? bpos[i] & ~BUCKET_FIRST : 0u;
-    const bool first = valid && (i == 0 || H[bpos[i - 1] & ~BUCKET_FIRST] != H[p]);
-#else
-    const uint32_t p = valid ? (uint32_t)Bo[i] : 0u;
-    const bool first = valid && (i == 0 || H[Bo[i - 1]] != H[p]);
-#endif
-    if (valid) {
-      bpos[i] = p | (first ? BUCKET_FIRST : 0u);
-      sidx[p] = i;
-    }
+    const uint32_t h = hashv(c);
+    const uint32_t up = (uint32_t)__shfl_up((int)h, 1, 64);
+    const uint32_t hp = lane ? up : hprev;
+    hprev = (uint32_t)__builtin_amdgcn_readlane((int)h, 63);
+    const bool first = valid && (i == 0 || hp != h);
+    if (valid) bpos[i] = posv(c) | (first ? BUCKET_FIRST : 0u);
     if (depth_out) {
       const uint64_t fm = __ballot(first);
       const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
@@ -536,9 +543,16 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
       if (fm) { carry = i0 + 63u - (uint32_t)__builtin_clzll(fm); before = false; }
     }
   }
+  if (depth_out && lane == 0) last_start[wave] = before ? ~0u : carry;
+  __syncthreads();   // every tile read from Y; last_start complete
+  // inverse permutation through Y: Y[p] = p's index in bpos
+#pragma unroll 1
+  for (uint32_t c = 0; c < MAXC; c++) {
+    if (t0 + 64 * c >= t1) break;
+    const uint32_t i = t0 + 64 * c + (uint32_t)lane;
+    if (i < t1) Y[posv(c)] = (uint16_t)i;
+  }
   if (depth_out) {
-    if (lane == 0) last_start[wave] = before ? ~0u : carry;
-    __syncthreads();
     // the tile's leading elements continue the last bucket started in an earlier tile
     uint32_t prev = ~0u;
     for (int w = wave - 1; w >= 0 && prev == ~0u; w--) prev = last_start[w];
@@ -547,9 +561,10 @@ __global__ __launch_bounds__(BSORT_THREADS) void k_buckets_sort(const uint8_t* _
     lm = lm > mine ? lm : mine;
     for (int d = 32; d >= 1; d >>= 1) { const uint32_t o = __shfl_xor(lm, d, 64); lm = lm > o ? lm : o; }
     if (lane == 0 && lm) atomicMax(&dmax, lm);
-    __syncthreads();
-    if (tid == 0) depth_out[jb.dslot] = dmax;
   }
+  __syncthreads();
+  for (uint32_t q = tid; q < nh; q += BSORT_THREADS) sidx[q] = Y[q];
+  if (depth_out && tid == 0) depth_out[jb.dslot] = dmax;
 }
 
 // k_bucket_depth: only the deepest bucket of a (stream, memLevel) (size - 1, as k_buckets_sort

@@ -242,7 +242,8 @@ def test_far_history_and_ring_retry(atz):
 
 def test_bucket_sort_matches_inorder_kernels(atz):
     """k_buckets_sort (LDS radix sort of the positions by hash) against the in-order bucket kernels,
-    array for array (ATZ_BUCKETS_VERIFY=1 rebuilds every job both ways and fails on any difference),
+    array for array and the deepest bucket it reports (ATZ_BUCKETS_VERIFY=1 rebuilds every job both ways
+    and fails on any difference),
     over every memLevel and stream sizes from empty to past the sort's LDS limit; the deflates must
     still equal the oracle's."""
     from antiz_amd import datagen
@@ -250,7 +251,8 @@ def test_bucket_sort_matches_inorder_kernels(atz):
     r = random.Random(5)
     buf = bytearray()
     items = []
-    sizes = [0, 1, 2, 3, 4, 63, 64, 65, 1000, 4094, 4096, 4097, 8191, 12289, 16384, 20481, 25900, 25999, 30000, 70000]
+    sizes = [0, 1, 2, 3, 4, 63, 64, 65, 1000, 4094, 4096, 4097, 8191, 12289, 16384, 20481, 25900, 25999, 30000,
+             40000, 65400, 70000]
     for k, n in enumerate(sizes * 2):
         kind = k % 3
         if kind == 0:
