@@ -1684,7 +1684,9 @@ static void level_dups(atz_ctx* x, std::vector<StreamState>& ss, std::vector<Tri
     if (t.clevel < 7 || t.clevel > 9 || (t.mode & 1)) continue;
     const StreamState& st = ss[t.stream];
     for (const auto& r : st.xl) {
-      if (r[0] != t.window || r[1] != t.memlevel || r[2] == t.clevel) continue;
+      // only a twin at a higher level: its lazy/nice bounds (main.cpp:739-745 lists levels descending)
+      // are at least this level's, so it made every read this level would; r[2] < L proves nothing
+      if (r[0] != t.window || r[1] != t.memlevel || r[2] <= t.clevel) continue;
       if (r[3] < lazy_host(t.clevel) && r[4] < nice_host(t.clevel) && budget_free(x, 2, t)) t.mode |= 128;
       break;
     }
