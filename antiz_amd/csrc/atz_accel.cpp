@@ -632,6 +632,16 @@ static int run_inflate_jobs(atz_ctx* c, const uint8_t* d_in, uint8_t* d_out, con
     for (uint32_t k = 0; k < n; k++) nf += res[k].nfar, cfar += res[k].cyc_far;
     std::fprintf(stderr, "atz: k_inflate far matches (source beyond the LDS ring): %llu, %.3f Gcyc\n",
                  (unsigned long long)nf, cfar / 1e9);
+    {
+      uint64_t nb = 0, ch = 0, nlg = 0, nbs = 0, chs = 0;
+      for (uint32_t k = 0; k < n; k++) {
+        nb += res[k].nblk; ch += res[k].cyc_hdr; nlg += res[k].nlong;
+        if (res[k].status == INF_END && res[k].consumed > 16) { nbs += res[k].nblk; chs += res[k].cyc_hdr; }
+      }
+      std::fprintf(stderr, "atz: k_inflate blocks %llu (streams: %llu), header+build %.3f Gcyc (streams: %.3f), "
+                   "codes > 6 bits in the fast loop %llu\n", (unsigned long long)nb, (unsigned long long)nbs, ch / 1e9,
+                   chs / 1e9, (unsigned long long)nlg);
+    }
     for (uint32_t k = 0; k < n; k++) {
       if (res[k].status == INF_END && res[k].consumed > 16) { ce += res[k].cyc; ne++; continue; }
       const int b = res[k].produced < 64 ? 0 : res[k].produced < 1024 ? 1 : res[k].produced < 4096 ? 2 : 3;

@@ -34,6 +34,7 @@ struct InfRes {
   uint64_t cyc, nlit, nmatch;  // shader clocks, literals, matches
   uint64_t cyc_copy, cyc_flush; // clocks in match copies (incl. the stage write before) / ring flushes
   uint64_t nfar, cyc_far;       // matches whose source lies beyond the LDS ring (read from HBM), their clocks
+  uint64_t nblk, cyc_hdr, nlong; // blocks, clocks in block headers + table builds, fast-loop codes > 6 bits
 #endif
 };
 

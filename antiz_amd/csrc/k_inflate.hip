@@ -247,11 +247,12 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
   if (j >= njobs) return;
   const InfJob job = jobs[j];
   const uint64_t t_start = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
-  uint64_t nlit = 0, nmatch = 0, cyc_copy = 0, cyc_flush = 0, nfar = 0, cyc_far = 0;
+  uint64_t nlit = 0, nmatch = 0, cyc_copy = 0, cyc_flush = 0, nfar = 0, cyc_far = 0, nblk = 0, cyc_hdr = 0, nlong = 0;
   uint8_t* const ring = sh.ring;
   uint16_t* const lens = sh.lens;
   // per-lane shift of the canonical compare: lane l in 1..15 looks at the first l stream bits
   const uint32_t lsh = (lane >= 1 && lane <= 15) ? (uint32_t)(15 - lane) : 31u;
+  const uint32_t laneb = (uint32_t)lane + 4033u;   // the literal run: lane nst is the one where nb + 1 == laneb
   // RFC 1951 base / extra bits per length symbol (lane = symbol - 257) and distance symbol
   const uint32_t lentab = lane < 29 ? (len_base((uint32_t)lane) << 4) | len_extra((uint32_t)lane) : 0u;
   const uint32_t disttab = lane < 30 ? (dist_base((uint32_t)lane) << 4) | dist_extra((uint32_t)lane) : 0u;
@@ -316,6 +317,8 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
   uint32_t ad_a = 1, ad_b = 0;
   int overflow = 0;
   // literal stage: output byte prod + l in lane l (l < nst)
+  // literal stage: lane l holds (output byte prod + l) << 4 in its low 12 bits (l < nst); the root
+  // entries go in unshifted (symbol << 4 | length), so staging a literal is VALU work only
   uint32_t stg = 0, nst = 0;
   auto flush = [&](bool final) __attribute__((always_inline)) {
     const uint64_t n = prod - flushed;
@@ -355,21 +358,22 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
   };
   auto stage_flush = [&]() __attribute__((always_inline)) {
     if (nst) {
-      if ((uint32_t)lane < nst) ring[(prod + lane) & RMASK] = (uint8_t)stg;
+      if ((uint32_t)lane < nst) ring[(prod + lane) & RMASK] = (uint8_t)(stg >> 4);
       prod += nst;
       nst = 0;
       if (prod - flushed >= FLUSH_AT) flush(false);
     }
   };
   auto put_lit = [&](uint32_t s) __attribute__((always_inline)) {
-    stg = ((uint32_t)lane == nst) ? s : stg;
+    stg = ((uint32_t)lane == nst) ? (s << 4) : stg;
     nst++;
     if (ATZ_INF_CLOCKS) nlit++;
     if (nst == 64) stage_flush();
   };
-  // copy `len` bytes from `dist` back (dist <= prod); the stage must be empty.  False: the source is
-  // beyond the ring and no HBM copy of it exists (R_RETRY).
-  auto copy = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) -> bool {
+  // copy `len` bytes from `dist` back (dist <= prod) to prod; the stage must be empty.  False: the
+  // source is beyond the ring and no HBM copy of it exists (R_RETRY).  The caller advances prod and
+  // checks the flush threshold.
+  auto copy_at = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) -> bool {
     if (ATZ_INF_CLOCKS) nmatch++;
     if (RING < INF_RING_FULL && dist > RING) {
       // Far source: [prod - dist, prod - dist + len) ends at least RING - 258 bytes back, so it was
@@ -389,37 +393,45 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
         }
       }
       if (ATZ_INF_CLOCKS) { nfar++; cyc_far += __builtin_amdgcn_s_memtime() - tf0; }
-    } else if (dist >= len) {
+    } else {
+      // overlapping (dist < len): the source repeats with period dist.  i % dist in float: i < 320
+      // and dist <= 258, so (i + 0.5) / dist stays >= 0.5 / 258 away from an integer, far above
+      // the error of v_rcp_f32 (checked exhaustively, with the reciprocal 2 ulp off either way)
+      const uint32_t base = (uint32_t)prod - dist;
+      const bool ovl = dist < len;
       for (uint32_t i0 = 0; i0 < len; i0 += 64) {
         const uint32_t i = i0 + lane;
+        uint32_t k = i;
+        if (ovl) k = i - (uint32_t)(((float)i + 0.5f) * __builtin_amdgcn_rcpf((float)dist)) * dist;
         uint8_t v = 0;
-        if (i < len) v = ring[(prod - dist + i) & RMASK];
+        if (i < len) v = ring[(base + k) & RMASK];
         __builtin_amdgcn_wave_barrier();
-        if (i < len) ring[(prod + i) & RMASK] = v;
-      }
-    } else {   // overlapping: the source repeats with period `dist`
-      for (uint32_t i0 = 0; i0 < len; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        uint8_t v = 0;
-        if (i < len) v = ring[(prod - dist + i % dist) & RMASK];
-        __builtin_amdgcn_wave_barrier();
-        if (i < len) ring[(prod + i) & RMASK] = v;
+        if (i < len) ring[((uint32_t)prod + i) & RMASK] = v;
       }
     }
+    return true;
+  };
+  auto copy = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) -> bool {
+    if (!copy_at(len, dist)) return false;
     prod += len;
     if (prod - flushed >= FLUSH_AT) flush(false);
     return true;
   };
 
   // inflate_table acceptance (Z/inftrees.c:32-141); type 0 CODES, 1 LENS, 2 DISTS. Returns 0 / -1.
-  auto build = [&](Huff& h, const uint16_t* ln, int n, int type) __attribute__((always_inline)) -> int {
-    uint32_t cnt = 0;
-    for (int g = 0; g < n; g += 64) {
-      const int i = g + lane;
-      const uint32_t len = i < n ? ln[i] : 0;
-      for (int l = 1; l <= 15; l++) {
-        const uint32_t c = __popcll(__ballot(len == (uint32_t)l));
-        if (lane == l) cnt += c;
+  // pre: lane l (1..15) of `given` holds the number of length-l codes when have_cnt (the dynamic
+  // header counts them while decoding the lengths), else the count pass runs here
+  auto build = [&](Huff& h, const uint16_t* ln, int n, int type, bool have_cnt, uint32_t given) __attribute__((always_inline)) -> int {
+    uint32_t cnt = given;
+    if (!have_cnt) {
+      cnt = 0;
+      for (int g = 0; g < n; g += 64) {
+        const int i = g + lane;
+        const uint32_t len = i < n ? ln[i] : 0;
+        for (int l = 1; l <= 15; l++) {
+          const uint32_t c = __popcll(__ballot(len == (uint32_t)l));
+          if (lane == l) cnt += c;
+        }
       }
     }
     int max = 0, left = 1, bad = 0;
@@ -443,10 +455,12 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
     // ballot-ranked counting sort into LDS, then into the packed VGPR table
     uint32_t run = my_offs;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t present = __ballot(lane >= 1 && lane <= 15 && cnt != 0);   // lengths that occur
     for (int g = 0; g < n; g += 64) {
       const int i = g + lane;
       const uint32_t len = i < n ? ln[i] : 0;
-      for (int l = 1; l <= 15; l++) {
+      for (uint64_t pm = present; pm; pm &= pm - 1) {
+        const int l = __ffsll((unsigned long long)pm) - 1;
         const uint64_t m = __ballot(len == (uint32_t)l);
         if (!m) continue;
         const uint32_t base = rl(run, l);
@@ -506,8 +520,9 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
 
   auto codes = [&](const Huff& lh, const Huff& dh) __attribute__((always_inline)) -> int {
     uint64_t need;
+    bool redo = false;   // the careful path decodes the next symbol (the fast loop gave it back)
     for (;;) {
-      if (pos + 64 <= limit) {
+      if (!redo && pos + 64 <= limit) {
         // ---- fast loop: while >= 64 input bits remain at a symbol's start every field of it is
         // buffered-or-refillable (<= 48 bits), so no NEEDBITS checks.  Bits consumed here are
         // counted in `used` (32-bit) and folded into pos when the loop leaves.
@@ -515,7 +530,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
         const uint64_t rr64 = limit - 64 - pos;
         const uint32_t rem = rr64 > 0x7fffffffull ? 0x7fffffffu : (uint32_t)rr64;
         uint32_t used = 0;
-        int rc = 1;   // 1: careful path next, R_OK / R_ERR: return
+        int rc = 1;   // 1: careful path next, R_OK / R_RETRY: return
         while (used <= rem) {
           if (bc <= 32) refill1();
           uint32_t e = rl(lh.root, (uint32_t)bb & 63);
@@ -525,66 +540,100 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
           // The end-of-fast-path test (used <= rem: >= 64 input bits left) is made at each refill
           // only: after a passing test the buffer holds bits up to at most 64 past it, all before
           // the input limit, and the run decodes only buffered bits (bc > 32 at every lookup).
-          while (e - 1u < 4095u) {
-            const uint32_t L = e & 15;
-            bb >>= L; bc -= L; used += L;
-            put_lit(e >> 4);
-            if (bc <= 32) {
-              if (used > rem) break;
-              refill1();
-            }
-            e = rl(lh.root, (uint32_t)bb & 63);
+          // The run never flushes: it leaves when the stage is full (the flush, a large inlined
+          // block, stays outside the loop, so the loop body is straight-line scalar code).
+          if (e - 1u < 4095u) {
+            // One back edge and a 4-instruction exit test: nb = nst + 4032 (compared with
+            // laneb, it reaches 4096 when the stage is full) and the end-of-fast-region stop
+            // (tested at refills only: after a passing test every buffered bit lies before the input
+            // limit) sets bit 16, so "short literal, stage not full, no stop" is max(e - 1, nb) < 4096
+            // (a root entry has a length >= 1, so e - 1 < 4096 means e in [1, 4095]).  ub = used + bc
+            // changes only at refills.
+            uint32_t nb = nst + 4032u, ub = used + bc;
+            do {
+              const uint32_t L = e & 15;
+              bb >>= L; bc -= L;
+              nb++;
+              stg = (laneb == nb) ? e : stg;
+              if (ATZ_INF_CLOCKS) nlit++;
+              if (bc <= 32) {
+                if (ub - bc > rem) nb |= 0x10000u;
+                refill1();
+                ub += 32;
+              }
+              e = rl(lh.root, (uint32_t)bb & 63);
+            } while (((e - 1u) > nb ? (e - 1u) : nb) < 4096u);
+            nst = (nb & 0xffffu) - 4032u;
+            used = ub - bc;
+            if (nst == 64) stage_flush();
+            if (used > rem) break;   // rc == 1: the careful path resumes at this symbol
+            if (e - 1u < 4095u) continue;   // the stage was full: back to the run (bc > 32 here)
           }
-          if (used > rem) break;   // rc == 1: the careful path resumes at this symbol
 #endif
+          // Anything unusual -- an invalid code, a fixed-code length/distance symbol 286-287 / 30-31,
+          // a distance beyond the output -- leaves the fast loop at the symbol's start (`sym0`) and
+          // is decoded once more by the careful path, which reports it with zlib's exact error
+          // position.  So the fast loop has three exits: careful path next, end of block, retry.
+          const uint32_t sym0 = used;
           if (e == 0) {   // code longer than 6 bits (or invalid): canonical compare
+            if (ATZ_INF_CLOCKS) nlong++;
             const uint32_t v = __builtin_bitreverse32((uint32_t)bb) >> 17;
             const uint32_t c = v >> lsh;
             const uint64_t m = __ballot((c - lh.first) < lh.count);
-            if (!m) { errneed = pos0 + used + 1; errcode = 10; used += 1; rc = R_ERR; break; }
+            if (!m) { redo = true; break; }
             const uint32_t L = (uint32_t)__ffsll((unsigned long long)m) - 1;
             e = (lh.sym(rl(c + lh.ofm, L)) << 4) | L;
           }
           const uint32_t L = e & 15, sym = e >> 4;
           bb >>= L; bc -= L; used += L;
-          if (sym < 256) { put_lit(sym); continue; }
+          if (sym < 256) { put_lit(sym); continue; }   // (the stage is never left full: the run needs a free lane)
           if (sym == 256) { rc = R_OK; break; }
           const uint32_t ls = sym - 257;
-          if (ls >= 29) { errneed = pos0 + used; errcode = 11; rc = R_ERR; break; }   // fixed codes 286/287
+          if (ls >= 29) { used = sym0; redo = true; break; }   // fixed codes 286/287
           const uint32_t lt = rl(lentab, ls);
           const uint32_t le = lt & 15;
           const uint32_t len = (lt >> 4) + ((uint32_t)bb & ((1u << le) - 1));
           bb >>= le; bc -= le; used += le;
           if (bc <= 32) refill1();
-          if (dh.max == 0) { errneed = pos0 + used + 1; errcode = 12; used += 1; rc = R_ERR; break; }
           uint32_t d = rl(dh.root, (uint32_t)bb & 63);
-          if (d == 0) {
+          if (d == 0) {   // (an empty distance code has an all-zero root and no lengths: m == 0)
             const uint32_t v = __builtin_bitreverse32((uint32_t)bb) >> 17;
             const uint32_t c = v >> lsh;
             const uint64_t m = __ballot((c - dh.first) < dh.count);
-            if (!m) { errneed = pos0 + used + 1; errcode = 12; used += 1; rc = R_ERR; break; }
+            if (!m) { used = sym0; redo = true; break; }
             const uint32_t L2 = (uint32_t)__ffsll((unsigned long long)m) - 1;
             d = (dh.sym(rl(c + dh.ofm, L2)) << 4) | L2;
           }
           const uint32_t L2 = d & 15, ds = d >> 4;
+          if (ds >= 30) { used = sym0; redo = true; break; }   // fixed distance 30/31
           bb >>= L2; bc -= L2; used += L2;
-          if (ds >= 30) { errneed = pos0 + used; errcode = 13; rc = R_ERR; break; }   // fixed distance 30/31
           const uint32_t dt = rl(disttab, ds);
           const uint32_t de = dt & 15;
           const uint32_t dist = (dt >> 4) + ((uint32_t)bb & ((1u << de) - 1));
           bb >>= de; bc -= de; used += de;
           const uint64_t tc0 = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
-          stage_flush();
-          if ((uint64_t)dist > prod) { errneed = pos0 + used; errcode = 14; rc = R_ERR; break; }   // too far back
-          if (!copy(len, dist)) { rc = R_RETRY; break; }
+          // the stage goes to the ring, the match is copied after it, one flush test for both
+          // (unflushed bytes stay < FLUSH_AT + 64 + 258)
+          if (nst) {
+            if ((uint32_t)lane < nst) ring[(prod + lane) & RMASK] = (uint8_t)(stg >> 4);
+            prod += nst;
+            nst = 0;
+          }
+          if ((uint64_t)dist > prod) { used = sym0; redo = true; break; }   // too far back
+          if (!copy_at(len, dist)) { rc = R_RETRY; break; }
+          prod += len;
+          if (prod - flushed >= FLUSH_AT) flush(false);
           if (ATZ_INF_CLOCKS) cyc_copy += __builtin_amdgcn_s_memtime() - tc0;
         }
         pos = pos0 + used;
-        if (bc <= 32) refill();
+        if (redo) seek(pos);   // the bit buffer is past the symbol the careful path decodes again
+        else if (bc <= 32) refill();
         if (rc != 1) return rc;
         continue;
       }
-      // ---- careful path (the last 8 input bytes): zlib's NEEDBITS points exactly
+      // ---- careful path (the last 8 input bytes, and one symbol the fast loop gave back):
+      // zlib's NEEDBITS points and error positions exactly
+      redo = false;
       if (bc <= 32) refill();
       int sym = decode(lh, false, need);
       if (sym == -2) return R_NEED;
@@ -624,6 +673,8 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
     int last;
     Huff lh, dh;
     do {
+      const uint64_t th0 = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
+      if (ATZ_INF_CLOCKS) nblk++;
       NEEDB(3);
       last = (int)peek(1);
       const uint32_t type = (peek(3) >> 1) & 3;
@@ -657,9 +708,9 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
         if (take < len) return R_NEED;
       } else if (type == 1) {                               // FIXED
         for (int i = lane; i < 288; i += 64) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
-        build(lh, lens, 288, 1);
+        build(lh, lens, 288, 1, false, 0);
         for (int i = lane; i < 32; i += 64) lens[i] = 5;
-        build(dh, lens, 32, 2);
+        build(dh, lens, 32, 2, false, 0);
       } else if (type == 2) {                               // DYNAMIC (Z/inflate.c:908-1013)
         NEEDB(14);
         const uint32_t nlen = peek(5) + 257;
@@ -675,16 +726,56 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
           if (lane == 0) lens[cl_order(i)] = (uint16_t)v;
         }
         Huff chh;
-        if (build(chh, lens, 19, 0)) FAIL(7, pos);
+        if (build(chh, lens, 19, 0, false, 0)) FAIL(7, pos);
         uint32_t have = 0;
         const uint32_t total = nlen + ndist;
         uint64_t need;
         for (int i = lane; i < 320; i += 64) lens[i] = 0;
         uint32_t prevlen = 0;
+        // per-length counts for the two builds, kept while the lengths are decoded: lane l counts
+        // the literal/length codes of length l, lane 16 + l the distance codes (a run may cross
+        // from one table into the other)
+        uint32_t lcnt = 0;
+        auto count = [&](uint32_t len, uint32_t n) __attribute__((always_inline)) {
+          if (len == 0) return;
+          const uint32_t nl = have < nlen ? (n < nlen - have ? n : nlen - have) : 0u;
+          lcnt += ((uint32_t)lane == len) ? nl : 0u;
+          lcnt += ((uint32_t)lane == len + 16) ? n - nl : 0u;
+        };
+        // Fast loop: the whole length sequence lies before the input limit (at most 7 + 7 bits per
+        // length), so no NEEDBITS tests.  Codes of <= 6 bits come from the root lane; a 7-bit code,
+        // an invalid pattern or an invalid repeat leaves the rest to the careful loop below, which
+        // reports errors at zlib's exact positions.
+        if (pos + 14ull * total + 64 <= limit) {
+          while (have < total) {
+            if (bc <= 32) refill1();
+            const uint32_t e = rl(chh.root, (uint32_t)bb & 63);
+            if (e == 0) break;
+            const uint32_t L = e & 15, sym = e >> 4;
+            if (sym < 16) {
+              bb >>= L; bc -= L; pos += L;
+              if (lane == 0) lens[have] = (uint16_t)sym;
+              count(sym, 1);
+              prevlen = sym;
+              have++;
+              continue;
+            }
+            const uint32_t eb = sym == 16 ? 2u : sym == 17 ? 3u : 7u;
+            const uint32_t x = (uint32_t)(bb >> L) & ((1u << eb) - 1);
+            const uint32_t copyn = (sym == 18 ? 11u : 3u) + x;
+            if ((sym == 16 && have == 0) || have + copyn > total) break;
+            const uint32_t len = sym == 16 ? prevlen : 0u;
+            bb >>= L + eb; bc -= L + eb; pos += L + eb;
+            for (uint32_t k = lane; k < copyn; k += 64) lens[have + k] = (uint16_t)len;
+            count(len, copyn);
+            prevlen = len;
+            have += copyn;
+          }
+        }
         while (have < total) {
           const int sym = decode(chh, true, need);
           if (sym == -2) return R_NEED;
-          if (sym < 16) { if (lane == 0) lens[have] = (uint16_t)sym; prevlen = (uint32_t)sym; have++; continue; }
+          if (sym < 16) { if (lane == 0) lens[have] = (uint16_t)sym; count((uint32_t)sym, 1); prevlen = (uint32_t)sym; have++; continue; }
           uint32_t copyn, len = 0, eb;
           if (sym == 16) eb = 2; else if (sym == 17) eb = 3; else eb = 7;
           NEEDB(eb);
@@ -700,15 +791,18 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
           drop(eb);
           if (have + copyn > total) FAIL(8, pos);
           for (uint32_t k = lane; k < copyn; k += 64) lens[have + k] = (uint16_t)len;
+          count(len, copyn);
           prevlen = len;
           have += copyn;
         }
         if (iuni(lens[256]) == 0) FAIL(9, pos);
-        if (build(lh, lens, (int)nlen, 1)) FAIL(9, pos);
-        if (build(dh, lens + nlen, (int)ndist, 2)) FAIL(9, pos);
+        const uint32_t dcnt = __shfl_down(lcnt, 16, 64);   // lane l: distance codes of length l
+        if (build(lh, lens, (int)nlen, 1, true, lcnt)) FAIL(9, pos);
+        if (build(dh, lens + nlen, (int)ndist, 2, true, dcnt)) FAIL(9, pos);
       } else {
         FAIL(15, pos);                                      // invalid block type
       }
+      if (ATZ_INF_CLOCKS) cyc_hdr += __builtin_amdgcn_s_memtime() - th0;
       if (type != 0) {   // one (inlined) decode loop for fixed and dynamic blocks
         const int rr = codes(lh, dh);
         if (rr != R_OK) return rr;
@@ -758,8 +852,10 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
   o.cyc = __builtin_amdgcn_s_memtime() - t_start;
   o.nlit = nlit; o.nmatch = nmatch; o.cyc_copy = cyc_copy; o.cyc_flush = cyc_flush;
   o.nfar = nfar; o.cyc_far = cyc_far;
+  o.nblk = nblk; o.cyc_hdr = cyc_hdr; o.nlong = nlong;
 #else
   (void)t_start; (void)nlit; (void)nmatch; (void)cyc_copy; (void)cyc_flush; (void)nfar; (void)cyc_far;
+  (void)nblk; (void)cyc_hdr; (void)nlong;
 #endif
   if (lane == 0) res[j] = o;
 }
