@@ -195,6 +195,21 @@ __device__ __forceinline__ uint32_t cl_order(uint32_t i) {
   return (uint32_t)((i < 12 ? (0x22caa324e804a30ull >> (5 * i)) : (0x3c2e1346cull >> (5 * (i - 12)))) & 31);
 }
 
+// Fast-loop entries (the roots' lanes hold them for codes of <= 6 bits): literal/length symbol s
+// with code length L is s << 4 | L for literals and end-of-block (< 4096 for literals), and a length
+// symbol adds its extra-bit count (bits 13-15) and base - 3 (bits 16-23); a distance symbol d is
+// L | extra bits << 4 | base << 8.  A length or distance is then base + one bit-field extract, and
+// its code and extra bits are consumed together.
+__device__ __forceinline__ uint32_t lit_entry(uint32_t s, uint32_t L) {
+  if (s <= 256) return (s << 4) | L;
+  const uint32_t ls = s - 257;
+  return (s << 4) | L | (len_extra(ls) << 13) | ((len_base(ls) - 3u) << 16);
+}
+__device__ __forceinline__ uint32_t dist_entry(uint32_t d, uint32_t L) {
+  return L | (dist_extra(d) << 4) | (dist_base(d) << 8);
+}
+__device__ __forceinline__ uint32_t ubfe(uint32_t x, uint32_t o, uint32_t w) { return __builtin_amdgcn_ubfe(x, o, w); }
+
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   for (int d = 32; d >= 1; d >>= 1) {
     uint32_t lo = __shfl_xor((uint32_t)v, d, 64);
@@ -241,6 +256,11 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
                                                unsigned long long* __restrict__ arena_used, uint64_t arena_cap) {
   constexpr uint32_t RMASK = RING - 1;
   constexpr uint32_t FLUSH_AT = RING / 2;   // unflushed bytes stay <= FLUSH_AT + 258 + 64 < RING
+  // WIDE: in the small ring, stage writes and match copies store all 64 lanes (no exec mask); the
+  // lanes past the data put garbage into the next < 64 slots, i.e. over bytes more than RING - 64
+  // back.  Those are long flushed, and a match reaching them is a far copy (dist > RING - 64), read
+  // from the HBM output.  The slots get their real bytes before anything reads them.  The 32 KiB
+  // ring holds the whole window, so it keeps the masks.
   __shared__ InfShared<RING> sh;
   const int lane = threadIdx.x;
   const uint32_t j = blockIdx.x;
@@ -358,7 +378,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
   };
   auto stage_flush = [&]() __attribute__((always_inline)) {
     if (nst) {
-      if ((uint32_t)lane < nst) ring[(prod + lane) & RMASK] = (uint8_t)(stg >> 4);
+      if (RING < INF_RING_FULL || (uint32_t)lane < nst) ring[(prod + lane) & RMASK] = (uint8_t)(stg >> 4);   // (see WIDE)
       prod += nst;
       nst = 0;
       if (prod - flushed >= FLUSH_AT) flush(false);
@@ -375,7 +395,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
   // checks the flush threshold.
   auto copy_at = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) -> bool {
     if (ATZ_INF_CLOCKS) nmatch++;
-    if (RING < INF_RING_FULL && dist > RING) {
+    if (RING < INF_RING_FULL && dist > RING - 64) {
       // Far source: [prod - dist, prod - dist + len) ends at least RING - 258 bytes back, so it was
       // flushed (unflushed bytes < RING/2 + 322) -- if this job's output still exists.  dist > RING
       // > len, so the copy does not overlap itself.  The flush's stores are drained first and the
@@ -404,9 +424,9 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
         uint32_t k = i;
         if (ovl) k = i - (uint32_t)(((float)i + 0.5f) * __builtin_amdgcn_rcpf((float)dist)) * dist;
         uint8_t v = 0;
-        if (i < len) v = ring[(base + k) & RMASK];
+        if (RING < INF_RING_FULL || i < len) v = ring[(base + k) & RMASK];
         __builtin_amdgcn_wave_barrier();
-        if (i < len) ring[((uint32_t)prod + i) & RMASK] = v;
+        if (RING < INF_RING_FULL || i < len) ring[((uint32_t)prod + i) & RMASK] = v;   // (see WIDE)
       }
     }
     return true;
@@ -472,16 +492,20 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
     h.t0 = sw[lane];
     h.t1 = n > 128 ? sw[64 + lane] : 0;
     h.t2 = n > 256 ? sw[128 + lane] : 0;
-    // 6-bit root: lane p resolves the code of length <= 6 its stream bits start with
+    // 6-bit root: lane p resolves the code of length <= 6 its stream bits start with, as a fast-loop
+    // entry (LENS, DISTS; the fixed distance symbols 30-31 stay 0, so the fast loop hands them to
+    // the careful path) or symbol << 4 | length (CODES)
     {
       const uint32_t rp = __builtin_bitreverse32((uint32_t)lane) >> 26;
-      uint32_t e = 0;
+      uint32_t sv = 0, lf = 0;
       const int lm = max < 6 ? max : 6;
       for (int l = 1; l <= lm; l++) {
         const uint32_t f = rl(h.first, l), k = rl(h.count, l), o = rl(h.ofm, l);
         const uint32_t c = rp >> (6 - l);
-        if (e == 0 && (c - f) < k) e = ((uint32_t)sh.sort[o + c] << 4) | (uint32_t)l;
+        if (lf == 0 && (c - f) < k) { sv = sh.sort[o + c]; lf = (uint32_t)l; }
       }
+      uint32_t e = 0;
+      if (lf) e = type == 1 ? lit_entry(sv, lf) : type == 2 ? (sv < 30 ? dist_entry(sv, lf) : 0u) : ((sv << 4) | lf);
       h.root = e;
     }
     return 0;
@@ -581,19 +605,17 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
             const uint32_t c = v >> lsh;
             const uint64_t m = __ballot((c - lh.first) < lh.count);
             if (!m) { redo = true; break; }
-            const uint32_t L = (uint32_t)__ffsll((unsigned long long)m) - 1;
-            e = (lh.sym(rl(c + lh.ofm, L)) << 4) | L;
+            const uint32_t Lc = (uint32_t)__ffsll((unsigned long long)m) - 1;
+            const uint32_t sc = lh.sym(rl(c + lh.ofm, Lc));
+            if (sc >= 286) { redo = true; break; }   // fixed codes 286/287
+            e = lit_entry(sc, Lc);
           }
-          const uint32_t L = e & 15, sym = e >> 4;
-          bb >>= L; bc -= L; used += L;
-          if (sym < 256) { put_lit(sym); continue; }   // (the stage is never left full: the run needs a free lane)
-          if (sym == 256) { rc = R_OK; break; }
-          const uint32_t ls = sym - 257;
-          if (ls >= 29) { used = sym0; redo = true; break; }   // fixed codes 286/287
-          const uint32_t lt = rl(lentab, ls);
-          const uint32_t le = lt & 15;
-          const uint32_t len = (lt >> 4) + ((uint32_t)bb & ((1u << le) - 1));
-          bb >>= le; bc -= le; used += le;
+          const uint32_t L = e & 15;
+          if (e < 4096u) { bb >>= L; bc -= L; used += L; put_lit(e >> 4); continue; }   // (the stage is never left full)
+          if (((e >> 4) & 511u) == 256u) { bb >>= L; bc -= L; used += L; rc = R_OK; break; }
+          const uint32_t le = (e >> 13) & 7u;
+          const uint32_t len = (e >> 16) + 3u + ubfe((uint32_t)bb, L, le);
+          bb >>= L + le; bc -= L + le; used += L + le;
           if (bc <= 32) refill1();
           uint32_t d = rl(dh.root, (uint32_t)bb & 63);
           if (d == 0) {   // (an empty distance code has an all-zero root and no lengths: m == 0)
@@ -601,21 +623,19 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
             const uint32_t c = v >> lsh;
             const uint64_t m = __ballot((c - dh.first) < dh.count);
             if (!m) { used = sym0; redo = true; break; }
-            const uint32_t L2 = (uint32_t)__ffsll((unsigned long long)m) - 1;
-            d = (dh.sym(rl(c + dh.ofm, L2)) << 4) | L2;
+            const uint32_t Lc = (uint32_t)__ffsll((unsigned long long)m) - 1;
+            const uint32_t dc = dh.sym(rl(c + dh.ofm, Lc));
+            if (dc >= 30) { used = sym0; redo = true; break; }   // fixed distance 30/31
+            d = dist_entry(dc, Lc);
           }
-          const uint32_t L2 = d & 15, ds = d >> 4;
-          if (ds >= 30) { used = sym0; redo = true; break; }   // fixed distance 30/31
-          bb >>= L2; bc -= L2; used += L2;
-          const uint32_t dt = rl(disttab, ds);
-          const uint32_t de = dt & 15;
-          const uint32_t dist = (dt >> 4) + ((uint32_t)bb & ((1u << de) - 1));
-          bb >>= de; bc -= de; used += de;
+          const uint32_t L2 = d & 15, de = (d >> 4) & 15u;
+          const uint32_t dist = (d >> 8) + ubfe((uint32_t)bb, L2, de);
+          bb >>= L2 + de; bc -= L2 + de; used += L2 + de;
           const uint64_t tc0 = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
           // the stage goes to the ring, the match is copied after it, one flush test for both
           // (unflushed bytes stay < FLUSH_AT + 64 + 258)
           if (nst) {
-            if ((uint32_t)lane < nst) ring[(prod + lane) & RMASK] = (uint8_t)(stg >> 4);
+            if (RING < INF_RING_FULL || (uint32_t)lane < nst) ring[(prod + lane) & RMASK] = (uint8_t)(stg >> 4);
             prod += nst;
             nst = 0;
           }
