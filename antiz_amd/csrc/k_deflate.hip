@@ -1088,11 +1088,12 @@ __device__ __forceinline__ void pq_down(LDS uint32_t* heap, int heap_len, int k,
       int j = p << 1;
       if (j > heap_len) { stop = true; break; }
       const int lj = (1 << t) - 2 + (j - (k << t));
-      uint32_t hj = (uint32_t)__builtin_amdgcn_readlane((int)g, lj);
-      if (j < heap_len) {
-        const uint32_t hj1 = (uint32_t)__builtin_amdgcn_readlane((int)g, lj + 1);
-        if ((hj1 >> 10) <= (hj >> 10)) { j++; hj = hj1; }
-      }
+      // the right child (ties go right); past heap_len the gathered lane holds ~0u, never chosen
+      const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)g, lj);
+      const uint32_t hr = (uint32_t)__builtin_amdgcn_readlane((int)g, lj + 1);
+      const uint32_t c = (hr >> 10) <= (hl >> 10) ? 1u : 0u;
+      const uint32_t hj = c ? hr : hl;
+      j += (int)c;
       if (vk <= (hj >> 10)) { stop = true; break; }
       heap[p] = hj;
       p = j;
@@ -1157,22 +1158,22 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
   if (heap_len <= 63) {
     // The whole heap in one VGPR (heap[i] in lane i): every sift level is two v_readlane and a
     // lane select, no LDS round trip.  Same steps, same tie-breaks as the LDS heap below.
-    uint32_t H = lane <= heap_len ? heap[lane] : 0xffffffffu;
+    // Lanes 0 and past heap_len hold ~0u (a key above every real one), so a sift level reads both
+    // children without testing j < len (lane 64 wraps to lane 0); the loop has one exit.
+    uint32_t H = lane >= 1 && lane <= heap_len ? heap[lane] : 0xffffffffu;
     auto rd = [&](int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)H, i); };
     auto wr = [&](int i, uint32_t v) { H = lane == i ? v : H; };
     auto down = [&](int len, int k) {
       const uint32_t v = rd(k), vk = v >> 10;
-      for (;;) {
-        int j = k << 1;
-        if (j > len) break;
-        uint32_t hj = rd(j);
-        if (j < len) {
-          const uint32_t hj1 = rd(j + 1);
-          if ((hj1 >> 10) <= (hj >> 10)) { j++; hj = hj1; }
-        }
-        if (vk <= (hj >> 10)) break;
-        wr(k, hj);
-        k = j;
+      int j = k << 1;
+      bool go = j <= len;
+      while (go) {
+        const uint32_t a = rd(j), b = rd(j + 1);
+        const uint32_t c = (b >> 10) <= (a >> 10) ? 1u : 0u;   // ties go right
+        const uint32_t hj = c ? b : a;
+        j += (int)c;
+        go = vk > (hj >> 10);
+        if (go) { wr(k, hj); k = j; j = k << 1; go = j <= len; }
       }
       wr(k, v);
     };
@@ -1180,6 +1181,7 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
     do {
       const uint32_t kn = rd(1);
       wr(1, rd(heap_len));
+      wr(heap_len, 0xffffffffu);
       heap_len--;
       down(heap_len, 1);
       const uint32_t km = rd(1);

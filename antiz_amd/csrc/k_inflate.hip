@@ -454,23 +454,23 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
         }
       }
     }
-    int max = 0, left = 1, bad = 0;
-    uint32_t code = 0, offs = 0, my_first = 0, my_offs = 0;
-    for (int l = 1; l <= 15; l++) {
-      const uint32_t c = rl(cnt, l);
-      if (c) max = l;
-      left <<= 1;
-      left -= (int)c;
-      if (left < 0) bad = 1;
-      if (lane == l) { my_first = code; my_offs = offs; }
-      code = (code + c) << 1;
-      offs += c;
-    }
+    // zlib's sequential pass over the lengths (inftrees.c: left, offs[], next code), lane-parallel:
+    // with w_l = count_l << (15 - l), the first code of length l is (sum over i < l of w_i) >> (15 - l),
+    // and "left" goes negative at some length exactly when the Kraft sum W = sum of w_l exceeds 2^15
+    // (the partial sums only grow); the code is incomplete when W < 2^15.  Two DPP scans.
+    const uint32_t cl = (lane >= 1 && lane <= 15) ? cnt : 0u;
+    const uint64_t nz = __ballot(cl != 0);
+    const int max = nz ? 63 - __clzll((long long)nz) : 0;
+    const uint32_t wl = cl << ((15 - lane) & 15);
+    const uint32_t wi = wave_incl_scan(wl), ci = wave_incl_scan(cl);
+    const uint32_t W = rl(wi, 15);
+    const uint32_t my_first = (lane >= 1 && lane <= 15) ? (wi - wl) >> (15 - lane) : 0u;
+    const uint32_t my_offs = ci - cl;
     h.max = max;
     h.root = 0;
     if (max == 0) { h.count = 0; h.first = 0; h.ofm = 0; return 0; }
-    if (bad) return -1;
-    if (left > 0 && (type == 0 || max != 1)) return -1;
+    if (W > 32768u) return -1;
+    if (W < 32768u && (type == 0 || max != 1)) return -1;
     h.first = my_first; h.count = (lane >= 1 && lane <= 15) ? cnt : 0; h.ofm = my_offs - my_first;
     // ballot-ranked counting sort into LDS, then into the packed VGPR table
     uint32_t run = my_offs;
