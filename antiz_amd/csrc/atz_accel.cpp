@@ -2114,13 +2114,22 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
 }
 // ATZ_PIPES=k (1..8), default 3.  C4 A/B after the 1024-thread match blocks (interleaved, 4 runs each):
 // 2 pipes ~988, 3 ~1022, 4 ~854 MB/s (earlier, with slower match walks, 2 was best)
-static size_t sweep_pipes() {
-  static size_t v = 0;
-  if (!v) {
+// Pipes for a sweep of n streams (ATZ_PIPES overrides).  Three pipes, two of which share a hardware
+// queue, keep the GPU full on a large file (more, or one queue each, let LDS-heavy kernels displace
+// each other: DESIGN s3.6).  A small sweep -- one rank's share of a file split over many GPUs -- is
+// bound by its rounds' slowest trials instead; with >= 8 hardware queues in the process
+// (GPU_MAX_HW_QUEUES, read at HIP init; bench.py sets it for such runs) six pipes overlap more rounds:
+// a 12 500-stream share 696-710 vs 628-655 MB/s on one MI355X (25 000: 904 vs 923, so only below 16 000).
+static size_t sweep_pipes(size_t n) {
+  static int env = -2, hwq = -1;
+  if (env == -2) {
     const char* e = std::getenv("ATZ_PIPES");
-    v = e ? (size_t)std::max(1, std::min(8, std::atoi(e))) : 3;
+    env = e ? std::max(1, std::min(8, std::atoi(e))) : -1;
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    hwq = q ? std::atoi(q) : 4;
   }
-  return v;
+  if (env > 0) return (size_t)env;
+  return n <= 16000 && hwq >= 8 ? 6 : 3;
 }
 // The sweep runs while the scan is still producing records: sweep_begin starts one host thread
 // per pipe, sweep_publish hands a range of ready records (inflated, Adler-32 known) to the pipes,
@@ -2164,7 +2173,7 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
   R.sd.assign(n_max, StreamDev{});
   if (int r = c->d_adler.reserve(n_max * 4 + 4096)) return r;
   if (int r = c->d_streams.reserve(n_max * sizeof(StreamDev) + 4096)) return r;
-  R.np = std::max<size_t>(1, std::min(sweep_pipes(), (n_max + 255) / 256));
+  R.np = std::max<size_t>(1, std::min(sweep_pipes(n_max), (n_max + 255) / 256));
   c->pipes_running = R.np;
   if (int r = ensure_pipes(c, R.np)) return r;
   for (size_t g = 0; g < R.np; g++) {

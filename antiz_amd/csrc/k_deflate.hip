@@ -1083,20 +1083,21 @@ __device__ __forceinline__ void pq_down(LDS uint32_t* heap, int heap_len, int k,
     const uint32_t g = (t_l <= 5 && idx <= heap_len) ? heap[idx] : 0xffffffffu;
     int p = k;
     bool stop = false;
+    // A child past heap_len reads ~0u from the gather, a key above every real one, so v stops there:
+    // the stop test also ends the path at the heap's bottom.  lj, the gathered lane of the left
+    // child, follows the path: a lane's left child is lane 2 * lane + 2 (k itself counts as -1).
+    int lj = 0;
 #pragma unroll
     for (int t = 1; t <= 5; t++) {
-      int j = p << 1;
-      if (j > heap_len) { stop = true; break; }
-      const int lj = (1 << t) - 2 + (j - (k << t));
-      // the right child (ties go right); past heap_len the gathered lane holds ~0u, never chosen
+      // the right child (ties go right)
       const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)g, lj);
       const uint32_t hr = (uint32_t)__builtin_amdgcn_readlane((int)g, lj + 1);
       const uint32_t c = (hr >> 10) <= (hl >> 10) ? 1u : 0u;
       const uint32_t hj = c ? hr : hl;
-      j += (int)c;
       if (vk <= (hj >> 10)) { stop = true; break; }
       heap[p] = hj;
-      p = j;
+      p = 2 * p + (int)c;
+      lj = 2 * (lj + (int)c) + 2;
     }
     k = p;
     if (stop) break;

@@ -32,7 +32,7 @@ fi
 if has shardtest; then
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_shard.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/shardtest.log 2>&1 || exit 9
 fi
-for N in 2 4; do
+for N in 2 4 8; do
   if has file$N; then
     ATZ_BENCH_BACKEND=gloo timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 --master-port $((29500 + N)) bench.py --gpus $N --steps 2 --warmup 1 --no-recon > $O/file$N.json 2> $O/file$N.err || exit 10
   fi
