@@ -857,6 +857,7 @@ static constexpr uint32_t HOLE_SLOTS = HOLE_SLOTS_M;   // fast mode: latest skip
 struct TreeWork {      // one tree under construction (zlib's heap / bl_count in LDS; dad and freq in TreeScratch)
   uint32_t heap[HEAPN + 1];  // packed keys (freq:16 | depth:5 | node:10) in [1, heap_len]; node ids from heap_max
   uint16_t bl_count[16];
+  uint32_t blc32[16];        // gen_bitlen's per-length leaf counters (LDS atomics)
 };
 
 // Pointer-jumping scratch of gen_bitlen.  It lives in the match-table ring's LDS (the parse is
@@ -1245,7 +1246,9 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
     }
     cur ^= 1;
   }
-  uint32_t blc = 0;   // lane b: bl_count[b]
+  // bl_count by LDS atomics: one ds_add per 64 nodes instead of 15 ballots (the adds to one
+  // counter serialise in the LDS pipe, not in the issue slots)
+  if (lane < 16) w.blc32[lane] = 0;
   int overflow = 0;
   for (int g = 0; g < nn; g += 64) {
     const int i = g + lane;
@@ -1259,12 +1262,12 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
     overflow += __popcll(__ballot(capped));
     if (bits > (uint32_t)max_length) bits = (uint32_t)max_length;
     const bool leaf = in_tree && i <= max_code;
-    if (leaf) lenv[i] = (uint8_t)bits;
-    for (int b = 1; b <= 15; b++) {
-      const uint32_t c = (uint32_t)__popcll(__ballot(leaf && bits == (uint32_t)b));
-      if (lane == b) blc += c;
+    if (leaf) {
+      lenv[i] = (uint8_t)bits;
+      __hip_atomic_fetch_add(&w.blc32[bits], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
+  uint32_t blc = lane >= 1 && lane < 16 ? w.blc32[lane] : 0u;   // lane b: bl_count[b]
   if (overflow) {   // Z/trees.c:531-564 (rare): sequential, as zlib
     auto bl = [&](int b) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)blc, b); };
     auto blset = [&](int b, uint32_t v) { blc = lane == b ? v : blc; };
@@ -1309,20 +1312,20 @@ __device__ __noinline__ TreeRes build_tree(LDS TreeWork& w, LDS TreeScratch& sc,
 __device__ __noinline__ void gen_codes(const LDS TreeWork& w, int max_code, LDS uint16_t* codes, LDS uint8_t* lens,
                                        int lane) {
   max_code = (int)uni((uint32_t)max_code);
-  uint32_t nc = 0;   // lane b: next_code[b]
-  {
-    uint32_t code = 0;
-    for (int bits = 1; bits <= 15; bits++) {
-      code = (code + w.bl_count[bits - 1]) << 1;
-      if (lane == bits) nc = code;
-    }
-  }
+  // lane b: next_code[b] = sum over i < b of bl_count[i] << (b - i), i.e. the exclusive prefix sum of
+  // bl_count[i] << (15 - i), shifted down by 15 - b (one DPP scan instead of zlib's 15-step loop)
+  const bool lb = lane >= 1 && lane <= 15;
+  const uint32_t bc = lb ? (uint32_t)w.bl_count[lane] : 0u;
+  const uint32_t wv = bc << ((15 - lane) & 15);
+  uint32_t nc = lb ? (wave_incl_scan(wv) - wv) >> (15 - lane) : 0u;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint64_t present = __ballot(bc != 0);   // lengths in use
   for (int g = 0; g <= max_code; g += 64) {
     const int n = g + lane;
     const uint32_t l = n <= max_code ? lens[n] : 0u;   // build_tree left the lengths here
     uint32_t mine = 0;
-    for (int b = 1; b <= 15; b++) {
+    for (uint64_t pm = present; pm; pm &= pm - 1) {
+      const int b = __ffsll((unsigned long long)pm) - 1;
       const uint64_t m = __ballot(l == (uint32_t)b);
       if (!m) continue;
       const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)nc, b);
