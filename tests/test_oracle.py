@@ -113,3 +113,14 @@ def test_maxdist_edge_fixture_pinned():
     for brute in (0, 1):
         rc, out, _ = _libs.ora_precompress(data, brute=brute)
         assert rc == 0 and hashlib.sha256(out).hexdigest() == MAXDIST_EDGE_SHA
+
+
+def test_inflate_edge_fixtures_pinned():
+    """tests/golden/inflate_edges.json: the real zlib 1.2.8's results (make_inflate_edges.py) on hand-built
+    streams at k_inflate's fast-loop edges (fixed-code 286/287 and distance 30/31, far distances,
+    incomplete dynamic distance trees, oversized HLIT/HDIST, all overlapping copies); the oracle agrees."""
+    cases = json.load(open(os.path.join(G.GOLD, "inflate_edges.json")))["cases"]
+    assert len(cases) > 400
+    for c in cases:
+        got = _libs.ora_inflate(bytes.fromhex(c["hex"]))
+        assert got == (c["status"], c["consumed"], c["produced"]), c["family"]
