@@ -312,9 +312,10 @@ def main():
                 log("PARITY FAILURE: the timed run's ATZ1 differs from the reference's")
 
     # reconstruct (-r, and precompress's default verify: main.cpp:869-950, 1173-1203) of the last ATZ1,
-    # resident in HBM; not part of the metric: its own wall time, and the round trip checked
+    # resident in HBM; not part of the metric: its own wall time, and the round trip checked.  Every rank
+    # of a shards run, and the one-GPU file run (at N > 1 in file mode the ATZ1 sits on rank 0 only)
     recon = None
-    if args.mode == "shards" and not args.no_recon:
+    if (args.mode == "shards" or world == 1) and not args.no_recon:
         dptr, alen, _ = ctx.precompress_device(dev.data_ptr(), data)
         hdev = torch.empty(alen + 4096, dtype=torch.uint8, device="cuda")
         torch.cuda.synchronize()

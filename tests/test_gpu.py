@@ -94,6 +94,29 @@ def test_inflate_matches_zlib_semantics(ctx):
     assert not bad, bad[:10]
 
 
+def test_inflate_edge_fixtures(ctx):
+    """k_inflate's fast-loop edges against the real zlib 1.2.8's results (tests/golden/inflate_edges.json,
+    made by make_inflate_edges.py from oracle/_ref/libzref.so): fixed-code symbols 286/287 and distance
+    codes 30/31 deep in the input and inside its last 8 bytes (Z/inffast.c:288, 303; Z/inflate.c:1064,
+    1100), distances past the output, incomplete one-code distance trees, oversized HLIT/HDIST, and one
+    stream per distance d = 1..258 holding a match of every length 3..258 at that distance -- every
+    (i, d) pair of the overlapping copy's v_rcp_f32 modulo (i < 320), whose bytes the Adler-32 trailer
+    checks."""
+    cases = json.load(open(os.path.join(GOLD, "inflate_edges.json")))["cases"]
+    buf = bytearray()
+    ranges = []
+    for k, c in enumerate(cases):
+        s = bytes.fromhex(c["hex"])
+        buf += bytes(k % 3)   # unaligned starts
+        ranges.append((len(buf), len(s)))
+        buf += s
+    got = ctx.inflate_batch(bytes(buf), ranges)
+    bad = [(c["family"], k, tuple(got[k]), (c["status"], c["consumed"], c["produced"]))
+           for k, c in enumerate(cases) if tuple(got[k]) != (c["status"], c["consumed"], c["produced"])]
+    assert not bad, bad[:10]
+    assert sum(c["family"] == "overlap" for c in cases) == 258
+
+
 @pytest.mark.parametrize("name", ["asd", "text4k", "rand5k", "input8k"])
 def test_deflate_kats_all_params(ctx, name):
     kat = json.load(open(os.path.join(GOLD, "deflate_kat.json")))
