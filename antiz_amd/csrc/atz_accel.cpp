@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <string>
 #include <memory>
 #include <new>
@@ -239,8 +240,9 @@ struct StreamState {
   std::vector<uint32_t> rawdiff;  // raw positions of the current best
   std::vector<uint8_t> diffval;
   uint32_t trials = 0;
-  uint32_t full_at = ~0u;         // list index whose trial ran past its match-table prefix: rerun with a full table
-  int32_t rp = -1;                // symbol-replay entries (levels 1-9) in the owning pipe's rp_pool
+  uint32_t full_at = ~0u;         // list index whose trial ran past its match-table prefix (flow: rerun as
+                                  // the stream's next step, with its whole table)
+  int32_t rp = -1;                // symbol-replay entries (levels 1-9) in the context's rp_pool
   bool recomp = false;
   // levels 7-9 already run budget-free at (window, memLevel): level, longest PL a lazy read improved,
   // longest length read (cross-level duplicates, see level_dups)
@@ -345,6 +347,9 @@ int header_type_host(unsigned b0, unsigned b1) {
 // ChainJob.infl_off / MatchJob.infl_off), so every kernel takes a null inflated-buffer base: the
 // records of one file may live in several allocations (one per scan piece).
 const uint8_t* const INFL_BASE = nullptr;
+// Hash-bucket tables likewise: chain_off fields hold a table's absolute address / 4 (DevArena / a pipe's
+// round-local d_chains), so the kernels take a null base.
+uint32_t* const CHAIN_BASE = nullptr;
 
 }  // namespace
 
@@ -369,20 +374,30 @@ struct RpEntry {
   uint8_t window = 0;
   uint8_t memlevel = 0;   // the saver's
 };
-// Saved sequences of one pipe: device memory in chunks (allocated on demand, kept across sweeps),
-// handed out by a bump pointer that each sweep resets.
-struct RpArena {
+// Device memory in 1 GiB chunks (allocated on demand, kept across sweeps), handed out by a bump
+// pointer that each sweep resets: the context's hash-bucket cache and its saved symbol sequences.
+// Shared by the sweep's pipes (a stream's tables, built by whichever pipe ran its step, are read by
+// the next one), hence the lock; addresses are absolute.
+struct DevArena {
   static constexpr uint64_t CHUNK = 1ull << 30;
+  std::mutex mu;
   std::vector<std::unique_ptr<DBuf>> chunks;
+  std::vector<std::pair<uint64_t, uint64_t>> span;   // [lo, hi) of each chunk (holds() without the lock's allocator state)
   size_t cur = 0;
-  uint64_t used = 0, total = 0;   // bytes in chunks[cur]; bytes handed out this sweep
-  void reset() { cur = 0; used = 0; total = 0; }
-  uint64_t alloc(uint64_t bytes, uint64_t cap) {   // device address, 0: none (cap reached, no memory)
+  uint64_t used = 0, total = 0, cap = 0;   // bytes in chunks[cur]; bytes handed out this sweep; limit
+  void reset(uint64_t cap_) {
+    std::lock_guard<std::mutex> lk(mu);
+    cur = 0; used = 0; total = 0; cap = cap_;
+  }
+  uint64_t alloc(uint64_t bytes) {   // device address (256-byte aligned), 0: none (cap reached, no memory)
+    bytes = (bytes + 255) & ~255ull;
+    std::lock_guard<std::mutex> lk(mu);
     if (total + bytes > cap) return 0;
     while (cur < chunks.size() && used + bytes > chunks[cur]->n) { cur++; used = 0; }
     if (cur == chunks.size()) {
       auto b = std::make_unique<DBuf>();
       if (b->reserve(std::max(CHUNK, bytes)) != 0) { (void)hipGetLastError(); return 0; }
+      span.push_back({(uint64_t)(uintptr_t)b->p, (uint64_t)(uintptr_t)b->p + b->n});
       chunks.push_back(std::move(b));
       used = 0;
     }
@@ -391,11 +406,10 @@ struct RpArena {
     total += bytes;
     return a;
   }
-  bool holds(uint64_t a, uint64_t len) const {   // [a, a + len) inside one chunk
-    for (const auto& b : chunks) {
-      const uint64_t lo = (uint64_t)(uintptr_t)b->p;
-      if (a >= lo && a + len <= lo + b->n) return true;
-    }
+  bool holds(uint64_t a, uint64_t len) {   // [a, a + len) inside one chunk
+    std::lock_guard<std::mutex> lk(mu);
+    for (const auto& s : span)
+      if (a >= s.first && a + len <= s.second) return true;
     return false;
   }
 };
@@ -403,8 +417,8 @@ struct ChainBufs {   // bucket-build job lists and scratch (one set per HIP stre
   DBuf d_cjobs, d_cjobs2, d_cjobs3, d_heads, d_heads2;
 };
 // One HIP stream of sweep work with its own buffers, kernel timers and counters.  The sweep runs
-// several pipes at once (streams partitioned among them, one host thread each), so one pipe's
-// launch tails, host gaps and small launches overlap another's work.
+// several pipes at once (one host thread each, taking batches of streams from the sweep's queues), so
+// one pipe's launch tails, host gaps and small launches overlap another's work.
 struct Pipe {
   hipStream_t st = nullptr;
   KTimer kt;
@@ -415,19 +429,12 @@ struct Pipe {
   // queues are shared by the pipes' streams (two pipes then share a queue, which measured faster
   // than every pipe on its own queue: DESIGN.md s3.6)
   hipStream_t pst = nullptr;
-  uint64_t chain_used = 0, chain_cap = 0;
-  std::vector<uint32_t> streams;   // the streams whose chain tables this pipe owns
-  // symbol replay: saved sequences (bump arena, reset per sweep) and per-stream entries
-  RpArena rp;
-  std::vector<std::array<struct RpEntry, 9>> rp_pool;   // [stream's entry][level - 1]
+  // (stream, memLevel) pairs whose tables this round built in d_chains because the context's bucket
+  // cache was full: forgotten at the round's end
+  std::vector<std::pair<uint32_t, int>> tmp_chains;
   // diagnostics (ATZ_TIMING): bucket builds, and per stream the memLevels a table-reading trial used
   uint64_t diag_builds = 0;
   std::vector<uint16_t> diag_need;
-  // streams handed to this pipe (scan pieces arrive while it sweeps); closed after the last piece
-  std::mutex in_mu;
-  std::condition_variable in_cv;
-  std::vector<uint32_t> inbox;
-  bool in_closed = false;
   int id = 0;
   // diagnostics (ATZ_TIMING): host phase times, per trial kind x level counters
   double t_list = 0, t_chains = 0, t_trials = 0, t_apply = 0;
@@ -461,11 +468,28 @@ struct atz_ctx {
   bool file_on_device = false;      // d_file holds the current file
   const uint8_t* dev_file = nullptr;
   atz_stats_t stats{};
-  // chains cache: per record and memlevel
-  std::vector<std::array<uint64_t, 10>> chain_off;   // offset in the owning pipe's d_chains
+  // hash-bucket cache: per record and memLevel the tables' absolute device address / 4 (u32 units
+  // from a null base; ~0: not built), in chain_arena
+  std::vector<std::array<uint64_t, 10>> chain_off;
+  DevArena chain_arena;
+  // symbol replay: saved sequences and per-stream entries (StreamState::rp indexes rp_pool, reserved
+  // for every stream of the sweep so that a pipe's push_back never moves another pipe's entries)
+  DevArena rp_arena;
+  std::vector<std::array<RpEntry, 9>> rp_pool;   // [stream's entry][level - 1]
+  std::mutex rp_mu;
   // deepest bucket - 1 per (stream, memLevel) at [10 s + m], written by k_buckets_sort into pinned
   // host memory (~0: not built yet); read after the building stream has been synchronised
   PinBuf depth_pin;
+  // The sweep's queues of streams waiting for their next step (see sched_take)
+  struct Sched {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool flow = true;                     // one shared queue pair (else: one queue per pipe, rounds)
+    std::vector<std::deque<uint32_t>> q;  // flow: one shared queue; rounds: one per pipe
+    std::vector<size_t> unfinished;       // published streams not done (flow: [0]; rounds: per pipe)
+    bool closed = false;                  // every stream is published
+    bool abort = false;
+  } sched;
   std::vector<std::unique_ptr<Pipe>> pipes;
   std::vector<std::unique_ptr<DBuf>> slabs;   // inflated records, one allocation per scan piece
   size_t pipes_running = 1;
@@ -1300,16 +1324,18 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
   return 0;
 }
 
+// Tables go into the context's bucket cache (chain_arena, kept for the stream's later trials by any
+// pipe); once it is full, into this pipe's d_chains for the current round only (forgotten by
+// forget_tmp_chains at the round's end).  Tables are addressed absolutely (null chains base).
+static void forget_tmp_chains(atz_ctx* x, Pipe* c) {
+  for (auto& q : c->tmp_chains) x->chain_off[q.first][q.second] = ~0ull;
+  c->tmp_chains.clear();
+}
 static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need, ChainBufs& B) {
-  auto words = [&](uint32_t s) { return 2 * ((x->recs[s].infl_len + 63) & ~63ull); };
-  uint64_t add = 0;
-  for (auto& q : need)
-    if (x->chain_off[q.first][q.second] == ~0ull) add += words(q.first);
-  if ((c->chain_used + add) * 4 > c->chain_cap) {   // drop this pipe's cache
-    for (uint32_t s : c->streams) x->chain_off[s].fill(~0ull);
-    c->chain_used = 0;
-  }
+  auto bytes = [&](uint32_t s) { return 8 * ((x->recs[s].infl_len + 63) & ~63ull); };
   std::vector<ChainJob> jobs;
+  std::vector<size_t> tmp;   // jobs whose table goes into d_chains (offset relative to it, for now)
+  uint64_t tmp_bytes = 0;
   for (auto& q : need) {
     uint32_t s = q.first;
     int m = q.second;
@@ -1317,33 +1343,33 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     ChainJob jb;
     jb.infl_off = x->infl_off[s];
     jb.n = x->recs[s].infl_len;
-    jb.chain_off = c->chain_used;
     jb.memlevel = (uint32_t)m;
     jb.slot = 0;
     jb.dslot = 10 * s + (uint32_t)m;
     jb.pad_ = 0;
-    x->chain_off[s][m] = c->chain_used;
-    c->chain_used += words(s);
+    const uint64_t a = x->chain_arena.alloc(bytes(s));
+    if (a) {
+      jb.chain_off = a >> 2;
+    } else {
+      jb.chain_off = tmp_bytes >> 2;
+      tmp_bytes += (bytes(s) + 255) & ~255ull;
+      tmp.push_back(jobs.size());
+      c->tmp_chains.push_back({s, m});
+    }
+    x->chain_off[s][m] = jb.chain_off;   // (relative ones are rebased below)
     jobs.push_back(jb);
     c->diag_builds++;
   }
   if (jobs.empty()) return 0;
-  // grow the cache (keeps contents)
-  size_t need_bytes = c->chain_used * 4 + 4096;
-  if (need_bytes > c->d_chains.n) {
-    void* np = nullptr;
-    size_t cap = std::min<size_t>(need_bytes + need_bytes / 2 + (64 << 20), c->chain_cap + (1ull << 30));
-    if (cap < need_bytes) cap = need_bytes;
-    if (hipMalloc(&np, cap) != hipSuccess) return ATZ_E_NOMEM;
-    if (c->d_chains.p) {
-      HIPCHK(hipMemcpyAsync(np, c->d_chains.p, c->d_chains.n, hipMemcpyDeviceToDevice, c->st));
-      HIPCHK(hipStreamSynchronize(c->st));
-      (void)hipFree(c->d_chains.p);
+  if (!tmp.empty()) {   // the round's own tables: d_chains is free (the pipe's earlier rounds are done)
+    if (int r = c->d_chains.reserve(tmp_bytes + 4096)) return r;
+    const uint64_t base = (uint64_t)(uintptr_t)c->d_chains.p >> 2;
+    for (size_t k : tmp) {
+      jobs[k].chain_off += base;
+      x->chain_off[(uint32_t)(jobs[k].dslot / 10)][jobs[k].memlevel] = jobs[k].chain_off;
     }
-    c->d_chains.p = np;
-    c->d_chains.n = cap;
   }
-  if (int r = build_bucket_jobs(x, c, B, jobs, c->d_chains.as<uint32_t>(), true, x->depth_pin.as<uint32_t>())) return r;
+  if (int r = build_bucket_jobs(x, c, B, jobs, CHAIN_BASE, true, x->depth_pin.as<uint32_t>())) return r;
   if (bucket_verify()) {
     // diagnostics (ATZ_BUCKETS_VERIFY=1): the same jobs again on the in-order kernels, compared
     uint64_t tot = 0;
@@ -1354,7 +1380,7 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     if (int r = build_bucket_jobs(x, c, B, alt, tmp.as<uint32_t>(), false, nullptr)) return r;
     std::vector<uint32_t> h1(tot), h2(tot);
     for (size_t k = 0; k < jobs.size(); k++)
-      HIPCHK(hipMemcpyAsync(h1.data() + alt[k].chain_off, c->d_chains.as<uint32_t>() + jobs[k].chain_off,
+      HIPCHK(hipMemcpyAsync(h1.data() + alt[k].chain_off, (const void*)(uintptr_t)(jobs[k].chain_off << 2),
                             8 * ((jobs[k].n + 63) & ~63ull), hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipMemcpyAsync(h2.data(), tmp.p, tot * 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
@@ -1445,11 +1471,11 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
     kbeg(c, 4);
     if (k < NC)
       hipLaunchKernelGGL(k_match_lds, dim3((uint32_t)cnt[k]), dim3(MATCH_THREADS), (uint32_t)(3 * cls[gmax[k]] + 64), c->st,
-                         INFL_BASE, c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(),
+                         INFL_BASE, CHAIN_BASE, c->d_R.as<uint2>(),
                          c->d_mjobs.as<MatchJob>() + beg[k]);
     else
       hipLaunchKernelGGL(k_match, dim3((uint32_t)cnt[k]), dim3(256), 0, c->st, INFL_BASE,
-                         c->d_chains.as<uint32_t>(), c->d_R.as<uint2>(), c->d_mjobs.as<MatchJob>() + beg[k]);
+                         CHAIN_BASE, c->d_R.as<uint2>(), c->d_mjobs.as<MatchJob>() + beg[k]);
     kend(c);
     KCHECK("k_match");
   }
@@ -1472,46 +1498,75 @@ static uint64_t sym_words(int kind, uint32_t memlevel, uint64_t n) {   // symbol
   return (mw_trial(kind, memlevel) ? n + 64 : 0) + (1ull << (memlevel + 6)) + 64;
 }
 
-// Runs the trials tr[k] (k = 0 stored, 1 fast, 2 slow levels); res[k] receives their results.
-// Chain tables must exist.  Match tables are built for a prefix of each trial's positions; a
-// trial that parses past it (TR_NEED_R) gets the rest of its table and is run again.
-static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
-                           std::vector<TrialRes>* res);
+// Trials of one launch group, kept between their first pass and their reruns: tr[k] (k = 0 stored,
+// 1 fast, 2 slow levels) in launch order (LPT, see trials_order), perm[k][q] = the caller's index of
+// tr[k][q], res[k] in launch order.  Match tables are built for a prefix of each trial's positions; a
+// trial that parses past it stops with TR_NEED_R, and trials_rerun completes its table and runs it
+// again.
+struct TrialSet {
+  std::vector<Trial> tr[3];
+  std::vector<uint32_t> perm[3];
+  std::vector<TrialRes> res[3];
+  size_t base = 0;   // next free slot of d_trials / d_tres
+};
 // A launch lasts as long as its slowest wave, so the trials go in longest-expected-first order
 // (classic LPT): low memLevels mean many blocks (one tree build each), fast levels mean hole
-// fallbacks, and the work grows with the stream.  Results come back in the caller's order.
-static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
-                      std::vector<TrialRes>* res) {
-  std::vector<Trial> tp[3];
-  std::vector<uint32_t> perm[3];
-  std::vector<TrialRes> rp[3];
+// fallbacks, and the work grows with the stream.  Multi-wave trials lead each kind (a launch of their own).
+static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
   for (int k = 0; k < 3; k++) {
-    const size_t n = tr[k].size();
-    perm[k].resize(n);
+    const size_t n = in[k].size();
+    S.perm[k].resize(n);
     std::vector<uint64_t> key(n);
     for (size_t q = 0; q < n; q++) {
-      const Trial& t = tr[k][q];
+      const Trial& t = in[k][q];
       key[q] = x->recs[t.stream].infl_len * (uint64_t)(k == 1 ? 3 : 1) * (uint64_t)(10 - t.memlevel) *
                (uint64_t)((t.mode & 8) ? 1 : 4);   // replays skip the match walks
-      perm[k][q] = (uint32_t)q;
+      S.perm[k][q] = (uint32_t)q;
     }
-    // multi-wave trials first (one launch of their own), each group longest first
-    std::stable_sort(perm[k].begin(), perm[k].end(), [&](uint32_t a, uint32_t b) {
-      const bool ma = mw_trial(k, tr[k][a].memlevel), mb = mw_trial(k, tr[k][b].memlevel);
+    std::stable_sort(S.perm[k].begin(), S.perm[k].end(), [&](uint32_t a, uint32_t b) {
+      const bool ma = mw_trial(k, in[k][a].memlevel), mb = mw_trial(k, in[k][b].memlevel);
       return ma != mb ? ma : key[a] > key[b];
     });
-    tp[k].resize(n);
-    for (size_t q = 0; q < n; q++) tp[k][q] = tr[k][perm[k][q]];
+    S.tr[k].resize(n);
+    for (size_t q = 0; q < n; q++) S.tr[k][q] = in[k][S.perm[k][q]];
+    S.res[k].clear();
   }
-  if (int r = run_trials_impl(x, c, d_cmp, tp, so, rp)) return r;
-  for (int k = 0; k < 3; k++) {
-    res[k].resize(tr[k].size());
-    for (size_t q = 0; q < tr[k].size(); q++) res[k][perm[k][q]] = rp[k][q];
-  }
+  S.base = 0;
+}
+// the trial kernels over h[0, cnt) (one kind, multi-wave ones first), at slots [base, base + cnt)
+static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepOpts& so, int k, const Trial* h,
+                         size_t cnt, size_t base) {
+  auto launch1 = [&](const Trial* hh, size_t n1, size_t b1, bool mw) -> int {
+    HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + b1, hh, n1 * sizeof(Trial), hipMemcpyHostToDevice, c->st));
+    SweepArgs A;
+    A.file = d_cmp; A.infl = INFL_BASE; A.chains = CHAIN_BASE;
+    A.R = c->d_R.as<uint2>();
+    A.streams = x->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + b1;
+    A.res = c->d_tres.as<TrialRes>() + b1; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
+    A.adler = x->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)n1;
+    dim3 g((uint32_t)n1), b(mw ? MW_THREADS : 64);
+    kbeg(c, 0);
+    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
+    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw, g, b, 0, c->st, A);
+    else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, 0, c->st, A);
+    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, 0, c->st, A);
+    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
+    kend(c);
+    KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
+    return 0;
+  };
+  size_t m = 0;
+  while (m < cnt && mw_trial(k, h[m].memlevel)) m++;
+  if (m)
+    if (int r = launch1(h, m, base, true)) return r;
+  if (cnt > m)
+    if (int r = launch1(h + m, cnt - m, base + m, false)) return r;
   return 0;
 }
-static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
-                           std::vector<TrialRes>* res) {
+// First pass: match-table prefixes, every trial once.  Chain tables must exist.
+static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, const SweepOpts& so) {
+  std::vector<Trial>* tr = S.tr;
+  std::vector<TrialRes>* res = S.res;
   uint64_t r_tot = 0;
   std::vector<MatchJob> mj;
   for (int k = 0; k < 3; k++)
@@ -1538,42 +1593,13 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
   const size_t tot_trials = tr[0].size() + tr[1].size() + tr[2].size();
   if (int r = c->d_trials.reserve(2 * tot_trials * sizeof(Trial) + 64)) return r;
   if (int r = c->d_tres.reserve(2 * tot_trials * sizeof(TrialRes) + 64)) return r;
-  auto launch1 = [&](int k, const Trial* h, size_t cnt, size_t base, bool mw) -> int {
-    HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + base, h, cnt * sizeof(Trial), hipMemcpyHostToDevice, c->st));
-    SweepArgs A;
-    A.file = d_cmp; A.infl = INFL_BASE; A.chains = c->d_chains.as<uint32_t>();
-    A.R = c->d_R.as<uint2>();
-    A.streams = x->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + base;
-    A.res = c->d_tres.as<TrialRes>() + base; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
-    A.adler = x->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)cnt;
-    dim3 g((uint32_t)cnt), b(mw ? MW_THREADS : 64);
-    kbeg(c, 0);
-    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
-    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw, g, b, 0, c->st, A);
-    else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, 0, c->st, A);
-    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, 0, c->st, A);
-    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
-    kend(c);
-    KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
-    return 0;
-  };
-  // the multi-wave trials lead each kind's list (run_trials orders them so): one launch each
-  auto launch = [&](int k, const Trial* h, size_t cnt, size_t base) -> int {
-    size_t m = 0;
-    while (m < cnt && mw_trial(k, h[m].memlevel)) m++;
-    if (m)
-      if (int r = launch1(k, h, m, base, true)) return r;
-    if (cnt > m)
-      if (int r = launch1(k, h + m, cnt - m, base + m, false)) return r;
-    return 0;
-  };
   size_t base = 0;
   size_t bases[3];
   for (int k = 0; k < 3; k++) {
     bases[k] = base;
     res[k].resize(tr[k].size());
     if (tr[k].empty()) continue;
-    if (int r = launch(k, tr[k].data(), tr[k].size(), base)) return r;
+    if (int r = trials_launch(x, c, d_cmp, so, k, tr[k].data(), tr[k].size(), base)) return r;
     base += tr[k].size();
   }
   for (int k = 0; k < 3; k++)
@@ -1582,13 +1608,21 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
                             hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
   kcollect(c);
-  // second pass: complete the match tables of the trials that need them and run those again
+  S.base = base;
+  return 0;
+}
+// Reruns: the TR_NEED_R trials for which want(trial) holds get the rest of their match table and run
+// again (their r_off region keeps the prefix).  The others keep TR_NEED_R.
+static int trials_rerun(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, const SweepOpts& so,
+                        const std::function<bool(const Trial&)>& want) {
+  std::vector<Trial>* tr = S.tr;
+  std::vector<TrialRes>* res = S.res;
   std::vector<Trial> again[3];
   std::vector<size_t> where[3];
-  mj.clear();
+  std::vector<MatchJob> mj;
   for (int k = 1; k < 3; k++)
     for (size_t q = 0; q < tr[k].size(); q++) {
-      if (res[k][q].state != TR_NEED_R) continue;
+      if (res[k][q].state != TR_NEED_R || (want && !want(tr[k][q]))) continue;
       Trial t = tr[k][q];
       const uint64_t n = x->recs[t.stream].infl_len;
       MatchJob m{};
@@ -1600,32 +1634,49 @@ static int run_trials_impl(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vecto
       where[k].push_back(q);
       c->stats.n_trials_rerun++;
     }
-  if (mj.empty()) return 0;
+  if (again[1].empty() && again[2].empty()) return 0;
+  // (slots past the first pass's: d_trials / d_tres hold 2 x the set)
   if (int r = launch_match(x, c, mj)) return r;
   std::vector<TrialRes> rr[3];
+  size_t base = S.base, bases[3] = {0, 0, 0};
+  if (base + again[1].size() + again[2].size() > 2 * (tr[0].size() + tr[1].size() + tr[2].size())) return ATZ_E_INTERNAL;
   for (int k = 1; k < 3; k++) {
+    bases[k] = base;
     if (again[k].empty()) continue;
-    if (int r = launch(k, again[k].data(), again[k].size(), base)) return r;
+    if (int r = trials_launch(x, c, d_cmp, so, k, again[k].data(), again[k].size(), base)) return r;
     rr[k].resize(again[k].size());
     base += again[k].size();
   }
-  {
-    size_t b2 = base;
-    for (int k = 2; k >= 1; k--) b2 -= again[k].size();
-    for (int k = 1; k < 3; k++) {
-      if (again[k].empty()) continue;
-      HIPCHK(hipMemcpyAsync(rr[k].data(), c->d_tres.as<TrialRes>() + b2, again[k].size() * sizeof(TrialRes),
+  for (int k = 1; k < 3; k++)
+    if (!again[k].empty())
+      HIPCHK(hipMemcpyAsync(rr[k].data(), c->d_tres.as<TrialRes>() + bases[k], again[k].size() * sizeof(TrialRes),
                             hipMemcpyDeviceToHost, c->st));
-      b2 += again[k].size();
-    }
-  }
   HIPCHK(hipStreamSynchronize(c->st));
   kcollect(c);
   for (int k = 1; k < 3; k++)
     for (size_t q = 0; q < again[k].size(); q++) {
       if (rr[k][q].state == TR_NEED_R) return ATZ_E_INTERNAL;
       res[k][where[k][q]] = rr[k][q];
+      tr[k][where[k][q]].x_lim = again[k][q].x_lim;
     }
+  S.base = base;
+  return 0;
+}
+// results in the caller's order
+static void trials_results(const TrialSet& S, std::vector<TrialRes>* res) {
+  for (int k = 0; k < 3; k++) {
+    res[k].resize(S.tr[k].size());
+    for (size_t q = 0; q < S.tr[k].size(); q++) res[k][S.perm[k][q]] = S.res[k][q];
+  }
+}
+// Runs the trials tr[k] to completion (first pass, then every rerun); res[k] receives their results.
+static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
+                      std::vector<TrialRes>* res) {
+  TrialSet S;
+  trials_order(x, tr, S);
+  if (int r = trials_first(x, c, d_cmp, S, so)) return r;
+  if (int r = trials_rerun(x, c, d_cmp, S, so, nullptr)) return r;
+  trials_results(S, res);
   return 0;
 }
 
@@ -1704,11 +1755,13 @@ static void level_dups(atz_ctx* x, std::vector<StreamState>& ss, std::vector<Tri
 }
 // after a round: what the budget-free level-7-9 trials that ran parsed (a replay parsed its saver's
 // whole sequence)
-static void level_record(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, const std::vector<Trial>& slow,
-                         const std::vector<TrialRes>& res) {
+// (streams for which mine(stream) holds)
+static void level_record(atz_ctx* x, std::vector<StreamState>& ss, const std::vector<Trial>& slow,
+                         const std::vector<TrialRes>& res, const std::function<bool(uint32_t)>& mine) {
   for (size_t q = 0; q < slow.size(); q++) {
     const Trial& t = slow[q];
     const TrialRes& r = res[q];
+    if (!mine(t.stream)) continue;
     if (t.clevel < 7 || t.clevel > 9 || (t.mode & 128) || r.state == TR_NEED_R || r.state == TR_OVERFLOW) continue;
     if (!budget_free(x, 2, t)) continue;
     StreamState& st = ss[t.stream];
@@ -1718,7 +1771,7 @@ static void level_record(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, cons
     uint32_t rm = r.reads_max;
     if (r.saved_flags & 4) {   // a replay: its saver's reads
       if (st.rp < 0) continue;
-      rm = c->rp_pool[st.rp][t.clevel - 1].reads_max;
+      rm = x->rp_pool[st.rp][t.clevel - 1].reads_max;
     }
     st.xl.push_back({(uint16_t)t.window, (uint16_t)t.memlevel, (uint16_t)t.clevel, (uint16_t)(rm >> 16),
                      (uint16_t)(rm & 0xffffu)});
@@ -1735,7 +1788,6 @@ static void level_record(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, cons
 // levels) only if their own table agrees on those entries, which the kernel checks before parsing.
 static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int kind, std::vector<Trial>& trs,
                         std::vector<std::array<uint32_t, 4>>& savers) {
-  const uint64_t cap = RP_ARENA_CAP / std::max<size_t>(1, x->pipes_running);
   const bool checked = replay_mode() != 3 && kind == 2;   // ATZ_REPLAY=3: budget-free replays only
   for (size_t q = 0; q < trs.size(); q++) {
     Trial& t = trs[q];
@@ -1746,8 +1798,13 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
     const bool bf = replay_free(x, kind, t);
     if (!bf && !checked) continue;
     StreamState& st = ss[t.stream];
-    if (st.rp < 0) { st.rp = (int32_t)c->rp_pool.size(); c->rp_pool.emplace_back(); }
-    RpEntry& e = c->rp_pool[st.rp][t.clevel - 1];
+    if (st.rp < 0) {   // the pool holds one entry per stream at most: never past its reserve
+      std::lock_guard<std::mutex> lk(x->rp_mu);
+      if (x->rp_pool.size() == x->rp_pool.capacity()) continue;
+      st.rp = (int32_t)x->rp_pool.size();
+      x->rp_pool.emplace_back();
+    }
+    RpEntry& e = x->rp_pool[st.rp][t.clevel - 1];
     if (e.state == 2 && e.window == t.window) {
       if (replay_mode() == 2) continue;
       replay_from(t, e, bf);
@@ -1756,7 +1813,7 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
     } else if (e.state == 0 && bf) {
       const uint64_t sb = (4 * (n + 64) + 255) & ~255ull, tb = kind == 2 ? ((8 * n + 255) & ~255ull) : 0;
       if (!e.addr) {
-        e.addr = c->rp.alloc(sb + tb, cap);
+        e.addr = x->rp_arena.alloc(sb + tb);
         if (!e.addr) continue;
         e.tab = tb ? e.addr + sb : 0;
       }
@@ -1773,33 +1830,105 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
 
 // match tables + output scratch of one round, over all pipes
 static constexpr uint64_t ROUND_BUDGET_BYTES = 24ull << 30;
-// The sweep of the streams c->streams on pipe c (per-kind x level counters: count, cycles
-// total/tree/emit/heap/fallback, parsed bytes, symbols, scan/send cycles, parse window phases).
+
+// Sweep scheduling (ATZ_SCHED).  Streams wait in queues for their next step; a pipe takes a batch,
+// runs one round on it (each stream's next K trials: tables, trial launches, the reference's rule per
+// stream) and hands back the streams that have not stopped.
+//  * rounds (default): each pipe sweeps a fixed interleaved share of the streams, all of them in every
+//    round; a trial that parsed past its match-table prefix (TR_NEED_R) is rerun with its whole table
+//    inside the round, before its stream's rule walk goes on.
+//  * flow (ATZ_SCHED=flow): the pipes share one queue and take batches of at most 1/pipes of the
+//    unfinished streams, so a stream's next step starts as soon as its own round is done; a TR_NEED_R
+//    trial reruns as the stream's next step (front of the queue) with its whole table, and speculative
+//    rounds (K > 1) build whole tables up front.  Measured slower than rounds on one MI355X (DESIGN.md
+//    s3.6: C4 1276-1341 vs 1442-1468 MB/s, a 12 500-stream share 504-598 vs 606-672): the trial
+//    kernels are issue-bound with about a thousand trial waves resident, so freeing streams from the
+//    round barrier adds concurrency the GPU cannot use and costs rounds.
+static bool sched_flow() {
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_SCHED"); v = e && std::string(e) == "flow"; }
+  return v == 1;
+}
+// Pipe g's next batch into `batch` (false: the sweep is over for this pipe); unf = streams not done.
+static bool sched_take(atz_ctx* x, int g, size_t np, std::vector<uint32_t>& batch, size_t& unf) {
+  auto& Q = x->sched;
+  std::unique_lock<std::mutex> lk(Q.mu);
+  batch.clear();
+  auto stop = [&] { return Q.abort || x->sweep_abort.load(std::memory_order_relaxed); };
+  if (!Q.flow) {
+    std::deque<uint32_t>& q = Q.q[g];
+    Q.cv.wait(lk, [&] { return stop() || !q.empty() || Q.closed; });
+    if (stop() || q.empty()) return false;
+    batch.assign(q.begin(), q.end());
+    q.clear();
+    unf = batch.size();
+    return true;
+  }
+  std::deque<uint32_t>& q = Q.q[0];
+  Q.cv.wait(lk, [&] { return stop() || !q.empty() || (Q.closed && Q.unfinished[0] == 0); });
+  if (stop() || q.empty()) return false;
+  unf = Q.unfinished[0];
+  const size_t cap = std::max<size_t>(64, (unf + np - 1) / np);
+  const size_t m = std::min(cap, q.size());
+  batch.assign(q.begin(), q.begin() + (long)m);
+  q.erase(q.begin(), q.begin() + (long)m);
+  return true;
+}
+// After a round: the batch's streams that have not stopped go back (`waiting`, which the round's
+// budget left out, first).
+static void sched_give(atz_ctx* x, int g, const std::vector<StreamState>& ss, const std::vector<uint32_t>& active,
+                       const std::vector<uint32_t>& waiting) {
+  auto& Q = x->sched;
+  std::lock_guard<std::mutex> lk(Q.mu);
+  size_t done = 0;
+  if (!Q.flow) {
+    std::vector<uint32_t> front(waiting);
+    for (uint32_t s : active) { if (ss[s].phase == 2) done++; else front.push_back(s); }
+    Q.q[g].insert(Q.q[g].begin(), front.begin(), front.end());
+  } else {
+    Q.q[0].insert(Q.q[0].begin(), waiting.begin(), waiting.end());
+    for (uint32_t s : active) {
+      if (ss[s].phase == 2) { done++; continue; }
+      if (ss[s].full_at == ss[s].idx) Q.q[0].push_front(s);   // a rerun: next in line
+      else Q.q[0].push_back(s);
+    }
+  }
+  Q.unfinished[Q.flow ? 0 : g] -= done;
+  Q.cv.notify_all();
+}
+static void sched_abort(atz_ctx* x) {
+  std::lock_guard<std::mutex> lk(x->sched.mu);
+  x->sched.abort = true;
+  x->sched.cv.notify_all();
+}
+
+// The sweep work of pipe c: rounds on the batches sched_take hands it (per-kind x level counters:
+// count, cycles total/tree/emit/heap/fallback, parsed bytes, symbols, scan/send cycles, parse window
+// phases).
 static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss, size_t target) {
   auto t0 = std::chrono::steady_clock::now();
   std::vector<uint32_t> active;
-  // new streams join at round boundaries; an idle pipe waits for the next scan piece
-  auto take_inbox = [&]() -> bool {   // false: nothing left to do
-    std::unique_lock<std::mutex> lk(c->in_mu);
-    if (active.empty()) c->in_cv.wait(lk, [&] { return !c->inbox.empty() || c->in_closed; });
-    for (uint32_t s : c->inbox) { active.push_back(s); c->streams.push_back(s); }
-    c->inbox.clear();
-    return !active.empty();
-  };
+  const bool flow = x->sched.flow;
+  const size_t np = x->pipes_running;
+  size_t unf = 0;
   SweepOpts so{x->o.recomp_tresh, x->o.sizediff_tresh, x->o.shortcut_len, x->o.mismatch_tol};
   uint64_t rounds = 0, ntr = 0, nsc = 0, nhz = 0, nspec = 0;
   std::vector<Trial> tr[3];
   std::vector<TrialRes> trres[3];
-  // A round evaluates the next K trials of every active stream (speculatively: a stream that
-  // stops at its j-th trial discards the results of the later ones), K sized so a round fills the
+  // A round evaluates the next K trials of every stream of the batch (speculatively: a stream that
+  // stops at its j-th trial discards the results of the later ones), K sized so the rounds fill the
   // GPU.  Results are applied per stream strictly in list order, so the outcome is the
   // reference's sequential one; the speculation only changes how much work runs per launch.
-  while (take_inbox()) {
-    if (x->sweep_abort.load(std::memory_order_relaxed)) break;
+  while (sched_take(x, c->id, np, active, unf)) {
     rounds++;
     std::vector<uint32_t> waiting;
+    struct Give {   // the batch goes back on every exit from the round (an error aborts the sweep anyway)
+      atz_ctx* x; Pipe* c; const std::vector<StreamState>& ss; const std::vector<uint32_t>& a, &w;
+      ~Give() { forget_tmp_chains(x, c); sched_give(x, c->id, ss, a, w); }
+    } give{x, c, ss, active, waiting};
     const auto tl0 = std::chrono::steady_clock::now();
-    const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, target / active.size()));
+    const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, flow ? target * np / std::max<size_t>(1, unf)
+                                                                                : target / active.size()));
     std::vector<std::pair<uint32_t, int>> need;
     std::vector<uint32_t> need_b;   // per need entry: the trial's walk budget (replay's budget-free test)
     for (int k = 0; k < 3; k++) tr[k].clear();
@@ -1828,7 +1957,9 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         Trial t{};
         t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
         t.best_ident = st.ident;
-        if (st.idx + j == st.full_at) t.mode |= 2;   // host-only bit: whole match table up front
+        // host-only bit 1: whole match table up front -- a deferred rerun, or any trial of a speculative
+        // flow round (K > 1: the sweep's tail, where a rerun's extra step would lengthen the stream's chain)
+        if (st.idx + j == st.full_at || (flow && K > 1)) t.mode |= 2;
         t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
         int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
@@ -1872,18 +2003,31 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       for (const Trial& t : tr[k]) {   // saved sequences stay inside the arena (a bad slot would fault the GPU)
         if (!(t.mode & 12)) continue;
         const uint64_t n = x->recs[t.stream].infl_len;
-        const bool tab_ok = !(t.mode & 48) || c->rp.holds(t.rp_tab, 8 * n);
-        if (!c->rp.holds(t.rp_syms, 4 * (n + 64)) || ((t.mode & 8) && t.rp_nsym > n) || !tab_ok) {
+        const bool tab_ok = !(t.mode & 48) || x->rp_arena.holds(t.rp_tab, 8 * n);
+        if (!x->rp_arena.holds(t.rp_syms, 4 * (n + 64)) || ((t.mode & 8) && t.rp_nsym > n) || !tab_ok) {
           std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
           return ATZ_E_INTERNAL;
         }
       }
     if (int r = c->d_out.reserve(out_tot + 4096)) return r;
     if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
-    auto finish_savers = [&]() {   // a complete saved sequence serves the stream's later trials at that level
+    // streams of the batch by index a into active: held[a] = its rule walk waits for a rerun (rounds)
+    std::vector<uint8_t> held(active.size(), 0);
+    std::vector<uint32_t> slot_of;   // stream -> a (only for the batch's streams)
+    auto a_of = [&](uint32_t s) -> size_t {
+      return std::lower_bound(slot_of.begin(), slot_of.end(), s, [&](uint32_t e, uint32_t v) { return active[e] < v; }) - slot_of.begin();
+    };
+    for (size_t a = 0; a < active.size(); a++) slot_of.push_back((uint32_t)a);
+    std::sort(slot_of.begin(), slot_of.end(), [&](uint32_t p1, uint32_t p2) { return active[p1] < active[p2]; });
+    auto is_held = [&](uint32_t s) -> bool { return held[slot_of[a_of(s)]] != 0; };
+    // a complete saved sequence serves the stream's later trials at that level (held streams' savers wait
+    // for their reruns: a saver stopped by TR_NEED_R runs again)
+    auto finish_savers = [&](bool held_ones) {
       for (const auto& sv : savers) {
+        const uint32_t s = tr[sv[0]][sv[1]].stream;
+        if (is_held(s) != held_ones) continue;
         const TrialRes& r = trres[sv[0]][sv[1]];
-        RpEntry& e = c->rp_pool[sv[2]][sv[3]];
+        RpEntry& e = x->rp_pool[sv[2]][sv[3]];
         if (r.state != TR_NEED_R && (r.saved_flags & 1u)) {
           e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags; e.reads_max = r.reads_max;
         } else {
@@ -1891,132 +2035,91 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         }
       }
     };
-    // duplicates are not launched; trials waiting for a saver of this round go in a second launch
+    // duplicates are not launched; trials waiting for a saver of this round go in a second launch set
     // (speculative rounds, K > 1: small files, the sweep's tail) once the saver's sequence is in
     TrialRes dup{};
     dup.state = TR_CANT_BEAT;
-    bool waiting_trials = false, dups = false;
+    bool waiting_trials = false;
     for (int k = 1; k < 3; k++)
-      for (const Trial& t : tr[k]) { waiting_trials |= (t.mode & 64) != 0; dups |= (t.mode & 128) != 0; }
-    if (!waiting_trials && !dups) {
-      if (int r = run_trials(x, c, d_file, tr, so, trres)) return r;
-      finish_savers();
-    } else {
-      std::vector<Trial> t1[3], t2[3];
-      std::vector<uint32_t> i1[3], i2[3];
-      std::vector<TrialRes> r1[3], r2[3];
+      for (const Trial& t : tr[k]) waiting_trials |= (t.mode & 64) != 0;
+    TrialSet SA, SB;                      // A: every trial neither a duplicate nor waiting; B: the waiting ones
+    std::vector<uint32_t> ia[3], ib[3];   // their indices in tr[k]
+    {
+      std::vector<Trial> ta[3];
       for (int k = 0; k < 3; k++) {
         trres[k].assign(tr[k].size(), dup);
         for (uint32_t q = 0; q < tr[k].size(); q++) {
-          if (tr[k][q].mode & 128) continue;
-          const bool w = (tr[k][q].mode & 64) != 0;
-          (w ? t2 : t1)[k].push_back(tr[k][q]);
-          (w ? i2 : i1)[k].push_back(q);
+          if (tr[k][q].mode & (64 | 128)) continue;
+          ta[k].push_back(tr[k][q]);
+          ia[k].push_back(q);
         }
       }
-      if (int r = run_trials(x, c, d_file, t1, so, r1)) return r;
+      trials_order(x, ta, SA);
+    }
+    auto collect = [&](const TrialSet& S, const std::vector<uint32_t>* idx) {
+      std::vector<TrialRes> rr[3];
+      trials_results(S, rr);
       for (int k = 0; k < 3; k++)
-        for (size_t j = 0; j < i1[k].size(); j++) trres[k][i1[k][j]] = r1[k][j];
-      finish_savers();
-      if (waiting_trials) {
-        std::vector<Trial> t3[3];
-        std::vector<uint32_t> i3[3];
-        for (int k = 1; k < 3; k++)
-          for (size_t j = 0; j < t2[k].size(); j++) {
-            Trial& t = t2[k][j];
-            t.mode &= ~64u;
-            const RpEntry& e = c->rp_pool[ss[t.stream].rp][t.clevel - 1];
-            if (e.state == 2 && e.window == t.window) replay_from(t, e, replay_free(x, k, t));
-            tr[k][i2[k][j]].mode = t.mode;
-            if (t.mode & 128) continue;
-            const uint64_t n = x->recs[t.stream].infl_len;
-            if ((t.mode & 8) && (!c->rp.holds(t.rp_syms, 4 * (n + 64)) || t.rp_nsym > n ||
-                                 ((t.mode & 16) && !c->rp.holds(t.rp_tab, 8 * n)))) {
-              std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
-              return ATZ_E_INTERNAL;
-            }
-            t3[k].push_back(t);
-            i3[k].push_back(i2[k][j]);
+        for (size_t j = 0; j < idx[k].size(); j++) trres[k][idx[k][j]] = rr[k][j];
+    };
+    if (int r = trials_first(x, c, d_file, SA, so)) return r;
+    if (waiting_trials) {   // the savers complete (reruns included) before the trials that wait for them
+      if (int r = trials_rerun(x, c, d_file, SA, so, nullptr)) return r;
+      collect(SA, ia);
+      finish_savers(false);
+      std::vector<Trial> t3[3];
+      for (int k = 1; k < 3; k++)
+        for (uint32_t q = 0; q < tr[k].size(); q++) {
+          Trial& t = tr[k][q];
+          if (!(t.mode & 64)) continue;
+          t.mode &= ~64u;
+          const RpEntry& e = x->rp_pool[ss[t.stream].rp][t.clevel - 1];
+          if (e.state == 2 && e.window == t.window) replay_from(t, e, replay_free(x, k, t));
+          if (t.mode & 128) continue;
+          const uint64_t n = x->recs[t.stream].infl_len;
+          if ((t.mode & 8) && (!x->rp_arena.holds(t.rp_syms, 4 * (n + 64)) || t.rp_nsym > n ||
+                               ((t.mode & 16) && !x->rp_arena.holds(t.rp_tab, 8 * n)))) {
+            std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
+            return ATZ_E_INTERNAL;
           }
-        if (int r = run_trials(x, c, d_file, t3, so, r2)) return r;
-        for (int k = 1; k < 3; k++)
-          for (size_t j = 0; j < i3[k].size(); j++) trres[k][i3[k][j]] = r2[k][j];
-      }
-    }
-    if (dedup_on() && x->depth_pin.p) level_record(x, c, ss, tr[2], trres[2]);
-    auto tc = std::chrono::steady_clock::now();
-    for (int k = 1; k < 3; k++)
-      for (size_t q = 0; q < tr[k].size(); q++) {
-        c->stats.n_trials_replayed += (trres[k][q].saved_flags >> 2) & 1u;
-        c->stats.n_replay_checked += (tr[k][q].mode >> 4) & 1u;
-        c->stats.n_trials_duplicate += (tr[k][q].mode >> 7) & 1u;
-        if (timing_on() && (tr[k][q].mode & 24) != 8 && !(tr[k][q].mode & 128)) {
-          if (c->diag_need.size() <= tr[k][q].stream) c->diag_need.resize(tr[k][q].stream + 1, 0);
-          c->diag_need[tr[k][q].stream] |= (uint16_t)(1u << tr[k][q].memlevel);
+          t3[k].push_back(t);
+          ib[k].push_back(q);
         }
-      }
-    c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
-    c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
-    if (timing_level() >= 2)
-      std::fprintf(stderr, "atz: pipe %d round %llu at %.1f ms: active %zu K %u trials %zu/%zu/%zu list %.1f chains %.1f (%zu builds) trials %.1f ms\n",
-                   c->id, (unsigned long long)rounds, std::chrono::duration<double, std::milli>(ta - t0).count(), active.size(), K,
-                   tr[0].size(), tr[1].size(), tr[2].size(), std::chrono::duration<double, std::milli>(ta - tl0).count(),
-                   std::chrono::duration<double, std::milli>(tb - ta).count(), nbuild,
-                   std::chrono::duration<double, std::milli>(tc - tb).count());
-    for (int k = 0; k < 3; k++)
-      for (size_t q = 0; q < tr[k].size(); q++) {
-        const TrialRes& r = trres[k][q];
-        const uint64_t C = x->recs[tr[k][q].stream].comp_len;
-        c->stats.trial_parsed_bytes += r.parsed;
-        c->stats.n_fast_fallbacks += r.fallbacks & 0xffffffffull;
-        c->stats.n_fast_restarts += r.fallbacks >> 32;
-        c->stats.trial_cyc_total += r.cyc_total; c->stats.trial_cyc_tree += r.cyc_tree;
-        c->stats.trial_cyc_emit += r.cyc_emit; c->stats.trial_blocks += r.blocks;
-        c->stats.trial_cyc_heap += r.cyc_heap; c->stats.trial_cyc_fallback += r.cyc_fallback;
-        c->stats.trial_symbols += r.symbols;
-        uint64_t* gk = c->kind[k][tr[k][q].clevel];
-        gk[0]++; gk[1] += r.cyc_total; gk[2] += r.cyc_tree; gk[3] += r.cyc_emit; gk[4] += r.cyc_heap;
-        gk[5] += r.cyc_fallback; gk[6] += r.parsed; gk[7] += r.symbols; gk[8] += r.cyc_scan; gk[9] += r.cyc_send;
-        for (int i = 0; i < 4; i++) gk[10 + i] += r.cyc_sec[i];
-        // SURVEY.md s8d: trial input read + compare read (bytes emitted and compared against the original)
-        if (!(tr[k][q].mode & 128))   // duplicates are not launched
-          c->stats.k_trial_alg_bytes += x->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
-      }
-    if (timing_on()) {   // slowest trials of the round (diagnostics)
-      std::vector<std::pair<uint64_t, std::pair<int, size_t>>> top;
-      for (int k = 0; k < 3; k++)
-        for (size_t q = 0; q < tr[k].size(); q++) top.push_back({trres[k][q].cyc_total, {k, q}});
-      std::sort(top.begin(), top.end(), [](auto& a, auto& b) { return a.first > b.first; });
-      for (size_t i = 0; i < top.size() && i < 3; i++) {
-        const Trial& t = tr[top[i].second.first][top[i].second.second];
-        const TrialRes& r = trres[top[i].second.first][top[i].second.second];
-        std::fprintf(stderr, "atz: round %llu slow trial: stream %u I=%llu c%u w%u m%u state %u cyc %.1fM syms %llu blocks %llu "
-                     "fallbacks %llu tree %.1fM emit %.1fM (heap %.1fM scan %.1fM send %.1fM fb %.1fM)\n", (unsigned long long)rounds, t.stream,
-                     (unsigned long long)x->recs[t.stream].infl_len, t.clevel, t.window, t.memlevel, r.state,
-                     r.cyc_total / 1e6, (unsigned long long)r.symbols, (unsigned long long)r.blocks,
-                     (unsigned long long)(r.fallbacks & 0xffffffffull), r.cyc_tree / 1e6, r.cyc_emit / 1e6, r.cyc_heap / 1e6,
-                     r.cyc_scan / 1e6, r.cyc_send / 1e6, r.cyc_fallback / 1e6);
-      }
+      trials_order(x, t3, SB);
+      if (int r = trials_first(x, c, d_file, SB, so)) return r;
+      collect(SB, ib);
+    } else {
+      collect(SA, ia);
     }
-    // apply the reference's sequential rule per stream, in list order
-    std::vector<DiffJob> dj;
-    std::vector<uint32_t> dj_stream;   // ~0u: superseded by a later improvement of the same stream
-    uint64_t dpos = 0;
-    for (size_t a = 0; a < active.size(); a++) {
+    auto tc = std::chrono::steady_clock::now();
+    // The reference's sequential rule per stream, in list order (main.cpp:685-700), walked up to the
+    // stream's stop; with defer, a walk that reaches a trial still to be rerun (TR_NEED_R) waits there
+    // (held) and resumes after the reruns.  A stream's live diff job (its latest improvement within the
+    // recomp threshold) is extracted by flush_diffs.
+    struct PendDiff { bool live = false; DiffJob d{}; };
+    std::vector<PendDiff> pend(active.size());
+    std::vector<uint32_t> jpos(mbeg.begin(), mbeg.end() - 1);
+    auto walk = [&](size_t a, bool defer) -> int {
       const uint32_t s = active[a];
       StreamState& st = ss[s];
       const uint64_t C = x->recs[s].comp_len;
       const uint32_t phase0 = st.phase;
-      int64_t last_dj = -1;
-      for (uint32_t j = mbeg[a]; j < mbeg[a + 1]; j++) {
+      held[a] = 0;
+      for (uint32_t j = jpos[a]; j < mbeg[a + 1]; j++) {
         if (st.phase != phase0) { nspec += mbeg[a + 1] - j; break; }   // stopped earlier this round
         const Trial& t = tr[mine[j].first][mine[j].second];
         const TrialRes& r = trres[mine[j].first][mine[j].second];
-        if (r.state == TR_NEED_R) {   // deferred rerun: next round, with its whole match table
-          st.full_at = st.idx;
-          nspec += mbeg[a + 1] - j - 1;
-          c->stats.n_trials_rerun++;
-          break;
+        if (r.state == TR_NEED_R) {
+          if (!defer) return ATZ_E_INTERNAL;   // every rerun a walk waits for has run
+          if (flow) {   // rerun as the stream's next step (its later trials of this round are discarded)
+            st.full_at = st.idx;
+            nspec += mbeg[a + 1] - j - 1;
+            c->stats.n_trials_rerun++;
+            break;
+          }
+          jpos[a] = j;
+          held[a] = 1;
+          return 0;
         }
         st.trials++;
         ntr++;
@@ -2029,18 +2132,15 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
           st.c = t.clevel; st.w = t.window; st.m = t.memlevel;
           st.first_diff = -1;
           st.rawdiff.clear(); st.diffval.clear();
-          if (last_dj >= 0) { dj_stream[last_dj] = ~0u; last_dj = -1; }
+          pend[a].live = false;   // an earlier improvement's diffs are superseded
           if (r.ident == C) fullmatch = true;
           else {
             if (r.ident + x->o.mismatch_tol >= C) fullmatch = true;
             if (C - r.ident <= x->o.recomp_tresh) {     // diffs are only ever written for recomp streams
-              DiffJob d;
+              DiffJob& d = pend[a].d;
               d.out_off = t.out_off; d.out_len = r.out_len; d.orig_off = x->recs[s].offset;
-              d.comp_len = C; d.dst = dpos; d.cap = C - r.ident;
-              dpos += d.cap;
-              last_dj = (int64_t)dj.size();
-              dj.push_back(d);
-              dj_stream.push_back(s);
+              d.comp_len = C; d.dst = 0; d.cap = C - r.ident;
+              pend[a].live = true;
             }
           }
         }
@@ -2057,8 +2157,24 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
           }
         }
       }
-    }
-    if (!dj.empty()) {
+      jpos[a] = mbeg[a + 1];
+      return 0;
+    };
+    // mismatch lists (main.cpp:699-714) of the live diff jobs of streams `which`, from the trials' outputs
+    auto flush_diffs = [&](const std::vector<size_t>& which) -> int {
+      std::vector<DiffJob> dj;
+      std::vector<size_t> dja;
+      uint64_t dpos = 0;
+      for (size_t a : which) {
+        if (!pend[a].live) continue;
+        pend[a].live = false;
+        DiffJob d = pend[a].d;
+        d.dst = dpos;
+        dpos += d.cap;
+        dj.push_back(d);
+        dja.push_back(a);
+      }
+      if (dj.empty()) return 0;
       if (int r = upload(c, c->d_diffjobs, dj.data(), dj.size() * sizeof(DiffJob))) return r;
       if (int r = c->d_diffpos.reserve(dpos * 4 + 64)) return r;
       if (int r = c->d_diffval.reserve(dpos + 64)) return r;
@@ -2079,17 +2195,102 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       kcollect(c);
       for (size_t q = 0; q < dj.size(); q++) {
         if (cnt[q] != dj[q].cap) return ATZ_E_INTERNAL;
-        if (dj_stream[q] == ~0u) continue;
-        StreamState& st = ss[dj_stream[q]];
+        StreamState& st = ss[active[dja[q]]];
         st.rawdiff.assign(pos.begin() + dj[q].dst, pos.begin() + dj[q].dst + dj[q].cap);
         st.diffval.assign(val.begin() + dj[q].dst, val.begin() + dj[q].dst + dj[q].cap);
         st.first_diff = st.rawdiff.empty() ? -1 : (int64_t)st.rawdiff[0];
       }
+      return 0;
+    };
+    // the bookkeeping that reads or writes a stream's state, for streams that are done with this round
+    auto settle = [&](bool held_ones) {
+      finish_savers(held_ones);
+      if (dedup_on() && x->depth_pin.p)
+        level_record(x, ss, tr[2], trres[2], [&](uint32_t s) { return is_held(s) == held_ones; });
+    };
+    for (size_t a = 0; a < active.size(); a++)
+      if (int r = walk(a, true)) return r;
+    settle(false);
+    bool any_held = false;
+    for (uint8_t h : held) any_held |= h != 0;
+    if (any_held) {   // rounds: the reruns of the held streams (every TR_NEED_R trial of theirs: which ones
+                      // the walk needs depends on the trials before)
+      auto want = [&](const Trial& t) { return is_held(t.stream); };
+      if (int r = trials_rerun(x, c, d_file, SA, so, want)) return r;
+      collect(SA, ia);
+      if (waiting_trials) {
+        if (int r = trials_rerun(x, c, d_file, SB, so, want)) return r;
+        collect(SB, ib);
+      }
+      for (size_t a = 0; a < active.size(); a++)
+        if (held[a]) {
+          held[a] = 0;
+          if (int r = walk(a, false)) return r;
+          held[a] = 1;   // (settle's selector)
+        }
+      settle(true);
     }
-    std::vector<uint32_t> next;
-    next.swap(waiting);   // streams that sat this round out go first
-    for (uint32_t s : active) if (ss[s].phase != 2) next.push_back(s);
-    active.swap(next);
+    {
+      std::vector<size_t> all(active.size());
+      for (size_t a = 0; a < active.size(); a++) all[a] = a;
+      if (int r = flush_diffs(all)) return r;
+    }
+    auto td = std::chrono::steady_clock::now();
+    for (int k = 1; k < 3; k++)
+      for (size_t q = 0; q < tr[k].size(); q++) {
+        c->stats.n_trials_replayed += (trres[k][q].saved_flags >> 2) & 1u;
+        c->stats.n_replay_checked += (tr[k][q].mode >> 4) & 1u;
+        c->stats.n_trials_duplicate += (tr[k][q].mode >> 7) & 1u;
+        if (timing_on() && (tr[k][q].mode & 24) != 8 && !(tr[k][q].mode & 128)) {
+          if (c->diag_need.size() <= tr[k][q].stream) c->diag_need.resize(tr[k][q].stream + 1, 0);
+          c->diag_need[tr[k][q].stream] |= (uint16_t)(1u << tr[k][q].memlevel);
+        }
+      }
+    c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
+    c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
+    if (timing_level() >= 2)
+      std::fprintf(stderr, "atz: pipe %d round %llu at %.1f ms: active %zu K %u trials %zu/%zu/%zu list %.1f chains %.1f (%zu builds) trials %.1f ms, reruns+apply %.1f ms\n",
+                   c->id, (unsigned long long)rounds, std::chrono::duration<double, std::milli>(ta - t0).count(), active.size(), K,
+                   tr[0].size(), tr[1].size(), tr[2].size(), std::chrono::duration<double, std::milli>(ta - tl0).count(),
+                   std::chrono::duration<double, std::milli>(tb - ta).count(), nbuild,
+                   std::chrono::duration<double, std::milli>(tc - tb).count(),
+                   std::chrono::duration<double, std::milli>(td - tc).count());
+    for (int k = 0; k < 3; k++)
+      for (size_t q = 0; q < tr[k].size(); q++) {
+        const TrialRes& r = trres[k][q];
+        const uint64_t C = x->recs[tr[k][q].stream].comp_len;
+        c->stats.trial_parsed_bytes += r.parsed;
+        c->stats.n_fast_fallbacks += r.fallbacks & 0xffffffffull;
+        c->stats.n_fast_restarts += r.fallbacks >> 32;
+        c->stats.trial_cyc_total += r.cyc_total; c->stats.trial_cyc_tree += r.cyc_tree;
+        c->stats.trial_cyc_emit += r.cyc_emit; c->stats.trial_blocks += r.blocks;
+        c->stats.trial_cyc_heap += r.cyc_heap; c->stats.trial_cyc_fallback += r.cyc_fallback;
+        c->stats.trial_symbols += r.symbols;
+        uint64_t* gk = c->kind[k][tr[k][q].clevel];
+        gk[0]++; gk[1] += r.cyc_total; gk[2] += r.cyc_tree; gk[3] += r.cyc_emit; gk[4] += r.cyc_heap;
+        gk[5] += r.cyc_fallback; gk[6] += r.parsed; gk[7] += r.symbols; gk[8] += r.cyc_scan; gk[9] += r.cyc_send;
+        for (int i = 0; i < 4; i++) gk[10 + i] += r.cyc_sec[i];
+        // SURVEY.md s8d: trial input read + compare read (bytes emitted and compared against the original)
+        if (!(tr[k][q].mode & 128))   // duplicates are not launched; a trial never rerun stopped at its prefix
+          c->stats.k_trial_alg_bytes += r.state == TR_NEED_R ? r.parsed
+                                        : x->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
+      }
+    if (timing_on()) {   // slowest trials of the round (diagnostics)
+      std::vector<std::pair<uint64_t, std::pair<int, size_t>>> top;
+      for (int k = 0; k < 3; k++)
+        for (size_t q = 0; q < tr[k].size(); q++) top.push_back({trres[k][q].cyc_total, {k, q}});
+      std::sort(top.begin(), top.end(), [](auto& a, auto& b) { return a.first > b.first; });
+      for (size_t i = 0; i < top.size() && i < 3; i++) {
+        const Trial& t = tr[top[i].second.first][top[i].second.second];
+        const TrialRes& r = trres[top[i].second.first][top[i].second.second];
+        std::fprintf(stderr, "atz: round %llu slow trial: stream %u I=%llu c%u w%u m%u state %u cyc %.1fM syms %llu blocks %llu "
+                     "fallbacks %llu tree %.1fM emit %.1fM (heap %.1fM scan %.1fM send %.1fM fb %.1fM)\n", (unsigned long long)rounds, t.stream,
+                     (unsigned long long)x->recs[t.stream].infl_len, t.clevel, t.window, t.memlevel, r.state,
+                     r.cyc_total / 1e6, (unsigned long long)r.symbols, (unsigned long long)r.blocks,
+                     (unsigned long long)(r.fallbacks & 0xffffffffull), r.cyc_tree / 1e6, r.cyc_emit / 1e6, r.cyc_heap / 1e6,
+                     r.cyc_scan / 1e6, r.cyc_send / 1e6, r.cyc_fallback / 1e6);
+      }
+    }
     c->t_apply += ms_since(tc);
   }
   c->stats.n_trials += ntr; c->stats.n_trials_shortcut += nsc; c->stats.n_rounds = rounds; c->stats.n_hazard += nhz;
@@ -2120,16 +2321,15 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
 // bound by its rounds' slowest trials instead; with >= 8 hardware queues in the process
 // (GPU_MAX_HW_QUEUES, read at HIP init; bench.py sets it for such runs) six pipes overlap more rounds:
 // a 12 500-stream share 696-710 vs 628-655 MB/s on one MI355X (25 000: 904 vs 923, so only below 16 000).
+// (Read once, thread-safely; GPU_MAX_HW_QUEUES only holds if it was set before HIP initialised.)
 static size_t sweep_pipes(size_t n) {
-  static int env = -2, hwq = -1;
-  if (env == -2) {
+  static const std::pair<int, int> cfg = [] {
     const char* e = std::getenv("ATZ_PIPES");
-    env = e ? std::max(1, std::min(8, std::atoi(e))) : -1;
     const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-    hwq = q ? std::atoi(q) : 4;
-  }
-  if (env > 0) return (size_t)env;
-  return n <= 16000 && hwq >= 8 ? 6 : 3;
+    return std::make_pair(e ? std::max(1, std::min(8, std::atoi(e))) : -1, q ? std::atoi(q) : 4);
+  }();
+  if (cfg.first > 0) return (size_t)cfg.first;
+  return n <= 16000 && cfg.second >= 8 ? 6 : 3;
 }
 // The sweep runs while the scan is still producing records: sweep_begin starts one host thread
 // per pipe, sweep_publish hands a range of ready records (inflated, Adler-32 known) to the pipes,
@@ -2146,12 +2346,14 @@ struct SweepRun {
   bool running = false;
 };
 
-static void sweep_close(atz_ctx* c, SweepRun& R) {
-  for (size_t g = 0; g < R.np; g++) {
-    Pipe* p = c->pipes[g].get();
-    std::lock_guard<std::mutex> lk(p->in_mu);
-    p->in_closed = true;
-    p->in_cv.notify_all();
+// abort: the pipes stop at their next round (an error, or a withdrawn speculative scan); else they
+// finish the published streams
+static void sweep_close(atz_ctx* c, SweepRun& R, bool abort = false) {
+  {
+    std::lock_guard<std::mutex> lk(c->sched.mu);
+    c->sched.closed = true;
+    if (abort) c->sched.abort = true;
+    c->sched.cv.notify_all();
   }
   for (auto& t : R.th) t.join();
   R.th.clear();
@@ -2166,6 +2368,10 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
   ss.assign(n_max, StreamState());
   c->chain_off.assign(n_max, {});
   for (auto& a : c->chain_off) a.fill(~0ull);
+  c->chain_arena.reset(CHAIN_CACHE_CAP);
+  c->rp_arena.reset(RP_ARENA_CAP);
+  c->rp_pool.clear();
+  c->rp_pool.reserve(n_max);
   if (int r = c->depth_pin.reserve(n_max * 40 + 64)) return r;
   std::memset(c->depth_pin.p, 0xff, n_max * 40);
   if (c->infl_off.size() < n_max) c->infl_off.resize(n_max);
@@ -2176,37 +2382,38 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
   R.np = std::max<size_t>(1, std::min(sweep_pipes(n_max), (n_max + 255) / 256));
   c->pipes_running = R.np;
   if (int r = ensure_pipes(c, R.np)) return r;
+  {
+    auto& Q = c->sched;
+    std::lock_guard<std::mutex> lk(Q.mu);
+    Q.flow = sched_flow();
+    Q.q.assign(Q.flow ? 1 : R.np, std::deque<uint32_t>());
+    Q.unfinished.assign(Q.flow ? 1 : R.np, 0);
+    Q.closed = false;
+    Q.abort = false;
+  }
   for (size_t g = 0; g < R.np; g++) {
     Pipe* p = c->pipes[g].get();
-    p->streams.clear();
-    p->inbox.clear();
-    p->in_closed = false;
+    p->tmp_chains.clear();
     p->stats = atz_stats_t{};
-    p->chain_used = 0;
-    p->chain_cap = CHAIN_CACHE_CAP / R.np;
-    p->rp.reset();
-    p->rp_pool.clear();
     p->t_list = p->t_chains = p->t_trials = p->t_apply = 0;
     std::memset(p->kind, 0, sizeof(p->kind));
   }
-  static size_t target = 0;   // trials per round and pipe (ATZ_TARGET: tuning)
-  if (!target) { const char* e = std::getenv("ATZ_TARGET"); target = e ? (size_t)std::max(256, std::atoi(e)) : 4096; }   // C4: 16384 758, 8192 774, 4096 787 MB/s
+  static const size_t target = [] {   // trials per round and pipe (ATZ_TARGET: tuning; C4: 16384 758, 8192 774, 4096 787 MB/s)
+    const char* e = std::getenv("ATZ_TARGET");
+    return e ? (size_t)std::max(256, std::atoi(e)) : (size_t)4096;
+  }();
   R.rc.assign(R.np, 0);
   R.running = true;
   for (size_t g = 0; g < R.np; g++)
     R.th.emplace_back([c, &R, &ss, g]() {
-      if (hipSetDevice(c->dev) != hipSuccess) { R.rc[g] = ATZ_E_HIP; return; }
+      if (hipSetDevice(c->dev) != hipSuccess) { R.rc[g] = ATZ_E_HIP; sched_abort(c); return; }
       R.rc[g] = sweep_pipe(c, c->pipes[g].get(), R.d_file, ss, target);
-      if (R.rc[g]) {   // a failed pipe keeps draining nothing: drop what reaches it
-        Pipe* p = c->pipes[g].get();
-        std::lock_guard<std::mutex> lk(p->in_mu);
-        p->inbox.clear();
-      }
+      if (R.rc[g]) sched_abort(c);   // the other pipes stop too (streams this one held never come back)
     });
   return 0;
 }
 
-// records [r0, r1) are inflated (infl_off, adler set): device table entries, then the pipes
+// records [r0, r1) are inflated (infl_off, adler set): device table entries, then the queues
 static int sweep_publish(atz_ctx* c, SweepRun& R, size_t r0, size_t r1) {
   if (r1 <= r0) return 0;
   if (r1 > R.sd.size()) return ATZ_E_INTERNAL;
@@ -2220,12 +2427,17 @@ static int sweep_publish(atz_ctx* c, SweepRun& R, size_t r0, size_t r1) {
   HIPCHK(hipMemcpyAsync(c->d_streams.as<StreamDev>() + r0, R.sd.data() + r0, (r1 - r0) * sizeof(StreamDev),
                         hipMemcpyHostToDevice, c->st));
   HIPCHK(hipStreamSynchronize(c->st));   // the pipes' streams read these tables
-  for (size_t g = 0; g < R.np; g++) {
-    Pipe* p = c->pipes[g].get();
-    std::lock_guard<std::mutex> lk(p->in_mu);
-    // interleaved over the pipes by global index: every pipe gets the same mix of classes and sizes
-    for (size_t s = r0 + (g + R.np - r0 % R.np) % R.np; s < r1; s += R.np) p->inbox.push_back((uint32_t)s);
-    p->in_cv.notify_all();
+  {
+    auto& Q = c->sched;
+    std::lock_guard<std::mutex> lk(Q.mu);
+    if (Q.flow) {
+      for (size_t s = r0; s < r1; s++) Q.q[0].push_back((uint32_t)s);
+      Q.unfinished[0] += r1 - r0;
+    } else {
+      // interleaved over the pipes by global index: every pipe gets the same mix of classes and sizes
+      for (size_t s = r0; s < r1; s++) { Q.q[s % R.np].push_back((uint32_t)s); Q.unfinished[s % R.np]++; }
+    }
+    Q.cv.notify_all();
   }
   R.published = r1;
   return 0;
@@ -2298,7 +2510,7 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
 struct SweepGuard {
   atz_ctx* c;
   SweepRun& R;
-  ~SweepGuard() { if (R.running) sweep_close(c, R); }
+  ~SweepGuard() { if (R.running) sweep_close(c, R, true); }
 };
 
 // the sweep of every record of the context (atz_sweep)
@@ -2495,7 +2707,7 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
     if (spec_abort_test()) same = false;
     if (!same) {
       c->sweep_abort.store(true);
-      sweep_close(c, R);
+      sweep_close(c, R, true);
       c->sweep_abort.store(false);
       c->recs.assign(check.begin(), check.end());   // capacity n_max: no reallocation
       if (int r = sweep_begin(c, d_file, ss, n_max, R)) return r;
@@ -2580,10 +2792,8 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
     }
     c->chain_off.assign(n, {});
     for (auto& a2 : c->chain_off) a2.fill(~0ull);
-    p->streams.clear();
-    for (size_t s = s0; s < s1; s++) p->streams.push_back((uint32_t)s);
-    p->chain_used = 0;
-    p->chain_cap = CHAIN_CACHE_CAP;
+    c->chain_arena.reset(CHAIN_CACHE_CAP);   // the last batch's kernels are done (run_trials synchronised)
+    p->tmp_chains.clear();
     std::vector<std::pair<uint32_t, int>> need;
     for (size_t s = s0; s < s1; s++) if ((params[s] >> 16) > 0) need.push_back({(uint32_t)s, (int)(params[s] & 0xff)});
     if (int r = ensure_chains(c, p, need)) return r;
