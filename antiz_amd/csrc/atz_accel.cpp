@@ -1844,6 +1844,11 @@ static constexpr uint64_t ROUND_BUDGET_BYTES = 24ull << 30;
 //    s3.6: C4 1276-1341 vs 1442-1468 MB/s, a 12 500-stream share 504-598 vs 606-672): the trial
 //    kernels are issue-bound with about a thousand trial waves resident, so freeing streams from the
 //    round barrier adds concurrency the GPU cannot use and costs rounds.
+// ATZ_FULLK=1: speculative rounds (K > 1) build whole match tables up front under the rounds scheduler too
+static bool fullk_on() {
+  static const bool v = [] { const char* e = std::getenv("ATZ_FULLK"); return e && std::atoi(e) != 0; }();
+  return v;
+}
 static bool sched_flow() {
   static int v = -1;
   if (v < 0) { const char* e = std::getenv("ATZ_SCHED"); v = e && std::string(e) == "flow"; }
@@ -1959,7 +1964,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         t.best_ident = st.ident;
         // host-only bit 1: whole match table up front -- a deferred rerun, or any trial of a speculative
         // flow round (K > 1: the sweep's tail, where a rerun's extra step would lengthen the stream's chain)
-        if (st.idx + j == st.full_at || (flow && K > 1)) t.mode |= 2;
+        if (st.idx + j == st.full_at || (K > 1 && (flow || fullk_on()))) t.mode |= 2;
         t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
         int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
@@ -1991,8 +1996,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     }
     size_t nbuild = 0;
     for (auto& q : need) nbuild += x->chain_off[q.first][q.second] == ~0ull;
-    if (int r = ensure_chains(x, c, need)) return r;
-    HIPCHK(hipStreamSynchronize(c->st));
+    if (int r = ensure_chains(x, c, need)) return r;   // (stream-ordered before the match walks: no sync)
     auto tb = std::chrono::steady_clock::now();
     for (int k = 1; k < 3; k++)
       for (Trial& t : tr[k]) {

@@ -5,15 +5,16 @@
 rocprofv3 serialises the dispatches while it collects counters, so every figure describes a kernel
 running alone on the GPU.  Units (MI355X guide, 'rocprofv3 PMC slots' and the cycle-constants table):
 SQ_WAVE_CYCLES, SQ_WAIT_*, SQ_ACTIVE_INST_* and SQ_BUSY_CYCLES count quad-cycles; GRBM_GUI_ACTIVE
-counts GPU cycles over the dispatch.  Capacities used for the fractions (gfx950: 256 CUs, one scalar
+counts GPU cycles over the dispatch summed over the 8 XCDs (elapsed = GRBM_GUI_ACTIVE / 8: k_inflate's
+one dispatch, 78 ms in the kernel trace, reads 1.46e9).  Capacities used for the fractions (gfx950: 256 CUs, one scalar
 unit and 4 SIMD-32 per CU, the sequencer issuing for one SIMD per cycle):
-  salu_issue_frac = SQ_INSTS_SALU / (256 CUs x GRBM_GUI_ACTIVE)      (one SALU per CU per cycle)
-  valu_issue_frac = 2 x SQ_INSTS_VALU / (4 x 256 x GRBM_GUI_ACTIVE)  (wave64 on a SIMD-32: 2 cycles)
-  lds_issue_frac  = SQ_INSTS_LDS / (256 x GRBM_GUI_ACTIVE)           (one LDS instruction per CU per cycle)
+  salu_issue_frac = SQ_INSTS_SALU / (256 CUs x elapsed)      (one SALU per CU per cycle)
+  valu_issue_frac = 2 x SQ_INSTS_VALU / (4 x 256 x elapsed)  (wave64 on a SIMD-32: 2 cycles)
+  lds_issue_frac  = SQ_INSTS_LDS / (256 x elapsed)           (one LDS instruction per CU per cycle)
   wait_frac       = SQ_WAIT_ANY / SQ_WAVE_CYCLES   (waves parked on s_waitcnt / barriers)
   stall_frac      = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (waves ready but not issued: pipe busy, dependency)
   active_frac     = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES
-  waves_resident  = 4 x SQ_WAVE_CYCLES / GRBM_GUI_ACTIVE (mean waves on the GPU while the kernel ran)
+  waves_resident  = 4 x SQ_WAVE_CYCLES / elapsed (mean waves on the GPU while the kernel ran)
 """
 import collections
 import csv
@@ -59,7 +60,7 @@ def main():
                 c[n + "_pass2"] = v
             else:
                 c[n] = v
-        g = c.get("GRBM_GUI_ACTIVE", 0) or 1
+        g = (c.get("GRBM_GUI_ACTIVE", 0) or 8) / 8.0
         wc = c.get("SQ_WAVE_CYCLES", 0) or 1
         e = {"counters": {n: int(v) for n, v in c.items()}}
         e["salu_issue_frac"] = round(c.get("SQ_INSTS_SALU", 0) / (256 * g), 4)
@@ -77,7 +78,7 @@ def main():
     for k in tk:
         for n, v in fam[k]["counters"].items():
             tot[n] += v
-    g = tot.get("GRBM_GUI_ACTIVE", 0) or 1
+    g = (tot.get("GRBM_GUI_ACTIVE", 0) or 8) / 8.0
     wc = tot.get("SQ_WAVE_CYCLES", 0) or 1
     trial = {"salu_issue_frac": round(tot["SQ_INSTS_SALU"] / (256 * g), 4),
              "valu_issue_frac": round(2 * tot["SQ_INSTS_VALU"] / (4 * 256 * g), 4),
