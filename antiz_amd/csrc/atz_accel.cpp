@@ -1849,6 +1849,12 @@ static bool fullk_on() {
   static const bool v = [] { const char* e = std::getenv("ATZ_FULLK"); return e && std::atoi(e) != 0; }();
   return v;
 }
+// ATZ_REBALANCE=0: rounds-scheduler pipes keep their initial share to the end
+static bool rebalance_on() {
+  static const bool v = [] { const char* e = std::getenv("ATZ_REBALANCE"); return !(e && std::atoi(e) == 0); }();
+  return v;
+}
+static constexpr size_t SHARE_MIN = 64;   // streams per part when a pipe splits its share
 static bool sched_flow() {
   static int v = -1;
   if (v < 0) { const char* e = std::getenv("ATZ_SCHED"); v = e && std::string(e) == "flow"; }
@@ -1861,8 +1867,13 @@ static bool sched_take(atz_ctx* x, int g, size_t np, std::vector<uint32_t>& batc
   batch.clear();
   auto stop = [&] { return Q.abort || x->sweep_abort.load(std::memory_order_relaxed); };
   if (!Q.flow) {
+    // a pipe whose own streams are done waits for a share of another's (sched_give) until all are done
     std::deque<uint32_t>& q = Q.q[g];
-    Q.cv.wait(lk, [&] { return stop() || !q.empty() || Q.closed; });
+    auto all_done = [&] {
+      for (size_t u : Q.unfinished) if (u) return false;
+      return true;
+    };
+    Q.cv.wait(lk, [&] { return stop() || !q.empty() || (Q.closed && all_done()); });
     if (stop() || q.empty()) return false;
     batch.assign(q.begin(), q.end());
     q.clear();
@@ -1889,7 +1900,28 @@ static void sched_give(atz_ctx* x, int g, const std::vector<StreamState>& ss, co
   if (!Q.flow) {
     std::vector<uint32_t> front(waiting);
     for (uint32_t s : active) { if (ss[s].phase == 2) done++; else front.push_back(s); }
+    Q.unfinished[g] -= done;
+    // The pipes' shares finish at different times (two of three pipes share a hardware queue; C4: the
+    // last pipe ended 130 ms after the first), so a pipe with streams left splits them with the pipes
+    // whose own streams are done, interleaved (the same mix of classes for each)
+    std::vector<int> idle;
+    for (int p = 0; p < (int)Q.q.size(); p++)
+      if (p != g && Q.unfinished[p] == 0 && Q.q[p].empty()) idle.push_back(p);
+    const size_t parts = std::min(idle.size() + 1, front.size() / SHARE_MIN);
+    if (parts > 1 && rebalance_on()) {
+      std::vector<uint32_t> keep;
+      for (size_t i = 0; i < front.size(); i++) {
+        const size_t k = i % parts;
+        if (k == 0) { keep.push_back(front[i]); continue; }
+        Q.q[idle[k - 1]].push_back(front[i]);
+        Q.unfinished[idle[k - 1]]++;
+        Q.unfinished[g]--;
+      }
+      front.swap(keep);
+    }
     Q.q[g].insert(Q.q[g].begin(), front.begin(), front.end());
+    Q.cv.notify_all();
+    return;
   } else {
     Q.q[0].insert(Q.q[0].begin(), waiting.begin(), waiting.end());
     for (uint32_t s : active) {
