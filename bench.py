@@ -126,6 +126,31 @@ def pmc_traffic():
     return d["k_trial"]["traffic_per_launch"], os.path.relpath(path, ROOT), d.get("code_sha")
 
 
+def pmc_issue():
+    """Issue utilisation of the trial kernels from the newest committed SQ profile (profiles/r*_v*_pmc_sq.json:
+    two rocprofv3 --pmc SQ passes over this bench with GRBM_GUI_ACTIVE, made by tools/pmc_sq_summary.py;
+    dispatches serialised by the profiler).  Fractions of the CU's scalar-issue, VALU-issue and LDS-issue
+    capacity, and of the waves' cycles spent parked on s_waitcnt (wait) or ready but not issued (stall)."""
+    import glob
+    import re
+    files = glob.glob(os.path.join(ROOT, "profiles", "r*_v*_pmc_sq.json"))
+    if not files:
+        return None
+    key = lambda p: tuple(int(x) for x in re.findall(r"r(\d+)_v(\d+)_", os.path.basename(p))[0])
+    path = max(files, key=key)
+    with open(path) as f:
+        d = json.load(f)
+    t = d["k_trial"]
+    out = {k: t[k] for k in ("salu_issue_frac", "valu_issue_frac", "lds_issue_frac", "wait_frac", "stall_frac",
+                             "active_frac", "waves_resident")}
+    out["source"] = os.path.relpath(path, ROOT)
+    out["code_sha"] = d.get("code_sha")
+    inf = d["kernels"].get("k_inflate")
+    if inf:
+        out["k_inflate_salu_issue_frac"] = inf["salu_issue_frac"]
+    return out
+
+
 def aggregate(dt, atz_len, shard_bytes, steps, world, device):
     """Cross-rank reduction of one timed run: max step time over ranks, per-rank ATZ sizes.
     value = bytes all ranks processed / the slowest rank's time (weak scaling: one shard per rank)."""
@@ -142,6 +167,24 @@ def aggregate(dt, atz_len, shard_bytes, steps, world, device):
     total_bytes = shard_bytes * world
     value = total_bytes / 1e6 / (dt / steps)
     return dt, value, [int(g.item()) for g in gathered]
+
+
+def rank_balance(st, world, device):
+    """Per-rank work of the last step (all-gathered): streams swept, trials, shader cycles the trials took
+    (the sweep's work, whatever the clock), sweep wall time; max/mean of the cycles shows how evenly the
+    split (atz_accel.cpp shard_records) shared the work."""
+    import torch
+    import torch.distributed as dist
+    keys = ("n_streams", "n_trials", "trial_cyc_total", "sweep_ms", "k_trial_ms")
+    mine = torch.tensor([float(st[k]) for k in keys], dtype=torch.float64, device=device)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    cols = {k: [float(r[i].item()) for r in allr] for i, k in enumerate(keys)}
+    cyc = cols["trial_cyc_total"]
+    mean = sum(cyc) / len(cyc) if cyc else 0.0
+    out = {k: [int(v) if k != "sweep_ms" and k != "k_trial_ms" else round(v, 1) for v in vals] for k, vals in cols.items()}
+    out["cyc_max_over_mean"] = round(max(cyc) / mean, 4) if mean > 0 else None
+    return out
 
 
 def main():
@@ -273,6 +316,7 @@ def main():
     dt = time.perf_counter() - t0
     shard_bytes = len(data) + sum(len(e[1]) for e in extra) if args.mode == "shards" else len(data) / world
     dt, value, atz_sizes = aggregate(dt, n, shard_bytes, args.steps, world, red_dev)
+    balance = rank_balance(stats[-1], world, red_dev) if world > 1 else None
     ms_per_step = dt * 1000.0 / args.steps
 
     last = stats[-1]
@@ -285,8 +329,10 @@ def main():
     roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
             "achieved_wall": round(achieved_wall, 3), "frac_wall": round(achieved_wall / HBM_PEAK_GBS, 6),
-            "limiter": "not HBM: per-trial serial parse on the scalar + vector issue pipes and dependent LDS "
-                       "latency (DESIGN.md s3.5); the HBM fraction is reported because it is the graded roofline",
+            "limiter": "not HBM: the trial kernels are latency-bound serial parses (see issue: waves parked on "
+                       "s_waitcnt most of their cycles, the CU's scalar issue part-used; DESIGN.md s3.5); the HBM "
+                       "fraction is reported because it is the graded roofline",
+            "issue": pmc_issue(),
             "traffic_unit": "bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE)", "traffic_source": traffic_src,
             "traffic_code_sha": traffic_sha,
             "kernel": "k_trial_{stored,fast,slow}", "launches": last["k_trial_launches"],
@@ -394,6 +440,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "atz_bytes_per_rank": atz_sizes,
+            "rank_balance": balance,
             "atz_parity": atz_check,
             "reconstruct": recon,
             "host_to_host": h2h,

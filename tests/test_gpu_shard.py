@@ -42,11 +42,11 @@ def _worker(rank, world, port, path, chunksize, q):
         with antiz_amd.Context(chunksize=chunksize, device=0) as ctx:
             out, n, st = shard.precompress_sharded(ctx, d, data, out_device="cuda")
             atz = out[:n].cpu().numpy().tobytes() if out is not None else None
-        q.put((rank, atz, st["n_streams"], st["n_recomp"], None))
+        q.put((rank, atz, st["n_streams"], st["n_recomp"], st["trial_cyc_total"], None))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:   # report instead of hanging the parent
-        q.put((rank, None, 0, 0, repr(e)))
+        q.put((rank, None, 0, 0, 0, repr(e)))
 
 
 def _run(world, path, chunksize):
@@ -59,9 +59,9 @@ def _run(world, path, chunksize):
         p.start()
     res = {}
     for _ in range(world):
-        r, atz, ns, nr, err = q.get(timeout=240)
+        r, atz, ns, nr, cyc, err = q.get(timeout=240)
         assert err is None, "rank %d: %s" % (r, err)
-        res[r] = (atz, ns, nr)
+        res[r] = (atz, ns, nr, cyc)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -92,18 +92,6 @@ def test_sharded_equals_single_gpu_and_oracle(sample, world, chunksize):
     assert sum(v[2] for v in res.values()) == st["n_recomp"]
 
 
-def _cost_split(recs, world):
-    """The split atz_shard_sweep makes (atz_accel.cpp shard_records): contiguous record ranges of equal
-    estimated cost, (I_s + 1024) x mean trials of the header class."""
-    import bisect
-    t = [6, 15, 6, 20]
-    cum = [0]
-    for off, typ, cl, il, fl in recs:
-        cum.append(cum[-1] + (il + 1024) * t[typ & 3])
-    cuts = [0] + [bisect.bisect_left(cum, cum[-1] * q // world) for q in range(1, world)] + [len(recs)]
-    return [cuts[q + 1] - cuts[q] for q in range(world)]
-
-
 @pytest.fixture(scope="module")
 def clustered(tmp_path_factory):
     """C4 streams followed by a cluster of C3's PNG-like Z_FILTERED streams (they match no trial, so
@@ -121,6 +109,10 @@ def clustered(tmp_path_factory):
 
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_cost_split_on_clustered_input(clustered, world):
+    """The ranks' record ranges partition the file's records, and the split follows cost, not counts: the
+    last rank, which holds the cluster of PNG-like streams (each runs its class's whole trial list), gets
+    fewer records than an equal split would give it, and the ranks' trial cycles stay within 2x of their
+    mean (the measured balance is reported by bench.py's rank_balance)."""
     import antiz_amd
     path, data, ref = clustered
     with antiz_amd.Context(device=0) as c:
@@ -128,4 +120,7 @@ def test_sharded_cost_split_on_clustered_input(clustered, world):
     res = _run(world, path, 524288)
     assert hashlib.sha256(res[0][0]).hexdigest() == hashlib.sha256(ref).hexdigest()
     counts = [res[r][1] for r in range(world)]
-    assert counts == _cost_split(recs, world)
+    assert sum(counts) == len(recs) and all(n > 0 for n in counts)
+    assert counts[-1] < len(recs) // world
+    cyc = [res[r][3] for r in range(world)]
+    assert max(cyc) <= 2.0 * sum(cyc) / world, cyc
