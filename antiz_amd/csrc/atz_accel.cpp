@@ -434,10 +434,13 @@ struct Pipe {
   std::vector<std::pair<uint32_t, int>> tmp_chains;
   // diagnostics (ATZ_TIMING): bucket builds, and per stream the memLevels a table-reading trial used
   uint64_t diag_builds = 0;
+  std::vector<std::pair<uint32_t, uint32_t>> diag_rt;   // ATZ_TIMING >= 3: every launched trial's realtime span
   std::vector<uint16_t> diag_need;
   int id = 0;
-  // diagnostics (ATZ_TIMING): host phase times, per trial kind x level counters
-  double t_list = 0, t_chains = 0, t_trials = 0, t_apply = 0;
+  // diagnostics (ATZ_TIMING): host phase times, per trial kind x level counters; time in HIP copy calls
+  // (host -> device uploads and result downloads) and in stream synchronisations
+  double t_list = 0, t_chains = 0, t_trials = 0, t_apply = 0, t_copy = 0, t_sync = 0;
+  uint64_t n_copy = 0, n_sync = 0;
   uint64_t kind[3][10][14] = {};
   ~Pipe() {
     if (pst) { hipStreamSynchronize(pst); hipStreamDestroy(pst); }
@@ -542,10 +545,29 @@ static void kcollect(C* c) {
 }
 
 // copy n host bytes into b (device capacity n + slack; the slack is never read from the host)
+template <class C> static void copy_timed(C*, double) {}
+template <> void copy_timed<Pipe>(Pipe* p, double ms) { p->t_copy += ms; p->n_copy++; }
+// a pipe's stream synchronisation, timed (ATZ_TIMING)
+static hipError_t pipe_sync(Pipe* p) {
+  const auto t = std::chrono::steady_clock::now();
+  const hipError_t e = hipStreamSynchronize(p->st);
+  p->t_sync += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+  p->n_sync++;
+  return e;
+}
+// a pipe's copy to or from the host, timed (ATZ_TIMING)
+static hipError_t pipe_copy(Pipe* p, void* dst, const void* src, size_t n, hipMemcpyKind k) {
+  const auto t = std::chrono::steady_clock::now();
+  const hipError_t e = hipMemcpyAsync(dst, src, n, k, p->st);
+  copy_timed(p, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count());
+  return e;
+}
 template <class C>
 static int upload(C* c, DBuf& b, const void* h, size_t n, size_t slack = 4096) {
   if (int r = b.reserve(n + slack)) return r;
+  const auto t = std::chrono::steady_clock::now();
   if (n) HIPCHK(hipMemcpyAsync(b.p, h, n, hipMemcpyHostToDevice, c->st));
+  copy_timed(c, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count());
   return 0;
 }
 
@@ -1537,7 +1559,7 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
 static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepOpts& so, int k, const Trial* h,
                          size_t cnt, size_t base) {
   auto launch1 = [&](const Trial* hh, size_t n1, size_t b1, bool mw) -> int {
-    HIPCHK(hipMemcpyAsync(c->d_trials.as<Trial>() + b1, hh, n1 * sizeof(Trial), hipMemcpyHostToDevice, c->st));
+    HIPCHK(pipe_copy(c, c->d_trials.as<Trial>() + b1, hh, n1 * sizeof(Trial), hipMemcpyHostToDevice));
     SweepArgs A;
     A.file = d_cmp; A.infl = INFL_BASE; A.chains = CHAIN_BASE;
     A.R = c->d_R.as<uint2>();
@@ -1604,9 +1626,8 @@ static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, 
   }
   for (int k = 0; k < 3; k++)
     if (!tr[k].empty())
-      HIPCHK(hipMemcpyAsync(res[k].data(), c->d_tres.as<TrialRes>() + bases[k], tr[k].size() * sizeof(TrialRes),
-                            hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
+      HIPCHK(pipe_copy(c, res[k].data(), c->d_tres.as<TrialRes>() + bases[k], tr[k].size() * sizeof(TrialRes), hipMemcpyDeviceToHost));
+  HIPCHK(pipe_sync(c));
   kcollect(c);
   S.base = base;
   return 0;
@@ -1649,9 +1670,8 @@ static int trials_rerun(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, 
   }
   for (int k = 1; k < 3; k++)
     if (!again[k].empty())
-      HIPCHK(hipMemcpyAsync(rr[k].data(), c->d_tres.as<TrialRes>() + bases[k], again[k].size() * sizeof(TrialRes),
-                            hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
+      HIPCHK(pipe_copy(c, rr[k].data(), c->d_tres.as<TrialRes>() + bases[k], again[k].size() * sizeof(TrialRes), hipMemcpyDeviceToHost));
+  HIPCHK(pipe_sync(c));
   kcollect(c);
   for (int k = 1; k < 3; k++)
     for (size_t q = 0; q < again[k].size(); q++) {
@@ -2018,7 +2038,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     std::vector<std::array<uint32_t, 4>> savers;   // (kind, index in tr[kind], rp_pool entry, level - 1)
     if (replay_on() && x->depth_pin.p) {
       if (int r = ensure_depths(x, c, need, need_b)) return r;
-      HIPCHK(hipStreamSynchronize(c->st));
+      HIPCHK(pipe_sync(c));
       if (dedup_on()) level_dups(x, ss, tr[2]);
       for (int k = 1; k < 3; k++) plan_replay(x, c, ss, k, tr[k], savers);
       need.clear();
@@ -2224,10 +2244,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       std::vector<uint32_t> pos(dpos);
       std::vector<uint8_t> val(dpos);
       std::vector<uint64_t> cnt(dj.size());
-      HIPCHK(hipMemcpyAsync(pos.data(), c->d_diffpos.p, dpos * 4, hipMemcpyDeviceToHost, c->st));
-      HIPCHK(hipMemcpyAsync(val.data(), c->d_diffval.p, dpos, hipMemcpyDeviceToHost, c->st));
-      HIPCHK(hipMemcpyAsync(cnt.data(), c->d_diffcnt.p, dj.size() * 8, hipMemcpyDeviceToHost, c->st));
-      HIPCHK(hipStreamSynchronize(c->st));
+      HIPCHK(pipe_copy(c, pos.data(), c->d_diffpos.p, dpos * 4, hipMemcpyDeviceToHost));
+      HIPCHK(pipe_copy(c, val.data(), c->d_diffval.p, dpos, hipMemcpyDeviceToHost));
+      HIPCHK(pipe_copy(c, cnt.data(), c->d_diffcnt.p, dj.size() * 8, hipMemcpyDeviceToHost));
+      HIPCHK(pipe_sync(c));
       kcollect(c);
       for (size_t q = 0; q < dj.size(); q++) {
         if (cnt[q] != dj[q].cap) return ATZ_E_INTERNAL;
@@ -2310,6 +2330,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         if (!(tr[k][q].mode & 128))   // duplicates are not launched; a trial never rerun stopped at its prefix
           c->stats.k_trial_alg_bytes += r.state == TR_NEED_R ? r.parsed
                                         : x->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
+        if (timing_level() >= 3 && !(tr[k][q].mode & 128)) c->diag_rt.push_back({r.rt0, r.rt1});
       }
     if (timing_on()) {   // slowest trials of the round (diagnostics)
       std::vector<std::pair<uint64_t, std::pair<int, size_t>>> top;
@@ -2431,7 +2452,8 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
     Pipe* p = c->pipes[g].get();
     p->tmp_chains.clear();
     p->stats = atz_stats_t{};
-    p->t_list = p->t_chains = p->t_trials = p->t_apply = 0;
+    p->t_list = p->t_chains = p->t_trials = p->t_apply = p->t_copy = p->t_sync = 0;
+    p->n_copy = p->n_sync = 0;
     std::memset(p->kind, 0, sizeof(p->kind));
   }
   static const size_t target = [] {   // trials per round and pipe (ATZ_TARGET: tuning; C4: 16384 758, 8192 774, 4096 787 MB/s)
@@ -2510,6 +2532,11 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
   if (timing_on()) {
     std::fprintf(stderr, "atz: sweep host: chains %.1f ms (incl. kernels), trials %.1f ms (incl. kernels), apply %.1f ms, total %.1f ms\n",
                  tch, ttr, tap, ms_since(R.t0));
+    for (size_t g = 0; g < np; g++) {
+      Pipe* p = c->pipes[g].get();
+      std::fprintf(stderr, "atz: pipe %zu: %llu copy calls %.1f ms, %llu syncs %.1f ms\n", g, (unsigned long long)p->n_copy,
+                   p->t_copy, (unsigned long long)p->n_sync, p->t_sync);
+    }
     uint64_t nb = 0, nn = 0;
     for (size_t g = 0; g < np; g++) {
       Pipe* p = c->pipes[g].get();
@@ -2520,6 +2547,37 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
     }
     std::fprintf(stderr, "atz: bucket builds %llu, (stream, memLevel) pairs a table-reading trial used %llu\n",
                  (unsigned long long)nb, (unsigned long long)nn);
+  }
+  if (timing_level() >= 3) {   // trials running at once over the sweep (first passes only: reruns overwrite)
+    std::vector<std::pair<uint32_t, int>> ev;
+    for (size_t g = 0; g < np; g++) {
+      Pipe* p = c->pipes[g].get();
+      for (auto& e : p->diag_rt) { ev.push_back({e.first, 1}); ev.push_back({e.second, -1}); }
+      p->diag_rt.clear();
+    }
+    if (!ev.empty()) {
+      std::sort(ev.begin(), ev.end());
+      const uint32_t t0 = ev.front().first, t1 = ev.back().first;
+      double area = 0;
+      int cur = 0, peak = 0;
+      uint32_t last = t0;
+      std::vector<double> bin((size_t)((t1 - t0) / 500000u) + 1, 0.0);   // 5 ms bins (100 MHz clock)
+      for (auto& e : ev) {
+        for (uint32_t a = last; a < e.first;) {
+          const uint32_t b = std::min<uint32_t>(e.first, (a / 500000u + 1u) * 500000u);
+          bin[(size_t)((a - t0) / 500000u)] += (double)cur * (b - a);
+          a = b;
+        }
+        area += (double)cur * (e.first - last);
+        cur += e.second;
+        peak = std::max(peak, cur);
+        last = e.first;
+      }
+      std::fprintf(stderr, "atz: trials in flight: mean %.0f over %.1f ms, peak %d; per 5 ms:", area / std::max<uint32_t>(1, t1 - t0),
+                   (t1 - t0) / 1e5, peak);
+      for (double v : bin) std::fprintf(stderr, " %.0f", v / 500000.0);
+      std::fprintf(stderr, "\n");
+    }
   }
   if (timing_on())
     for (int k = 0; k < 3; k++)

@@ -98,6 +98,7 @@ struct TrialRes {
   uint32_t saved_flags; // bit0: the whole input was parsed (the sequence is complete), bit1: end-of-input
                         // literal, bit2: the trial replayed a saved sequence
   uint32_t reads_max;   // slow parses: (longest prev_length a lazy read improved) << 16 | longest length read
+  uint32_t rt0, rt1;    // diagnostics: s_memrealtime (100 MHz) at the trial's start and end, low 32 bits
   uint32_t pad_;
 };
 enum : uint32_t {

@@ -1979,6 +1979,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     b.cyc_heap = b.cyc_scan = b.cyc_send = 0;
   }
   const uint64_t cstart = clock64();
+  const uint32_t rtstart = (uint32_t)__builtin_amdgcn_s_memrealtime();
   if (wave == 0) init_block(s.f, lane);
   uint32_t hazard = 0;
   // Symbols and block statistics are tallied straight into HBM (syms) and LDS (lfreq / dfreq).
@@ -2737,6 +2738,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     r.saved_syms = sbase;
     r.saved_flags = saved_flags;
     r.reads_max = rmax;
+    r.rt0 = rtstart;
+    r.rt1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
     A.res[t] = r;
   }
 }
