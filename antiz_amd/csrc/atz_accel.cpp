@@ -1567,12 +1567,15 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
     A.res = c->d_tres.as<TrialRes>() + b1; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
     A.adler = x->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)n1;
     dim3 g((uint32_t)n1), b(mw ? MW_THREADS : 64);
+    // ATZ_XLDS=n (diagnostics): n bytes of unused dynamic LDS per trial block, to see how much the
+    // trial kernels' LDS footprint limits the sweep when they share the CUs with the table kernels
+    static const uint32_t xlds = [] { const char* e = std::getenv("ATZ_XLDS"); return e ? (uint32_t)std::atoi(e) : 0u; }();
     kbeg(c, 0);
-    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
-    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw, g, b, 0, c->st, A);
-    else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, 0, c->st, A);
-    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, 0, c->st, A);
-    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
+    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, xlds, c->st, A);
+    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw, g, b, xlds, c->st, A);
+    else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, xlds, c->st, A);
+    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, xlds, c->st, A);
+    else hipLaunchKernelGGL(k_trial_slow, g, b, xlds, c->st, A);
     kend(c);
     KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
     return 0;
@@ -1874,7 +1877,11 @@ static bool rebalance_on() {
   static const bool v = [] { const char* e = std::getenv("ATZ_REBALANCE"); return !(e && std::atoi(e) == 0); }();
   return v;
 }
-static constexpr size_t SHARE_MIN = 64;   // streams per part when a pipe splits its share
+static constexpr size_t SHARE_MIN = 64;
+static size_t kref_pipes() {
+  static const size_t v = [] { const char* e = std::getenv("ATZ_KREF"); return e ? (size_t)std::max(0, std::atoi(e)) : (size_t)0; }();
+  return v;
+}   // streams per part when a pipe splits its share
 static bool sched_flow() {
   static int v = -1;
   if (v < 0) { const char* e = std::getenv("ATZ_SCHED"); v = e && std::string(e) == "flow"; }
@@ -1897,7 +1904,8 @@ static bool sched_take(atz_ctx* x, int g, size_t np, std::vector<uint32_t>& batc
     if (stop() || q.empty()) return false;
     batch.assign(q.begin(), q.end());
     q.clear();
-    unf = batch.size();
+    unf = 0;   // streams not done, over all pipes
+    for (size_t u : Q.unfinished) unf += u;
     return true;
   }
   std::deque<uint32_t>& q = Q.q[0];
@@ -1984,8 +1992,12 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       ~Give() { forget_tmp_chains(x, c); sched_give(x, c->id, ss, a, w); }
     } give{x, c, ss, active, waiting};
     const auto tl0 = std::chrono::steady_clock::now();
+    // speculation depth: `target` trials per round and pipe; ATZ_KREF=n sizes it as if n pipes shared
+    // the unfinished streams (more pipes then overlap more rounds without speculating deeper)
+    const size_t kref = kref_pipes();
     const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, flow ? target * np / std::max<size_t>(1, unf)
-                                                                                : target / active.size()));
+                                                                       : kref ? target * kref / std::max<size_t>(1, unf)
+                                                                              : target / active.size()));
     std::vector<std::pair<uint32_t, int>> need;
     std::vector<uint32_t> need_b;   // per need entry: the trial's walk budget (replay's budget-free test)
     for (int k = 0; k < 3; k++) tr[k].clear();
