@@ -1516,6 +1516,12 @@ static uint32_t mw_max_memlevel() {   // ATZ_MW=m: multi-wave up to memLevel m (
   return (uint32_t)v;
 }
 static bool mw_trial(int kind, uint32_t memlevel) { return kind != 0 && memlevel <= mw_max_memlevel(); }
+// a fast trial whose stream has at most INS_SMALL positions runs on the 2 KiB insertion ring
+// (ATZ_INS16=0: every fast trial on the 32 KiB-position ring)
+static bool ins_small(atz_ctx* x, const Trial& t) {
+  static const bool on = [] { const char* e = std::getenv("ATZ_INS16"); return !(e && std::atoi(e) == 0); }();
+  return on && x->recs[t.stream].infl_len <= INS_SMALL;
+}
 static uint64_t sym_words(int kind, uint32_t memlevel, uint64_t n) {   // symbol buffer of a trial (u32 units)
   return (mw_trial(kind, memlevel) ? n + 64 : 0) + (1ull << (memlevel + 6)) + 64;
 }
@@ -1545,9 +1551,12 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
                (uint64_t)((t.mode & 8) ? 1 : 4);   // replays skip the match walks
       S.perm[k][q] = (uint32_t)q;
     }
+    // (fast kind: then the trials whose insertion ring fits INS_SMALL bits, a launch of their own)
     std::stable_sort(S.perm[k].begin(), S.perm[k].end(), [&](uint32_t a, uint32_t b) {
       const bool ma = mw_trial(k, in[k][a].memlevel), mb = mw_trial(k, in[k][b].memlevel);
-      return ma != mb ? ma : key[a] > key[b];
+      if (ma != mb) return ma;
+      const bool sa = k == 1 && ins_small(x, in[k][a]), sb = k == 1 && ins_small(x, in[k][b]);
+      return sa != sb ? sa : key[a] > key[b];
     });
     S.tr[k].resize(n);
     for (size_t q = 0; q < n; q++) S.tr[k][q] = in[k][S.perm[k][q]];
@@ -1555,10 +1564,11 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
   }
   S.base = 0;
 }
-// the trial kernels over h[0, cnt) (one kind, multi-wave ones first), at slots [base, base + cnt)
+// the trial kernels over h[0, cnt) (one kind, multi-wave ones first, each group's small-ring fast trials
+// first), at slots [base, base + cnt)
 static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepOpts& so, int k, const Trial* h,
                          size_t cnt, size_t base) {
-  auto launch1 = [&](const Trial* hh, size_t n1, size_t b1, bool mw) -> int {
+  auto launch1 = [&](const Trial* hh, size_t n1, size_t b1, bool mw, bool small) -> int {
     HIPCHK(pipe_copy(c, c->d_trials.as<Trial>() + b1, hh, n1 * sizeof(Trial), hipMemcpyHostToDevice));
     SweepArgs A;
     A.file = d_cmp; A.infl = INFL_BASE; A.chains = CHAIN_BASE;
@@ -1572,20 +1582,24 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
     static const uint32_t xlds = [] { const char* e = std::getenv("ATZ_XLDS"); return e ? (uint32_t)std::atoi(e) : 0u; }();
     kbeg(c, 0);
     if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, xlds, c->st, A);
-    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw, g, b, xlds, c->st, A);
-    else if (k == 1) hipLaunchKernelGGL(k_trial_fast, g, b, xlds, c->st, A);
+    else if (k == 1 && mw && small) hipLaunchKernelGGL(k_trial_fast_mw<INS_SMALL>, g, b, xlds, c->st, A);
+    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw<BITMAP_BITS>, g, b, xlds, c->st, A);
+    else if (k == 1 && small) hipLaunchKernelGGL(k_trial_fast<INS_SMALL>, g, b, xlds, c->st, A);
+    else if (k == 1) hipLaunchKernelGGL(k_trial_fast<BITMAP_BITS>, g, b, xlds, c->st, A);
     else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, xlds, c->st, A);
     else hipLaunchKernelGGL(k_trial_slow, g, b, xlds, c->st, A);
     kend(c);
     KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
     return 0;
   };
-  size_t m = 0;
-  while (m < cnt && mw_trial(k, h[m].memlevel)) m++;
-  if (m)
-    if (int r = launch1(h, m, base, true)) return r;
-  if (cnt > m)
-    if (int r = launch1(h + m, cnt - m, base + m, false)) return r;
+  size_t i = 0;
+  while (i < cnt) {   // runs of equal (multi-wave, small ring): trials_order made them contiguous
+    const bool mw = mw_trial(k, h[i].memlevel), small = k == 1 && ins_small(x, h[i]);
+    size_t j = i + 1;
+    while (j < cnt && mw_trial(k, h[j].memlevel) == mw && (k == 1 && ins_small(x, h[j])) == small) j++;
+    if (int r = launch1(h + i, j - i, base + i, mw, small)) return r;
+    i = j;
+  }
   return 0;
 }
 // First pass: match-table prefixes, every trial once.  Chain tables must exist.

@@ -906,12 +906,18 @@ struct TrialShared {
   // used while a block is emitted, when the parse is paused (like TreeScratch during build_tree)
 };
 
+// INS: bits of the insertion ring, position mod INS.  32768 serves every stream; a stream of at most
+// 16384 positions never aliases in 16384 bits, and its trials take 2 KiB less LDS (14 waves per CU
+// instead of 11: the fast kind is the LDS-bound one)
+template <uint32_t INS>
 struct TrialSharedFast {
+  static constexpr uint32_t INS_BITS = INS;
   TrialShared t;
   uint64_t ring[512];   // match-table entries around the parse window (RING_SLOW)
-  uint32_t ins[BITMAP_BITS / 32];   // insertion ring (InsRing)
+  uint32_t ins[INS / 32];   // insertion ring (InsRing)
   uint32_t holes[HOLE_SLOTS];   // position + 1 of the latest non-inserted position with hash & (SLOTS-1)
 };
+static constexpr uint32_t INS_SMALL = 16384;
 
 static constexpr uint32_t RING_SLOW = 512;   // >= 127 + 2 * 258 + 64: a walk never leaves the ring
 struct TrialSharedSlow {
@@ -953,10 +959,12 @@ struct MWPart {
   MWFlusher fl[MW_F];
   MWCtl ctl;
 };
+template <uint32_t INS>
 struct TrialSharedFastMW {
+  static constexpr uint32_t INS_BITS = INS;
   TrialShared t;
   uint64_t ring[512];
-  uint32_t ins[BITMAP_BITS / 32];
+  uint32_t ins[INS / 32];
   uint32_t holes[HOLE_SLOTS];
   MWPart mw;
 };
@@ -965,9 +973,9 @@ struct TrialSharedSlowMW {
   uint64_t ring[RING_SLOW];
   MWPart mw;
 };
-static_assert(sizeof(TrialSharedFastMW) <= 64 * 1024 && sizeof(TrialSharedSlowMW) <= 64 * 1024, "static LDS of a block");
+static_assert(sizeof(TrialSharedFastMW<BITMAP_BITS>) <= 64 * 1024 && sizeof(TrialSharedSlowMW) <= 64 * 1024, "static LDS of a block");
 template <typename T> struct HasMW { static constexpr bool value = false; };
-template <> struct HasMW<TrialSharedFastMW> { static constexpr bool value = true; };
+template <uint32_t INS> struct HasMW<TrialSharedFastMW<INS>> { static constexpr bool value = true; };
 template <> struct HasMW<TrialSharedSlowMW> { static constexpr bool value = true; };
 __device__ __forceinline__ uint32_t ld_acq(const LDS uint32_t& x) {
   return uni(__hip_atomic_load(&x, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -2176,10 +2184,11 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     // window's own holes are entered before the check, so a hole behind the node only makes the
     // check conservative (slot collisions likewise).
     LDS uint32_t* holes = (LDS uint32_t*)shm.holes;
-    LDS uint32_t* ins = (LDS uint32_t*)shm.ins;   // insertion bits, position mod BITMAP_BITS
+    LDS uint32_t* ins = (LDS uint32_t*)shm.ins;   // insertion bits, position mod SH::INS_BITS
+    constexpr uint32_t INS_MASK = SH::INS_BITS / 32 - 1;
     for (int i = lane; i < (int)HOLE_SLOTS; i += 64) holes[i] = 0;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    auto ins_get = [&](uint32_t q) -> bool { return (ins[(q >> 5) & (BITMAP_BITS / 32 - 1)] >> (q & 31)) & 1u; };
+    auto ins_get = [&](uint32_t q) -> bool { return (ins[(q >> 5) & INS_MASK] >> (q & 31)) & 1u; };
     // insertion bits and holes of the positions [lo, hi) covered by path nodes; cover(p) gives the
     // node y <= p covering p and its match length (0: literal).  cover runs with all lanes active
     // (it may shuffle: a lane outside EXEC would read as 0).
@@ -2200,7 +2209,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
           const uint32_t sh = 32u * (uint32_t)lane;
           const uint32_t m = (uint32_t)(sm >> sh), bv = (uint32_t)(bits >> sh);
           if (m) {
-            LDS uint32_t& w = ins[((c0 + sh) >> 5) & (BITMAP_BITS / 32 - 1)];
+            LDS uint32_t& w = ins[((c0 + sh) >> 5) & INS_MASK];
             w = (w & ~m) | (bv & m);
           }
         }
@@ -2752,8 +2761,9 @@ __global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_stored(SweepArgs
   __shared__ struct { TrialShared t; uint64_t ring[(STAGE_WORDS + 1) / 2]; } shm;   // ring: staging only
   trial_body<0>(A, shm, threadIdx.x);
 }
+template <uint32_t INS>   // INS_SMALL: streams of at most INS_SMALL positions only (host side)
 __global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_fast(SweepArgs A) {
-  __shared__ TrialSharedFast shm;
+  __shared__ TrialSharedFast<INS> shm;
   trial_body<1>(A, shm, threadIdx.x);
 }
 __global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_slow(SweepArgs A) {
@@ -2762,8 +2772,9 @@ __global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_slow(SweepArgs A
 }
 // multi-wave trials (small blocks): wave 0 parses, waves 1..MW_F flush
 static constexpr uint32_t MW_THREADS = 64 * (1 + MW_F);
+template <uint32_t INS>
 __global__ __launch_bounds__(MW_THREADS, TRIAL_SLOW_WAVES) void k_trial_fast_mw(SweepArgs A) {
-  __shared__ TrialSharedFastMW shm;
+  __shared__ TrialSharedFastMW<INS> shm;
   trial_body<1>(A, shm, (int)(threadIdx.x & 63));
 }
 __global__ __launch_bounds__(MW_THREADS, TRIAL_SLOW_WAVES) void k_trial_slow_mw(SweepArgs A) {
