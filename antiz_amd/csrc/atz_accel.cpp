@@ -227,6 +227,7 @@ struct Rec {
   int type;
   uint32_t flags;
   uint64_t arena_off = ~0ull;   // scan output kept in the arena (complete), else ~0
+  bool noshort = false;         // k_inflate's INF_HINT_NOSHORT (the multi-GPU split's cost estimate)
 };
 
 struct StreamState {
@@ -735,7 +736,7 @@ static uint64_t rd8(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); retur
 struct ScanCand { uint32_t chunk; int32_t type; uint64_t i; };
 // pending stream: its bytes are chunk j0 from i0 plus the napp following chunk buffers (size
 // bytes); they are materialized only for a second refill (rare)
-struct ScanPend { uint64_t off; int type; int state; uint32_t j0, napp; uint64_t i0, size; uint64_t in, out; long spec_chunk; int refills; };
+struct ScanPend { uint64_t off; int type; int state; uint32_t j0, napp; uint64_t i0, size; uint64_t in, out; long spec_chunk; int refills; bool noshort; };
 struct ScanState {
   std::vector<Chunk> chunks;
   std::vector<ScanCand> cands;
@@ -858,7 +859,10 @@ static long scan_select(const ScanState& S, uint32_t j, uint64_t i0, std::vector
     const InfRes& r = S.cres[k];
     if (r.consumed <= 16) continue;
     if (r.status == INF_END) {
-      if (out) out->push_back({cd.i + ch.co, r.consumed, r.produced, cd.type, 0, r.arena_off});
+      if (out) {
+        out->push_back({cd.i + ch.co, r.consumed, r.produced, cd.type, 0, r.arena_off});
+        out->back().noshort = (r.err & INF_HINT_NOSHORT) != 0;
+      }
       i = cd.i + r.consumed;
     } else if (r.consumed == ch.len - cd.i) {
       return (long)k;
@@ -1058,6 +1062,7 @@ static int scan_replay(atz_ctx* c, const uint8_t* h, ScanState& S, uint32_t ja, 
       }
       if (st == INF_END) {
         recs.push_back({pd.off, pd.in, pd.out, pd.type, 1});
+        recs.back().noshort = pd.noshort;
         i = ch.len - avail;
       }
       S.need_more = avail == 0;
@@ -1069,6 +1074,7 @@ static int scan_replay(atz_ctx* c, const uint8_t* h, ScanState& S, uint32_t ja, 
         S.need_more = true;
         pd.off = cd.i + ch.co; pd.type = cd.type; pd.state = (int)S.cres[k].status;
         pd.in = S.cres[k].consumed; pd.out = S.cres[k].produced;
+        pd.noshort = (S.cres[k].err & INF_HINT_NOSHORT) != 0;
         pd.j0 = j; pd.i0 = cd.i; pd.napp = 0;
         pd.size = cd.i == 0 ? ch.len : ch.len - cd.i;
         pd.spec_chunk = (i == 0 && S.pend0[j] == k) ? (long)j : -2;
@@ -3187,16 +3193,25 @@ static void shard_range(uint32_t nch, int rank, int world, uint32_t& ja, uint32_
 // estimated cost.  A stream's sweep costs about I_s x the trials it runs, and the trial count is set
 // by its header class: the class's list (main.cpp:487-560) is walked until the stream's own
 // parameters are reached.  Mean trials per stream measured with the oracle on C4 (uniform clevel /
-// memLevel): FLEVEL 0 5.8, 1 14.7, 2 5.5, 3 10.3; FLEVEL 3 streams that match nothing (C3's
-// PNG-like Z_FILTERED streams) run all 81, so class 3 is weighted between the two.  Every rank
-// computes the same split from the same record list.  Records another rank's scan decoded are
-// inflated again here (their scan output stays in that rank's arena).
+// memLevel): FLEVEL 0 5.8, 1 14.7, 2 5.5, 3 10.3.  A stream that matches no entry runs the whole
+// list (81-82 entries): the scan flags the likely ones (Rec::noshort, k_inflate's first-block test:
+// Z_FILTERED output such as C3's PNG-like streams, which no list entry reproduces).  Every rank
+// computes the same split from the same record list (the hints travel in the scan blobs).  Records
+// another rank's scan decoded are inflated again here (their scan output stays in that rank's arena).
+static bool split_hint_on() {   // ATZ_SPLIT_HINT=0: round 3's fixed class weights (class 3: 20), no hint
+  static int v = -1;
+  if (v < 0) { const char* e = std::getenv("ATZ_SPLIT_HINT"); v = e ? std::atoi(e) : 1; }
+  return v != 0;
+}
+static uint64_t shard_cost(const Rec& r) {
+  static constexpr uint64_t trials_by_class[4] = {6, 15, 6, 10};
+  if (!split_hint_on()) return (r.infl_len + 1024) * ((r.type & 3) == 3 ? 20 : trials_by_class[r.type & 3]);
+  return (r.infl_len + 1024) * (r.noshort ? 81 : trials_by_class[(uint32_t)r.type & 3u]);
+}
 static void shard_records(const std::vector<Rec>& recs, int rank, int world, size_t& r0, size_t& r1) {
-  static constexpr uint64_t trials_by_class[4] = {6, 15, 6, 20};
   const size_t n = recs.size();
   std::vector<uint64_t> cum(n + 1, 0);
-  for (size_t s = 0; s < n; s++)
-    cum[s + 1] = cum[s] + (recs[s].infl_len + 1024) * trials_by_class[(uint32_t)recs[s].type & 3u];
+  for (size_t s = 0; s < n; s++) cum[s + 1] = cum[s] + shard_cost(recs[s]);
   auto cut = [&](int q) -> size_t {   // first record whose cost starts at or after q/world of the total
     if (q <= 0) return 0;
     if (q >= world) return n;
@@ -3228,7 +3243,9 @@ static int shard_scan_impl(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
   blob[5] = k1 - k0; blob[6] = F;
   blob.reserve(SHARD_HDR + 3 * (k1 - k0) + 4 * (sh.jb - sh.ja));
   for (size_t k = k0; k < k1; k++) {
-    blob.push_back(S.cres[k].status); blob.push_back(S.cres[k].consumed); blob.push_back(S.cres[k].produced);
+    // status, with the candidate's cost hint in bit 32
+    blob.push_back(S.cres[k].status | ((S.cres[k].err & INF_HINT_NOSHORT) ? 1ull << 32 : 0ull));
+    blob.push_back(S.cres[k].consumed); blob.push_back(S.cres[k].produced);
   }
   for (uint32_t j = sh.ja; j < sh.jb; j++) {
     blob.push_back((uint64_t)(int64_t)S.pend0[j]);
@@ -3267,6 +3284,7 @@ static int shard_sweep_impl(atz_ctx* c, const uint8_t* d_file, const uint8_t* h,
     for (size_t k = k0; k < k1; k++, p += 3) {
       InfRes r{};
       r.status = (uint32_t)p[0]; r.consumed = p[1]; r.produced = p[2]; r.arena_off = ARENA_NONE;
+      r.err = (p[0] >> 32) & 1u ? INF_HINT_NOSHORT : 0u;
       S.cres[k] = r;
     }
     for (uint32_t j = ja; j < jb; j++, p += 4) {
@@ -3438,7 +3456,8 @@ int atz_scan(atz_ctx_t* c, const uint8_t* file, uint64_t len, atz_cand_t** out, 
     if (!*out) return ATZ_E_NOMEM;
     for (size_t s = 0; s < c->recs.size(); s++) {
       (*out)[s].offset = c->recs[s].offset; (*out)[s].comp_len = c->recs[s].comp_len;
-      (*out)[s].infl_len = c->recs[s].infl_len; (*out)[s].type = c->recs[s].type; (*out)[s].flags = c->recs[s].flags;
+      (*out)[s].infl_len = c->recs[s].infl_len; (*out)[s].type = c->recs[s].type;
+      (*out)[s].flags = c->recs[s].flags | (c->recs[s].noshort ? 2u : 0u);
     }
     c->scan_valid = true;
     return ATZ_OK;

@@ -24,9 +24,13 @@ static constexpr uint64_t ARENA_NONE = ~0ull;
 
 enum : uint32_t { INF_END = 0, INF_ERROR = 1, INF_NEED = 2, INF_RETRY = 3 };   // RETRY: rerun with the 32 KiB ring
 
+// InfRes.err bit 31: the first block is dynamic and codes matches, none of length 3-5 (a cost hint
+// for the multi-GPU split; the low bits are the failing check's code)
+static constexpr uint32_t INF_HINT_NOSHORT = 1u << 31;
+
 struct InfRes {
   uint32_t status;    // INF_*
-  uint32_t err;       // diagnostic code of the failing check
+  uint32_t err;       // diagnostic code of the failing check | INF_HINT_NOSHORT
   uint64_t consumed;  // zlib total_in at the stop
   uint64_t produced;  // zlib total_out at the stop
   uint64_t arena_off; // ARENA_OUT jobs: offset of the output slot (ARENA_NONE: none / incomplete)

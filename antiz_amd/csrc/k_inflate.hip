@@ -539,6 +539,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
 
   uint64_t errneed = 0;
   uint32_t errcode = 0;
+  uint32_t hint = 0;   // INF_HINT_NOSHORT (see the dynamic header below)
 #define NEEDB(k) do { if (!has(k)) return R_NEED; } while (0)
 #define FAIL(code, needpos) do { errneed = (needpos); errcode = (code); return R_ERR; } while (0)
 
@@ -692,6 +693,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
     if (flg & 0x20) { NEEDB(32); FAIL(4, pos + 32); }      // preset dictionary: not a stream end
     int last;
     Huff lh, dh;
+    uint32_t nblk_seen = 0;
     do {
       const uint64_t th0 = ATZ_INF_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
       if (ATZ_INF_CLOCKS) nblk++;
@@ -816,6 +818,15 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
           have += copyn;
         }
         if (iuni(lens[256]) == 0) FAIL(9, pos);
+        if (nblk_seen == 0) {
+          // Cost hint for the multi-GPU split, part of no output: the first block codes matches, but
+          // none of length 3-5 (symbols 257-259).  zlib's Z_FILTERED strategy drops those
+          // (Z/deflate.c:1774-1782), and no entry of the reference's trial lists uses it, so such a
+          // stream usually runs its whole list.
+          const uint32_t v = (uint32_t)lane < nlen - 257u ? (uint32_t)lens[257 + lane] : 0u;
+          const uint64_t m = __ballot(v != 0);
+          if (m != 0 && (m & 7u) == 0) hint = INF_HINT_NOSHORT;
+        }
         const uint32_t dcnt = __shfl_down(lcnt, 16, 64);   // lane l: distance codes of length l
         if (build(lh, lens, (int)nlen, 1, true, lcnt)) FAIL(9, pos);
         if (build(dh, lens + nlen, (int)ndist, 2, true, dcnt)) FAIL(9, pos);
@@ -823,6 +834,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
         FAIL(15, pos);                                      // invalid block type
       }
       if (ATZ_INF_CLOCKS) cyc_hdr += __builtin_amdgcn_s_memtime() - th0;
+      nblk_seen++;
       if (type != 0) {   // one (inlined) decode loop for fixed and dynamic blocks
         const int rr = codes(lh, dh);
         if (rr != R_OK) return rr;
@@ -850,7 +862,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
   InfRes o;
   o.arena_off = (rr == R_OK && to_arena) ? arena_off : ARENA_NONE;
   o.produced = prod;
-  o.err = errcode;
+  o.err = errcode | hint;
   if (rr == R_RETRY) {
     o.status = INF_RETRY;
     o.consumed = 0;

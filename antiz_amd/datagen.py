@@ -186,7 +186,13 @@ def gen_c5(seed=5, n_streams=100000, workers=None):
     return gen_c4(seed, n_streams, (10, 15), workers)
 
 
-CONFIGS = {"c1": gen_c1, "c2": gen_c2, "c3": gen_c3, "c4": gen_c4, "c5": gen_c5}
+def gen_c4c3(seed=4, n_streams=100000, c3_bytes=100 * 1000 * 1000, workers=None):
+    """C4 followed by a C3 cluster (its PNG-like Z_FILTERED streams run their whole trial list): the
+    multi-GPU split's balance test (bench.py --workload c4c3), not a BASELINE config."""
+    return gen_c4(seed, n_streams, workers=workers) + gen_c3(seed=3, total=c3_bytes, workers=workers)
+
+
+CONFIGS = {"c1": gen_c1, "c2": gen_c2, "c3": gen_c3, "c4": gen_c4, "c5": gen_c5, "c4c3": gen_c4c3}
 
 
 def cached(name, cache_dir, **kw):

@@ -198,9 +198,10 @@ def main():
     ap.add_argument("--no-recon", action="store_true", help="skip the reconstruct (-r / verify) measurement")
     ap.add_argument("--no-h2h", action="store_true", help="skip the host-to-host (atz_precompress) measurement")
     ap.add_argument("--cache", default=os.environ.get("ATZ_BENCH_CACHE", "/tmp/atz_bench_cache"))
-    ap.add_argument("--workload", choices=("c4", "c5"), default="c4",
+    ap.add_argument("--workload", choices=("c4", "c5", "c4c3"), default="c4",
                     help="c4: the metric's workload (BASELINE configs[3]); c5: configs[4], the same generator with "
-                         "windowBits U10-15 and --brute-window (a measurement beside the metric, not its value)")
+                         "windowBits U10-15 and --brute-window (a measurement beside the metric, not its value); "
+                         "c4c3: C4 followed by a 100 MB C3 cluster, for the split's rank balance at N > 1")
     ap.add_argument("--files-per-gpu", type=int, default=1,
                     help="independent files in flight per GPU (one context and host thread each; shards mode). "
                          "1 = the metric's workload; 2 measures the multi-file throughput mode (DESIGN s3.6)")
@@ -238,7 +239,7 @@ def main():
     import antiz_amd
     from antiz_amd import datagen
 
-    base = 4 if args.workload == "c4" else 5
+    base = 5 if args.workload == "c5" else 4
     seed = base + rank if args.mode == "shards" else base
     nf = max(1, args.files_per_gpu) if args.mode == "shards" else 1
     t0 = time.time()
@@ -407,6 +408,10 @@ def main():
         cpu = cpu_baseline(args.cpu_sample_streams, seed, ctx, args.workload)
 
     if rank == 0:
+        wl = {"c4": "C4: %d zlib streams (clevel U1-9, memLevel U1-9, w15)",
+              "c5": "C5: %d zlib streams (clevel U1-9, memLevel U1-9, windowBits U10-15), --brute-window",
+              "c4c3": "C4 (%d zlib streams) followed by a 100 MB C3 cluster (PDF-like, PNG-like Z_FILTERED, "
+                      "JAR-like)"}[args.workload] % args.streams
         out = {
             "metric": "input MB/s precompressed (1 GB synthetic, 100k streams) at 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -421,19 +426,12 @@ def main():
             "dtype": "u8",
             "data": "synthetic (antiz_amd.datagen %s, seed %s; text from a seeded 20k-word vocabulary)"
                     % (args.workload.upper(), ("%d+rank" if args.mode == "shards" else "%d") % base),
-            "config": ({"workload": "C4: %d zlib streams (clevel U1-9, memLevel U1-9, w15), %.3f GB per GPU, "
-                                    "default thresholds" % (args.streams, len(data) / 1e9)
-                                    if args.workload == "c4" else
-                                    "C5: %d zlib streams (clevel U1-9, memLevel U1-9, windowBits U10-15), %.3f GB "
-                                    "per GPU, --brute-window, default thresholds" % (args.streams, len(data) / 1e9),
+            "config": ({"workload": wl + ", %.3f GB per GPU, default thresholds" % (len(data) / 1e9),
                         "streams_per_gpu": args.streams * nf, "bytes_per_gpu": len(data) + sum(len(e[1]) for e in extra),
                         "files_per_gpu": nf, "parallelism": "stream-sharded dp%d" % world}
                        if args.mode == "shards" or world == 1 else
-                       {"workload": ("C4: one file of %d zlib streams (clevel U1-9, memLevel U1-9, w15)"
-                                     if args.workload == "c4" else
-                                     "C5: one file of %d zlib streams (clevel U1-9, memLevel U1-9, windowBits U10-15), "
-                                     "--brute-window") % args.streams
-                                    + ", %.3f GB, split over %d GPUs, default thresholds" % (len(data) / 1e9, world),
+                       {"workload": "one file, " + wl + ", %.3f GB, split over %d GPUs, default thresholds"
+                                    % (len(data) / 1e9, world),
                         "file_bytes": len(data),
                         "parallelism": "one file: scan by chunk ranges, cost-balanced stream split x%d, RCCL gather"
                                        % world}),

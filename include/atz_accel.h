@@ -45,7 +45,9 @@ typedef struct {
     uint64_t comp_len;   /* streamLength */
     uint64_t infl_len;   /* inflatedLength */
     int32_t  type;       /* offsetType 0..23 */
-    uint32_t flags;      /* bit0: recorded through a chunk-boundary continuation */
+    uint32_t flags;      /* bit0: recorded through a chunk-boundary continuation; bit1: the first block is
+                            dynamic and codes matches but none of length 3-5 (a Z_FILTERED-like stream: the
+                            multi-GPU split's cost hint, not part of the reference's record) */
 } atz_cand_t;
 
 /* ATZdata::streamOffset after Phase 3. */

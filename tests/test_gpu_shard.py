@@ -107,6 +107,72 @@ def clustered(tmp_path_factory):
     return path, data, ref
 
 
+def _first_block_noshort(stream):
+    """The split's cost hint restated (k_inflate.hip, INF_HINT_NOSHORT): the zlib stream's first block is
+    dynamic (RFC 1951 3.2.7) and its literal/length code lengths give codes to some length symbol but to
+    none of 257-259 (lengths 3-5), which zlib's Z_FILTERED never emits (Z/deflate.c:1774-1782)."""
+    pos = [16]
+
+    def bits(n):
+        v = 0
+        for i in range(n):
+            p = pos[0] + i
+            v |= ((stream[p >> 3] >> (p & 7)) & 1) << i
+        pos[0] += n
+        return v
+
+    bits(1)
+    if bits(2) != 2:
+        return False
+    nlen, ndist, ncode = bits(5) + 257, bits(5) + 1, bits(4) + 4
+    order = [16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15]
+    cl = [0] * 19
+    for i in range(ncode):
+        cl[order[i]] = bits(3)
+    # canonical code -> symbol for the code-length alphabet
+    table, code = {}, 0
+    for length in range(1, 8):
+        for sym in range(19):
+            if cl[sym] == length:
+                table[(length, code)] = sym
+                code += 1
+        code <<= 1
+    lens = []
+    while len(lens) < nlen + ndist:
+        c, n = 0, 0
+        while (n, c) not in table:
+            c, n = (c << 1) | bits(1), n + 1
+            assert n <= 7
+        sym = table[(n, c)]
+        if sym < 16:
+            lens.append(sym)
+        elif sym == 16:
+            lens += [lens[-1]] * (3 + bits(2))
+        elif sym == 17:
+            lens += [0] * (3 + bits(3))
+        else:
+            lens += [0] * (11 + bits(7))
+    m = [lens[257 + i] != 0 for i in range(nlen - 257)]
+    return any(m) and not any(m[:3])
+
+
+def test_split_hint_matches_first_block_headers(clustered):
+    """Candidate flag bit1 (k_inflate's first-block test) equals the restatement above on every record,
+    and it marks the PNG-like Z_FILTERED cluster: most of the C3 part's zlib streams run their whole
+    trial list, while the C4 part's streams (default strategy) are almost never marked."""
+    import antiz_amd
+    path, data, _ = clustered
+    with antiz_amd.Context(device=0) as c:
+        recs = c.scan(data)
+    got = [(r[4] >> 1) & 1 for r in recs]
+    want = [int(_first_block_noshort(data[r[0]:r[0] + r[2]])) for r in recs]
+    assert got == want
+    c4_len = len(__import__("antiz_amd.datagen", fromlist=["x"]).gen_c4(seed=43, n_streams=500))
+    c4 = [g for r, g in zip(recs, got) if r[0] < c4_len]
+    c3 = [g for r, g in zip(recs, got) if r[0] >= c4_len]
+    assert sum(c4) <= len(c4) // 50 and sum(c3) >= len(c3) // 5, (sum(c4), len(c4), sum(c3), len(c3))
+
+
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_cost_split_on_clustered_input(clustered, world):
     """The ranks' record ranges partition the file's records, and the split follows cost, not counts: the
