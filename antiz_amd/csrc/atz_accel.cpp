@@ -500,6 +500,8 @@ struct atz_ctx {
   std::atomic<bool> sweep_abort{false};   // the pipes stop at their next round (a withdrawn speculative scan)
   // precompress_dev's large per-call state, kept so its capacity survives the calls
   std::shared_ptr<struct ScanState> scan_keep;
+  // atz_precompress: called once the sweep has every record, with an upper estimate of the ATZ1 size
+  std::function<void(uint64_t)> on_records;
   std::vector<StreamState> ss_keep;
   std::vector<StreamDev> sd_keep;
   // multi-GPU precompress of one file (atz_shard_*): this rank's state between the calls
@@ -1522,10 +1524,11 @@ static uint32_t mw_max_memlevel() {   // ATZ_MW=m: multi-wave up to memLevel m (
   return (uint32_t)v;
 }
 static bool mw_trial(int kind, uint32_t memlevel) { return kind != 0 && memlevel <= mw_max_memlevel(); }
-// a fast trial whose stream has at most INS_SMALL positions runs on the 2 KiB insertion ring
-// (ATZ_INS16=0: every fast trial on the 32 KiB-position ring)
+// ATZ_INS16=1: a fast trial whose stream has at most INS_SMALL positions runs on the 2 KiB insertion
+// ring (more fast trials per CU).  Off by default: measured slower (C4 1295-1332 vs 1476-1482 MB/s,
+// k_trial 814-828 vs 630-646 ms summed; the 12 500-stream share 515-536 vs 670-690; gpurun_out/ins16)
 static bool ins_small(atz_ctx* x, const Trial& t) {
-  static const bool on = [] { const char* e = std::getenv("ATZ_INS16"); return !(e && std::atoi(e) == 0); }();
+  static const bool on = [] { const char* e = std::getenv("ATZ_INS16"); return e && std::atoi(e) != 0; }();
   return on && x->recs[t.stream].infl_len <= INS_SMALL;
 }
 static uint64_t sym_words(int kind, uint32_t memlevel, uint64_t n) {   // symbol buffer of a trial (u32 units)
@@ -2818,6 +2821,11 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
     if (int r = inflate_records(c, d_file, F, 0, r1, *c->slabs[0])) return r;
     if (int r = sweep_publish(c, R, 0, r1)) return r;
     TMARK("scan: speculative records out");
+    if (c->on_records) {   // ATZ1 <= header + every record's descriptor (diffs aside) + payload + the file
+      uint64_t est = F + 4096;
+      for (size_t s = 0; s < r1; s++) est += c->recs[s].infl_len + 64;
+      c->on_records(est);
+    }
     if (int r = scan_continuations(c, h, d_file, S, 0, nch)) return r;
     S.need_more = false;
     S.pd = ScanPend{};
@@ -3500,6 +3508,44 @@ int atz_sweep(atz_ctx_t* c, const atz_cand_t* cands, uint64_t n, atz_result_t* r
   });
 }
 
+// The host ATZ1 buffer of atz_precompress.  A fresh 1.5 GB buffer costs more in first-touch page
+// faults (the kernel zeroing every page: ~155 ms on one thread, measured on the box) than its D2H copy
+// (~28 ms into touched pages, tools/h2h_probe.py), so helper threads allocate and touch a buffer of the
+// estimated size while the GPU sweeps.
+struct HostOut {
+  uint8_t* p = nullptr;
+  uint64_t cap = 0;
+  std::vector<std::thread> th;
+  void start(uint64_t est) {
+    if (p) return;
+    p = (uint8_t*)std::malloc(est + 1);
+    if (!p) return;
+    cap = est;
+    const unsigned T = 4;
+    const uint64_t part = ((est + 1 + T - 1) / T + 4095) & ~4095ull;
+    for (unsigned i = 0; i < T; i++)
+      th.emplace_back([this, i, part]() {
+        const uint64_t a = i * part, b = std::min<uint64_t>(cap + 1, a + part);
+        volatile uint8_t* q = p;
+        for (uint64_t k = a; k < b; k += 4096) q[k] = 0;
+      });
+  }
+  void join() { for (auto& t : th) t.join(); th.clear(); }
+  uint8_t* take(uint64_t n) {   // a buffer of at least n bytes (ownership to the caller)
+    join();
+    uint8_t* r = p;
+    if (r && n > cap + 1) {
+      uint8_t* g = (uint8_t*)std::realloc(r, n);
+      if (!g) { std::free(r); r = nullptr; } else r = g;
+    } else if (!r) {
+      r = (uint8_t*)std::malloc(n);
+    }
+    p = nullptr; cap = 0;
+    return r;
+  }
+  ~HostOut() { join(); std::free(p); }
+};
+
 int atz_precompress(atz_ctx_t* c, const uint8_t* file, uint64_t len, uint8_t** atz, uint64_t* atz_len,
                     atz_stats_t* stats) {
   return guarded([&]() -> int {
@@ -3507,10 +3553,15 @@ int atz_precompress(atz_ctx_t* c, const uint8_t* file, uint64_t len, uint8_t** a
     if (!c || (!file && len) || !atz || !atz_len) return ATZ_E_ARG;
     if (int r = upload(c, c->d_file, file, len)) return r;
     uint64_t al = 0;
+    HostOut ho;
+    c->on_records = [&ho](uint64_t est) { ho.start(est); };
+    struct Reset { atz_ctx* c; ~Reset() { c->on_records = nullptr; } } reset{c};
     if (int r = precompress_dev(c, c->d_file.as<uint8_t>(), file, len, &al, nullptr)) return r;
-    uint8_t* h = (uint8_t*)std::malloc(al + 1);
+    c->on_records = nullptr;
+    uint8_t* h = ho.take(al + 1);
     if (!h) return ATZ_E_NOMEM;
-    HIPCHK(hipMemcpy(h, c->d_atz.p, al, hipMemcpyDeviceToHost));
+    const hipError_t e = hipMemcpy(h, c->d_atz.p, al, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) { std::free(h); HIPCHK(e); }
     *atz = h; *atz_len = al;
     if (stats) *stats = c->stats;
     return ATZ_OK;

@@ -170,12 +170,14 @@ def aggregate(dt, atz_len, shard_bytes, steps, world, device):
 
 
 def rank_balance(st, world, device):
-    """Per-rank work of the last step (all-gathered): streams swept, trials, shader cycles the trials took
-    (the sweep's work, whatever the clock), sweep wall time; max/mean of the cycles shows how evenly the
-    split (atz_accel.cpp shard_records) shared the work."""
+    """Per-rank work of the last step (all-gathered): streams swept, trials, the trials' algorithmic bytes
+    (input parsed + output compared), shader cycles the trials took, sweep wall time.  max/mean
+    of the algorithmic bytes shows how evenly the split (atz_accel.cpp shard_records) shared the work;
+    the cycles say the same on one GPU per rank, but with several ranks sharing one GPU (a gloo
+    rehearsal) they also count the waits the co-running ranks cause."""
     import torch
     import torch.distributed as dist
-    keys = ("n_streams", "n_trials", "trial_cyc_total", "sweep_ms", "k_trial_ms")
+    keys = ("n_streams", "n_trials", "k_trial_alg_bytes", "trial_cyc_total", "sweep_ms", "k_trial_ms")
     mine = torch.tensor([float(st[k]) for k in keys], dtype=torch.float64, device=device)
     allr = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(allr, mine)
@@ -184,6 +186,9 @@ def rank_balance(st, world, device):
     mean = sum(cyc) / len(cyc) if cyc else 0.0
     out = {k: [int(v) if k != "sweep_ms" and k != "k_trial_ms" else round(v, 1) for v in vals] for k, vals in cols.items()}
     out["cyc_max_over_mean"] = round(max(cyc) / mean, 4) if mean > 0 else None
+    alg = cols["k_trial_alg_bytes"]
+    amean = sum(alg) / len(alg) if alg else 0.0
+    out["alg_max_over_mean"] = round(max(alg) / amean, 4) if amean > 0 else None
     return out
 
 

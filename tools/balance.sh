@@ -8,7 +8,7 @@ tag=${1:-bal}; W=${2:-8}
 out=gpurun_out/$tag; mkdir -p $out
 export ATZ_BENCH_BACKEND=gloo ATZ_BENCH_CACHE=/tmp/atz_bench_cache
 port=29611
-for wl in c4 c4c3; do
+for wl in ${WLS:-c4 c4c3}; do
   for hint in 1 0; do
     port=$((port + 1))
     echo "== $wl hint=$hint $(date +%T)"
@@ -18,6 +18,6 @@ for wl in c4 c4c3; do
     python3 -c "
 import json,sys
 d=json.loads(open('$out/${wl}_h$hint.json').read().strip().splitlines()[-1])
-b=d['rank_balance']; print('$wl hint=$hint', d['value'], 'MB/s', d['ms_per_step'], 'ms; cyc max/mean', b['cyc_max_over_mean'], 'sweep_ms', b['sweep_ms'], 'streams', b['n_streams'], 'parity', d.get('atz_parity'))"
+b=d['rank_balance']; print('$wl hint=$hint', d['value'], 'MB/s', d['ms_per_step'], 'ms; alg max/mean', b['alg_max_over_mean'], 'cyc max/mean', b['cyc_max_over_mean'], 'sweep_ms', b['sweep_ms'], 'streams', b['n_streams'], 'parity', d.get('atz_parity'))"
   done
 done
