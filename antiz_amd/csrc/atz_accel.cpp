@@ -3508,42 +3508,72 @@ int atz_sweep(atz_ctx_t* c, const atz_cand_t* cands, uint64_t n, atz_result_t* r
   });
 }
 
-// The host ATZ1 buffer of atz_precompress.  A fresh 1.5 GB buffer costs more in first-touch page
-// faults (the kernel zeroing every page: ~155 ms on one thread, measured on the box) than its D2H copy
-// (~28 ms into touched pages, tools/h2h_probe.py), so helper threads allocate and touch a buffer of the
-// estimated size while the GPU sweeps.
+// The host ATZ1 buffer of atz_precompress.  A D2H copy into a fresh 1.5 GB malloc buffer took ~155 ms
+// (first-touch page faults, the kernel zeroing every page, and the runtime's staging of pageable
+// memory), against ~28 ms into pinned memory (tools/h2h_probe.py).  So while the GPU sweeps, a helper
+// thread allocates a buffer of the estimated size, touches its pages and registers it with HIP; the
+// ATZ1 is then copied at DMA speed and the buffer unregistered before the caller gets it (a plain
+// malloc buffer, atz_free).
 struct HostOut {
+  static constexpr uint64_t PIECE = 64ull << 20;   // registered in pieces: no long hold of the driver's locks
   uint8_t* p = nullptr;
   uint64_t cap = 0;
-  std::vector<std::thread> th;
+  std::vector<uint64_t> reg;   // registered pieces [k * PIECE, ...), in order
+  double t_reg = 0;
+  int mode = 2;                // ATZ_H2H_PREP: 0 plain malloc at the end, 1 touch, 2 touch + register
+  std::thread th;
+  HostOut() { const char* e = std::getenv("ATZ_H2H_PREP"); if (e) mode = std::atoi(e); }
   void start(uint64_t est) {
-    if (p) return;
+    if (mode <= 0 || p || th.joinable()) return;
     p = (uint8_t*)std::malloc(est + 1);
     if (!p) return;
     cap = est;
-    const unsigned T = 4;
-    const uint64_t part = ((est + 1 + T - 1) / T + 4095) & ~4095ull;
-    for (unsigned i = 0; i < T; i++)
-      th.emplace_back([this, i, part]() {
-        const uint64_t a = i * part, b = std::min<uint64_t>(cap + 1, a + part);
+    th = std::thread([this]() {
+      const auto t0 = std::chrono::steady_clock::now();
+      const uint64_t n = cap + 1;
+      for (uint64_t a = 0; a < n; a += PIECE) {
+        const uint64_t b = std::min<uint64_t>(n, a + PIECE);
         volatile uint8_t* q = p;
         for (uint64_t k = a; k < b; k += 4096) q[k] = 0;
-      });
+        if (mode >= 2) {
+          if (hipHostRegister(p + a, b - a, hipHostRegisterDefault) != hipSuccess) { (void)hipGetLastError(); mode = 1; }
+          else reg.push_back(a);
+        }
+      }
+      t_reg = ms_since(t0);
+    });
   }
-  void join() { for (auto& t : th) t.join(); th.clear(); }
-  uint8_t* take(uint64_t n) {   // a buffer of at least n bytes (ownership to the caller)
+  void join() { if (th.joinable()) th.join(); }
+  uint8_t* take(uint64_t n) {   // a buffer of at least n bytes
     join();
     uint8_t* r = p;
     if (r && n > cap + 1) {
+      unreg();
       uint8_t* g = (uint8_t*)std::realloc(r, n);
-      if (!g) { std::free(r); r = nullptr; } else r = g;
+      if (!g) std::free(r);
+      r = g;
     } else if (!r) {
       r = (uint8_t*)std::malloc(n);
     }
-    p = nullptr; cap = 0;
+    p = r; cap = r ? n - 1 : 0;
     return r;
   }
-  ~HostOut() { join(); std::free(p); }
+  // the D2H: registered pieces one copy each (a copy never spans two registrations), the rest plain
+  hipError_t copy_from(const void* d, uint64_t n, hipStream_t st) {
+    uint64_t done = 0;
+    for (uint64_t a : reg) {
+      if (a >= n) break;
+      const uint64_t b = std::min<uint64_t>(n, a + PIECE);
+      const hipError_t e = hipMemcpyAsync(p + a, (const uint8_t*)d + a, b - a, hipMemcpyDeviceToHost, st);
+      if (e != hipSuccess) return e;
+      done = b;
+    }
+    if (hipError_t e = hipStreamSynchronize(st)) return e;
+    return done < n ? hipMemcpy(p + done, (const uint8_t*)d + done, n - done, hipMemcpyDeviceToHost) : hipSuccess;
+  }
+  void unreg() { for (uint64_t a : reg) (void)hipHostUnregister(p + a); reg.clear(); }
+  uint8_t* release() { unreg(); uint8_t* r = p; p = nullptr; cap = 0; return r; }
+  ~HostOut() { join(); unreg(); std::free(p); }
 };
 
 int atz_precompress(atz_ctx_t* c, const uint8_t* file, uint64_t len, uint8_t** atz, uint64_t* atz_len,
@@ -3551,17 +3581,27 @@ int atz_precompress(atz_ctx_t* c, const uint8_t* file, uint64_t len, uint8_t** a
   return guarded([&]() -> int {
     (void)hipGetLastError();
     if (!c || (!file && len) || !atz || !atz_len) return ATZ_E_ARG;
+    const auto t0 = std::chrono::steady_clock::now();
     if (int r = upload(c, c->d_file, file, len)) return r;
+    HIPCHK(hipStreamSynchronize(c->st));
+    const double t_up = ms_since(t0);
     uint64_t al = 0;
     HostOut ho;
     c->on_records = [&ho](uint64_t est) { ho.start(est); };
     struct Reset { atz_ctx* c; ~Reset() { c->on_records = nullptr; } } reset{c};
     if (int r = precompress_dev(c, c->d_file.as<uint8_t>(), file, len, &al, nullptr)) return r;
     c->on_records = nullptr;
+    const double t_dev = ms_since(t0);
     uint8_t* h = ho.take(al + 1);
     if (!h) return ATZ_E_NOMEM;
-    const hipError_t e = hipMemcpy(h, c->d_atz.p, al, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) { std::free(h); HIPCHK(e); }
+    const double t_take = ms_since(t0);
+    HIPCHK(ho.copy_from(c->d_atz.p, al, c->st));
+    const double t_d2h = ms_since(t0);
+    h = ho.release();
+    if (timing_on() || std::getenv("ATZ_H2H_TIMING"))
+      std::fprintf(stderr, "atz: host path: upload %.1f ms, device %.1f ms, host buffer wait %.1f ms (touch + "
+                   "register %.1f ms on the helper), D2H %.1f ms, unregister %.1f ms\n", t_up, t_dev - t_up,
+                   t_take - t_dev, ho.t_reg, t_d2h - t_take, ms_since(t0) - t_d2h);
     *atz = h; *atz_len = al;
     if (stats) *stats = c->stats;
     return ATZ_OK;
