@@ -228,6 +228,7 @@ struct Rec {
   uint32_t flags;
   uint64_t arena_off = ~0ull;   // scan output kept in the arena (complete), else ~0
   bool noshort = false;         // k_inflate's INF_HINT_NOSHORT (the multi-GPU split's cost estimate)
+  uint8_t mhint = 0;            // k_inflate's first-block memLevel (0: none; whole match tables for it)
 };
 
 struct StreamState {
@@ -738,7 +739,7 @@ static uint64_t rd8(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); retur
 struct ScanCand { uint32_t chunk; int32_t type; uint64_t i; };
 // pending stream: its bytes are chunk j0 from i0 plus the napp following chunk buffers (size
 // bytes); they are materialized only for a second refill (rare)
-struct ScanPend { uint64_t off; int type; int state; uint32_t j0, napp; uint64_t i0, size; uint64_t in, out; long spec_chunk; int refills; bool noshort; };
+struct ScanPend { uint64_t off; int type; int state; uint32_t j0, napp; uint64_t i0, size; uint64_t in, out; long spec_chunk; int refills; bool noshort; uint8_t mhint; };
 struct ScanState {
   std::vector<Chunk> chunks;
   std::vector<ScanCand> cands;
@@ -864,6 +865,7 @@ static long scan_select(const ScanState& S, uint32_t j, uint64_t i0, std::vector
       if (out) {
         out->push_back({cd.i + ch.co, r.consumed, r.produced, cd.type, 0, r.arena_off});
         out->back().noshort = (r.err & INF_HINT_NOSHORT) != 0;
+        out->back().mhint = (uint8_t)((r.err >> INF_HINT_MLEV_SHIFT) & 15u);
       }
       i = cd.i + r.consumed;
     } else if (r.consumed == ch.len - cd.i) {
@@ -1065,6 +1067,7 @@ static int scan_replay(atz_ctx* c, const uint8_t* h, ScanState& S, uint32_t ja, 
       if (st == INF_END) {
         recs.push_back({pd.off, pd.in, pd.out, pd.type, 1});
         recs.back().noshort = pd.noshort;
+        recs.back().mhint = pd.mhint;
         i = ch.len - avail;
       }
       S.need_more = avail == 0;
@@ -1077,6 +1080,7 @@ static int scan_replay(atz_ctx* c, const uint8_t* h, ScanState& S, uint32_t ja, 
         pd.off = cd.i + ch.co; pd.type = cd.type; pd.state = (int)S.cres[k].status;
         pd.in = S.cres[k].consumed; pd.out = S.cres[k].produced;
         pd.noshort = (S.cres[k].err & INF_HINT_NOSHORT) != 0;
+        pd.mhint = (uint8_t)((S.cres[k].err >> INF_HINT_MLEV_SHIFT) & 15u);
         pd.j0 = j; pd.i0 = cd.i; pd.napp = 0;
         pd.size = cd.i == 0 ? ch.len : ch.len - cd.i;
         pd.spec_chunk = (i == 0 && S.pend0[j] == k) ? (long)j : -2;
@@ -1440,6 +1444,17 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
   return 0;
 }
 
+// Whole match tables in the first pass for the memLevel a stream's first block names (k_inflate's
+// INF_HINT_MLEV): that trial is the stream's likely winner, which otherwise parses past its prefix and
+// runs again with the rest of its table.  Same-box A/B (gpurun_out/mh*, 2 runs each): C4 1504-1515 vs
+// 1442-1491 MB/s (reruns 105 k -> 29 k, k_trial 648-663 -> 559-565 ms summed); 50 000 streams
+// 1270-1315 vs 1279-1282; 25 000 947-968 vs 938-967; 12 500 669-673 vs 684-686 (a small sweep's rounds
+// are latency-bound, and the hinted trials' whole tables lengthen the first pass).  So: sweeps of more
+// than 16 000 streams (ATZ_MHINT=0 / 1 forces it off / on)
+static bool mhint_on(const atz_ctx* x) {
+  static const int v = [] { const char* e = std::getenv("ATZ_MHINT"); return e ? std::atoi(e) : -1; }();
+  return v < 0 ? x->recs.size() > 16000 : v != 0;
+}
 // Match-table prefix for a trial that may stop early: enough positions for the blocks that decide
 // the shortcut (~3 positions per symbol, lit_bufsize symbols per block); the rest on demand.
 static uint64_t match_prefix(uint64_t n, int memlevel) {   // 2 x lit_bufsize positions, at least 1024
@@ -1630,7 +1645,9 @@ static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, 
       if ((t.mode & 24) == 8) { t.r_off = 0; t.x_lim = n; continue; }   // unchecked replays: no match table
       t.r_off = r_tot;
       r_tot += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
-      t.x_lim = (t.mode & 3) ? n : match_prefix(n, t.memlevel);
+      // whole tables where the trial must parse the whole stream, and for the memLevel the stream's first
+      // block names (its likely winner: no rerun with the rest of the table)
+      t.x_lim = (t.mode & 3) || (mhint_on(x) && t.memlevel == x->recs[t.stream].mhint) ? n : match_prefix(n, t.memlevel);
       MatchJob m{};
       m.infl_off = x->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
       m.p0 = 0; m.p1 = t.x_lim; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
@@ -3251,8 +3268,8 @@ static int shard_scan_impl(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
   blob[5] = k1 - k0; blob[6] = F;
   blob.reserve(SHARD_HDR + 3 * (k1 - k0) + 4 * (sh.jb - sh.ja));
   for (size_t k = k0; k < k1; k++) {
-    // status, with the candidate's cost hint in bit 32
-    blob.push_back(S.cres[k].status | ((S.cres[k].err & INF_HINT_NOSHORT) ? 1ull << 32 : 0ull));
+    // status, with the candidate's hints in bits 32-35 (the first block's memLevel) and 36 (INF_HINT_NOSHORT)
+    blob.push_back(S.cres[k].status | ((uint64_t)(S.cres[k].err >> INF_HINT_MLEV_SHIFT) << 32));
     blob.push_back(S.cres[k].consumed); blob.push_back(S.cres[k].produced);
   }
   for (uint32_t j = sh.ja; j < sh.jb; j++) {
@@ -3292,7 +3309,7 @@ static int shard_sweep_impl(atz_ctx* c, const uint8_t* d_file, const uint8_t* h,
     for (size_t k = k0; k < k1; k++, p += 3) {
       InfRes r{};
       r.status = (uint32_t)p[0]; r.consumed = p[1]; r.produced = p[2]; r.arena_off = ARENA_NONE;
-      r.err = (p[0] >> 32) & 1u ? INF_HINT_NOSHORT : 0u;
+      r.err = (uint32_t)((p[0] >> 32) & 31u) << INF_HINT_MLEV_SHIFT;
       S.cres[k] = r;
     }
     for (uint32_t j = ja; j < jb; j++, p += 4) {
@@ -3465,7 +3482,7 @@ int atz_scan(atz_ctx_t* c, const uint8_t* file, uint64_t len, atz_cand_t** out, 
     for (size_t s = 0; s < c->recs.size(); s++) {
       (*out)[s].offset = c->recs[s].offset; (*out)[s].comp_len = c->recs[s].comp_len;
       (*out)[s].infl_len = c->recs[s].infl_len; (*out)[s].type = c->recs[s].type;
-      (*out)[s].flags = c->recs[s].flags | (c->recs[s].noshort ? 2u : 0u);
+      (*out)[s].flags = c->recs[s].flags | (c->recs[s].noshort ? 2u : 0u) | ((uint32_t)c->recs[s].mhint << 2);
     }
     c->scan_valid = true;
     return ATZ_OK;

@@ -25,8 +25,11 @@ static constexpr uint64_t ARENA_NONE = ~0ull;
 enum : uint32_t { INF_END = 0, INF_ERROR = 1, INF_NEED = 2, INF_RETRY = 3 };   // RETRY: rerun with the 32 KiB ring
 
 // InfRes.err bit 31: the first block is dynamic and codes matches, none of length 3-5 (a cost hint
-// for the multi-GPU split; the low bits are the failing check's code)
+// for the multi-GPU split); bits 27-30: the memLevel (1-9) whose lit_bufsize - 1 symbols the first
+// block holds when more blocks follow, else 0 (the sweep builds whole match tables for that memLevel's
+// trials); the low bits are the failing check's code
 static constexpr uint32_t INF_HINT_NOSHORT = 1u << 31;
+static constexpr uint32_t INF_HINT_MLEV_SHIFT = 27;
 
 struct InfRes {
   uint32_t status;    // INF_*

@@ -539,7 +539,8 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
 
   uint64_t errneed = 0;
   uint32_t errcode = 0;
-  uint32_t hint = 0;   // INF_HINT_NOSHORT (see the dynamic header below)
+  uint32_t hint = 0;   // INF_HINT_NOSHORT (see the dynamic header below) | INF_HINT_MLEV
+  uint32_t mls = 0;    // sum of (length - 1) over the block's matches: symbols = bytes - mls
 #define NEEDB(k) do { if (!has(k)) return R_NEED; } while (0)
 #define FAIL(code, needpos) do { errneed = (needpos); errcode = (code); return R_ERR; } while (0)
 
@@ -641,6 +642,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
             nst = 0;
           }
           if ((uint64_t)dist > prod) { used = sym0; redo = true; break; }   // too far back
+          mls += len - 1u;
           if (!copy_at(len, dist)) { rc = R_RETRY; break; }
           prod += len;
           if (prod - flushed >= FLUSH_AT) flush(false);
@@ -677,6 +679,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
       drop(de);
       stage_flush();
       if ((uint64_t)dist > prod) FAIL(14, pos);            // invalid distance too far back
+      mls += len - 1u;
       if (!copy(len, dist)) return R_RETRY;
     }
   };
@@ -836,8 +839,18 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
       if (ATZ_INF_CLOCKS) cyc_hdr += __builtin_amdgcn_s_memtime() - th0;
       nblk_seen++;
       if (type != 0) {   // one (inlined) decode loop for fixed and dynamic blocks
+        const uint64_t b0 = prod + nst;
+        mls = 0;
         const int rr = codes(lh, dh);
         if (rr != R_OK) return rr;
+        if (nblk_seen == 1 && !last) {
+          // Sweep hint, part of no output: zlib flushes a block when its symbol buffer is full
+          // (_tr_tally, Z/trees.c:1050, Z/deflate.h:328-338), so a first block that is not the last holds exactly
+          // lit_bufsize - 1 = 2^(memLevel + 6) - 1 symbols
+          const uint64_t syms = prod + nst - b0 - mls;
+          if (syms >= 127 && syms <= 32767 && ((syms + 1) & syms) == 0)
+            hint |= (uint32_t)(__builtin_ctzll(syms + 1) - 6) << INF_HINT_MLEV_SHIFT;
+        }
       }
     } while (!last);
     // CHECK (Z/inflate.c:1174-1195)

@@ -47,7 +47,9 @@ typedef struct {
     int32_t  type;       /* offsetType 0..23 */
     uint32_t flags;      /* bit0: recorded through a chunk-boundary continuation; bit1: the first block is
                             dynamic and codes matches but none of length 3-5 (a Z_FILTERED-like stream: the
-                            multi-GPU split's cost hint, not part of the reference's record) */
+                            multi-GPU split's cost hint, not part of the reference's record); bits 2-5:
+                            the memLevel (1-9) whose lit_bufsize - 1 symbols the first block holds when
+                            more blocks follow, else 0 (a sweep hint, likewise not the reference's) */
 } atz_cand_t;
 
 /* ATZdata::streamOffset after Phase 3. */

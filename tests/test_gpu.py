@@ -317,6 +317,12 @@ def test_bench_config_slice_matches_oracle(atz):
         got = [(r["clevel"], r["window"], r["memlevel"], r["ident"], r["recomp"]) for r in res]
         exp = [(s["clevel"], s["window"], s["memlevel"], s["ident"], s["recomp"]) for s in st_ref["streams"]]
         assert got == exp
+        # the scan's first-block memLevel (candidate flags bits 2-5: a multi-block stream's first block
+        # holds lit_bufsize - 1 symbols) names the memLevel the sweep found for every exactly
+        # reproduced stream it is set for
+        hinted = [((r[4] >> 2) & 15, s) for r, s in zip(recs, st_ref["streams"])]
+        full = [(h, s["memlevel"]) for h, s in hinted if h and s["ident"] == s["comp_len"]]
+        assert len(full) > 600 and all(h == m for h, m in full), [x for x in full if x[0] != x[1]][:10]
         out, st = c.precompress(data)
         assert st["n_streams"] > 1500 and st["n_recomp"] == st["n_streams"]
         assert sha(out) == sha(ref)
