@@ -42,7 +42,7 @@ def _worker(rank, world, port, path, chunksize, q):
         with antiz_amd.Context(chunksize=chunksize, device=0) as ctx:
             out, n, st = shard.precompress_sharded(ctx, d, data, out_device="cuda")
             atz = out[:n].cpu().numpy().tobytes() if out is not None else None
-        q.put((rank, atz, st["n_streams"], st["n_recomp"], st["trial_cyc_total"], None))
+        q.put((rank, atz, st["n_streams"], st["n_recomp"], st["k_trial_alg_bytes"], None))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:   # report instead of hanging the parent
@@ -177,8 +177,9 @@ def test_split_hint_matches_first_block_headers(clustered):
 def test_sharded_cost_split_on_clustered_input(clustered, world):
     """The ranks' record ranges partition the file's records, and the split follows cost, not counts: the
     last rank, which holds the cluster of PNG-like streams (each runs its class's whole trial list), gets
-    fewer records than an equal split would give it, and the ranks' trial cycles stay within 2x of their
-    mean (the measured balance is reported by bench.py's rank_balance)."""
+    fewer records than an equal split would give it, and the ranks' trial work (algorithmic bytes: input
+    parsed + output compared; shader cycles would also count the waits of ranks sharing the one GPU)
+    stays within 2x of their mean (bench.py's rank_balance reports the measured balance)."""
     import antiz_amd
     path, data, ref = clustered
     with antiz_amd.Context(device=0) as c:
@@ -188,5 +189,5 @@ def test_sharded_cost_split_on_clustered_input(clustered, world):
     counts = [res[r][1] for r in range(world)]
     assert sum(counts) == len(recs) and all(n > 0 for n in counts)
     assert counts[-1] < len(recs) // world
-    cyc = [res[r][3] for r in range(world)]
-    assert max(cyc) <= 2.0 * sum(cyc) / world, cyc
+    work = [res[r][3] for r in range(world)]
+    assert max(work) <= 2.0 * sum(work) / world, work
