@@ -1451,9 +1451,15 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
 // 1270-1315 vs 1279-1282; 25 000 947-968 vs 938-967; 12 500 669-673 vs 684-686 (a small sweep's rounds
 // are latency-bound, and the hinted trials' whole tables lengthen the first pass).  So: sweeps of more
 // than 16 000 streams (ATZ_MHINT=0 / 1 forces it off / on)
+// ATZ_HDEPTH=1: a round runs a hinted stream's list at least through its next entry at the hinted
+// memLevel (speculation up to the likely winner; its whole table is built whatever the sweep's size)
+static bool hdepth_on() {
+  static const bool on = [] { const char* e = std::getenv("ATZ_HDEPTH"); return e && std::atoi(e) != 0; }();
+  return on;
+}
 static bool mhint_on(const atz_ctx* x) {
   static const int v = [] { const char* e = std::getenv("ATZ_MHINT"); return e ? std::atoi(e) : -1; }();
-  return v < 0 ? x->recs.size() > 16000 : v != 0;
+  return v < 0 ? x->recs.size() > 16000 || hdepth_on() : v != 0;
 }
 // Match-table prefix for a trial that may stop early: enough positions for the blocks that decide
 // the shortcut (~3 positions per symbol, lit_bufsize symbols per block); the rest on demand.
@@ -2053,7 +2059,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       mbeg[a] = (uint32_t)mine.size();
       const uint32_t s = active[a];
       StreamState& st = ss[s];
-      const uint32_t Ks = K;
+      uint32_t Ks = K;
+      if (hdepth_on() && x->recs[s].mhint)
+        for (uint32_t j = 0; j < 64 && st.idx + j < st.list->size(); j++)
+          if (((*st.list)[st.idx + j] & 0xffu) == x->recs[s].mhint) { Ks = std::max(Ks, j + 1); break; }
       // scratch of a round (match tables, outputs, symbols) is bounded: streams past the budget
       // wait for the next round, where they go first
       if (a > 0 && round_bytes > round_budget) {
