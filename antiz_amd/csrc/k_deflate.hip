@@ -925,6 +925,7 @@ struct TrialSharedSlow {
   uint64_t ring[RING_SLOW];   // match-table entries (.x low, .y high) of the positions around the window
 };
 static_assert(sizeof(TreeScratch) <= RING_SLOW * sizeof(uint64_t), "tree scratch overlays the ring");
+static_assert(offsetof(BitOut, cyc_scan) == offsetof(BitOut, cyc_heap) + 8, "block_trees' cyc[0], cyc[1]");
 static_assert(STAGE_WORDS * 4 <= RING_SLOW * sizeof(uint64_t), "emission staging overlays the ring");
 
 // Multi-wave trials (small blocks: memLevel <= MW_MAX_MEMLEVEL, host side).  A block of lit_bufsize
@@ -947,7 +948,9 @@ struct MWFlusher {
   TreeCodes k;
   TreeScratch sc;                // gen_bitlen scratch, then the emission staging
   uint64_t cyc_tree, cyc_emit;   // diagnostics
+  uint64_t cyc_heap, cyc_scan;   // diagnostics (ATZ_STEP_CLOCKS; consecutive: block_trees' cyc[0], cyc[1])
 };
+static_assert(offsetof(MWFlusher, cyc_scan) == offsetof(MWFlusher, cyc_heap) + 8, "block_trees' cyc[0], cyc[1]");
 struct MWCtl {
   uint32_t next_emit;   // index of the next block to emit
   uint32_t stop;        // the trial is decided (state), or the parser gave up (TR_NEED_R)
@@ -1608,7 +1611,9 @@ struct BlockPlan {
   uint64_t opt_lenb, static_lenb;
   int lmax, dmax, max_blindex;
 };
-__device__ __noinline__ BlockPlan block_trees(const LDS BlockFreq& f, LDS TreeCodes& s, LDS TreeScratch& sc, LDS BitOut& b,
+// cyc[0] / cyc[1]: the caller's heap / scan_tree clock counters (ATZ_STEP_CLOCKS), its own: a
+// multi-wave trial's flushers build trees at the same time
+__device__ __noinline__ BlockPlan block_trees(const LDS BlockFreq& f, LDS TreeCodes& s, LDS TreeScratch& sc, LDS uint64_t* cyc,
                                               uint32_t level, uint64_t stored_len, int lane) {
   level = uni(level);
   stored_len = uni(stored_len);
@@ -1618,7 +1623,7 @@ __device__ __noinline__ BlockPlan block_trees(const LDS BlockFreq& f, LDS TreeCo
     // literal/length tree
     for (int i = lane; i < NLC; i += 64) sc.freq[i] = (uint16_t)(f.lfreq2[i >> 1] >> (16 * (i & 1)));
     TreeRes r = build_tree(s.w, sc, s.llen, NLC, 15, (const CONSTANT uint8_t*)c_xlb, 257, (const CONSTANT uint8_t*)c_t.st_llen,
-                           b.cyc_heap, lane);
+                           cyc[0], lane);
     pl.lmax = (int)uni((uint32_t)r.max_code);
     opt_len += uni(r.d_opt);
     static_len += uni(r.d_static);
@@ -1627,7 +1632,7 @@ __device__ __noinline__ BlockPlan block_trees(const LDS BlockFreq& f, LDS TreeCo
     // distance tree
     for (int i = lane; i < NDC; i += 64) sc.freq[i] = (uint16_t)(f.dfreq2[i >> 1] >> (16 * (i & 1)));
     r = build_tree(s.w, sc, s.dlen, NDC, 15, (const CONSTANT uint8_t*)c_xdb, 0, (const CONSTANT uint8_t*)c_t.st_dlen,
-                   b.cyc_heap, lane);
+                   cyc[0], lane);
     pl.dmax = (int)uni((uint32_t)r.max_code);
     opt_len += uni(r.d_opt);
     static_len += uni(r.d_static);
@@ -1638,9 +1643,9 @@ __device__ __noinline__ BlockPlan block_trees(const LDS BlockFreq& f, LDS TreeCo
     const uint64_t cs0 = STEP_CLOCK();
     rle_tree(s, nullptr, s.llen, pl.lmax, false, 0, lane);
     rle_tree(s, nullptr, s.dlen, pl.dmax, false, 0, lane);
-    b.cyc_scan += STEP_CLOCK() - cs0;
+    if (lane == 0) cyc[1] += STEP_CLOCK() - cs0;
     for (int i = lane; i < NBLC; i += 64) sc.freq[i] = (uint16_t)s.bfreq[i];
-    r = build_tree(s.w, sc, s.blen, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, b.cyc_heap, lane);
+    r = build_tree(s.w, sc, s.blen, NBLC, 7, (const CONSTANT uint8_t*)c_xblb, 0, nullptr, cyc[0], lane);
     const int bmax = (int)uni((uint32_t)r.max_code);
     opt_len += uni(r.d_opt);
     gen_codes(s.w, bmax, s.bcode, s.blen, lane);
@@ -1768,7 +1773,7 @@ __device__ __forceinline__ uint32_t flush_block(LDS TrialShared& s, LDS TreeScra
                                                 uint32_t last_lit, uint32_t level, uint32_t lbs, int last, const SweepOpts& opt,
                                                 uint64_t best_ident, bool full_needed, int lane) {
   const uint64_t c0 = clock64();
-  const BlockPlan pl = block_trees(s.f, s.k, sc, b, level, (uint64_t)((int64_t)p - block_start), lane);
+  const BlockPlan pl = block_trees(s.f, s.k, sc, &b.cyc_heap, level, (uint64_t)((int64_t)p - block_start), lane);
   const uint64_t c1 = clock64();
   b.cyc_tree += c1 - c0;
   const uint32_t hz = block_emit(s.k, (LDS uint32_t*)&sc, b, syms, in, block_start, p, S, last_lit, lbs, last, opt, best_ident,
@@ -1866,7 +1871,7 @@ __device__ void trial_flusher(const SweepArgs& A, LDS TrialShared& s, LDS MWPart
     const uint32_t last_lit = uni(sl.last_lit), sbase = uni(sl.sbase);
     const int last = (int)uni(sl.last);
     const uint64_t c0 = clock64();
-    const BlockPlan pl = block_trees(sl.f, me.k, me.sc, b, level, (uint64_t)((int64_t)p - bs), lane);
+    const BlockPlan pl = block_trees(sl.f, me.k, me.sc, &me.cyc_heap, level, (uint64_t)((int64_t)p - bs), lane);
     st_rel(sl.seq, 0u, lane);   // the parser may refill the slot
     const uint64_t c1 = clock64();
     bool turn = false;
@@ -2006,7 +2011,8 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
   if constexpr (MW) {
     LDS MWPart& mw = *(LDS MWPart*)&shm.mw;
     if (wave == 0) {
-      if (lane < MW_F) { mw.slot[lane].seq = 0; mw.fl[lane].cyc_tree = 0; mw.fl[lane].cyc_emit = 0; }
+      if (lane < MW_F) { mw.slot[lane].seq = 0; mw.fl[lane].cyc_tree = 0; mw.fl[lane].cyc_emit = 0;
+                        mw.fl[lane].cyc_heap = 0; mw.fl[lane].cyc_scan = 0; }
       if (lane == 0) {
         mw.ctl.next_emit = 0; mw.ctl.stop = 0; mw.ctl.parse_done = 0; mw.ctl.nblocks = 0;
         mw.ctl.state = ~0u; mw.ctl.hazard = 0;
@@ -2714,7 +2720,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     if (state != TR_NEED_R || cs != ~0u) state = cs;
     hazard |= uni(mw.ctl.hazard);
     if (lane == 0) {
-      for (int f = 0; f < MW_F; f++) { b.cyc_tree += mw.fl[f].cyc_tree; b.cyc_emit += mw.fl[f].cyc_emit; }
+      for (int f = 0; f < MW_F; f++) {
+        b.cyc_tree += mw.fl[f].cyc_tree; b.cyc_emit += mw.fl[f].cyc_emit;
+        b.cyc_heap += mw.fl[f].cyc_heap; b.cyc_scan += mw.fl[f].cyc_scan;
+      }
     }
   }
   uint32_t rmax = (run_imp << 16) | run_len;   // both < 2^16: per-field maxima by two reductions
