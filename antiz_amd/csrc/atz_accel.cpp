@@ -494,6 +494,7 @@ struct atz_ctx {
     std::vector<size_t> unfinished;       // published streams not done (flow: [0]; rounds: per pipe)
     bool closed = false;                  // every stream is published
     bool abort = false;
+    std::atomic<size_t> published{0};     // streams published to the sweep so far (round_target)
   } sched;
   std::vector<std::unique_ptr<Pipe>> pipes;
   std::vector<std::unique_ptr<DBuf>> slabs;   // inflated records, one allocation per scan piece
@@ -2017,7 +2018,8 @@ static void sched_abort(atz_ctx* x) {
 // The sweep work of pipe c: rounds on the batches sched_take hands it (per-kind x level counters:
 // count, cycles total/tree/emit/heap/fallback, parsed bytes, symbols, scan/send cycles, parse window
 // phases).
-static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss, size_t target) {
+static size_t round_target(const atz_ctx* x);
+static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
   auto t0 = std::chrono::steady_clock::now();
   std::vector<uint32_t> active;
   const bool flow = x->sched.flow;
@@ -2042,6 +2044,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     // speculation depth: `target` trials per round and pipe; ATZ_KREF=n sizes it as if n pipes shared
     // the unfinished streams (more pipes then overlap more rounds without speculating deeper)
     const size_t kref = kref_pipes();
+    const size_t target = round_target(x);
     const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, flow ? target * np / std::max<size_t>(1, unf)
                                                                        : kref ? target * kref / std::max<size_t>(1, unf)
                                                                               : target / active.size()));
@@ -2441,14 +2444,26 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
 // (GPU_MAX_HW_QUEUES, read at HIP init; bench.py sets it for such runs) six pipes overlap more rounds:
 // a 12 500-stream share 696-710 vs 628-655 MB/s on one MI355X (25 000: 904 vs 923, so only below 16 000).
 // (Read once, thread-safely; GPU_MAX_HW_QUEUES only holds if it was set before HIP initialised.)
+// Round 4 re-measured it after the round rework (`gpurun_out/tq`, same box, 2 runs each, 12 500 streams):
+// 6 pipes on 8 queues 629-648 MB/s, with a round target of 8192 630-640, 3 pipes with 8192 651-687; so
+// three pipes everywhere, and small sweeps get the larger round target instead (round_target).
 static size_t sweep_pipes(size_t n) {
-  static const std::pair<int, int> cfg = [] {
+  (void)n;
+  static const int cfg = [] {
     const char* e = std::getenv("ATZ_PIPES");
-    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-    return std::make_pair(e ? std::max(1, std::min(8, std::atoi(e))) : -1, q ? std::atoi(q) : 4);
+    return e ? std::max(1, std::min(8, std::atoi(e))) : 3;
   }();
-  if (cfg.first > 0) return (size_t)cfg.first;
-  return n <= 16000 && cfg.second >= 8 ? 6 : 3;
+  return (size_t)cfg;
+}
+// Trials per round and pipe (K = target / the pipe's active streams, 1..32).  ATZ_TARGET overrides.
+// A sweep of few streams -- one rank's share of a file split over 4 or 8 GPUs -- runs the same ~16 rounds
+// as the whole file with a fraction of the trials each, so its rounds are latency-bound and a deeper
+// round pays (same box, 2 runs each: 12 500 streams 677-690 -> 713-763 MB/s, 25 000 928-938 -> 981-994;
+// the whole C4 file: no difference, 1439-1501 vs 1466-1539).
+static size_t round_target(const atz_ctx* x) {
+  static const int env = [] { const char* e = std::getenv("ATZ_TARGET"); return e ? std::max(256, std::atoi(e)) : 0; }();
+  if (env) return (size_t)env;
+  return x->sched.published.load() <= 32000 ? 8192 : 4096;
 }
 // The sweep runs while the scan is still producing records: sweep_begin starts one host thread
 // per pipe, sweep_publish hands a range of ready records (inflated, Adler-32 known) to the pipes,
@@ -2509,6 +2524,7 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
     Q.unfinished.assign(Q.flow ? 1 : R.np, 0);
     Q.closed = false;
     Q.abort = false;
+    Q.published = 0;
   }
   for (size_t g = 0; g < R.np; g++) {
     Pipe* p = c->pipes[g].get();
@@ -2518,16 +2534,12 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
     p->n_copy = p->n_sync = 0;
     std::memset(p->kind, 0, sizeof(p->kind));
   }
-  static const size_t target = [] {   // trials per round and pipe (ATZ_TARGET: tuning; C4: 16384 758, 8192 774, 4096 787 MB/s)
-    const char* e = std::getenv("ATZ_TARGET");
-    return e ? (size_t)std::max(256, std::atoi(e)) : (size_t)4096;
-  }();
   R.rc.assign(R.np, 0);
   R.running = true;
   for (size_t g = 0; g < R.np; g++)
     R.th.emplace_back([c, &R, &ss, g]() {
       if (hipSetDevice(c->dev) != hipSuccess) { R.rc[g] = ATZ_E_HIP; sched_abort(c); return; }
-      R.rc[g] = sweep_pipe(c, c->pipes[g].get(), R.d_file, ss, target);
+      R.rc[g] = sweep_pipe(c, c->pipes[g].get(), R.d_file, ss);
       if (R.rc[g]) sched_abort(c);   // the other pipes stop too (streams this one held never come back)
     });
   return 0;
@@ -2557,6 +2569,7 @@ static int sweep_publish(atz_ctx* c, SweepRun& R, size_t r0, size_t r1) {
       // interleaved over the pipes by global index: every pipe gets the same mix of classes and sizes
       for (size_t s = r0; s < r1; s++) { Q.q[s % R.np].push_back((uint32_t)s); Q.unfinished[s % R.np]++; }
     }
+    Q.published = r1;
     Q.cv.notify_all();
   }
   R.published = r1;
