@@ -2444,22 +2444,23 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
 // (GPU_MAX_HW_QUEUES, read at HIP init; bench.py sets it for such runs) six pipes overlap more rounds:
 // a 12 500-stream share 696-710 vs 628-655 MB/s on one MI355X (25 000: 904 vs 923, so only below 16 000).
 // (Read once, thread-safely; GPU_MAX_HW_QUEUES only holds if it was set before HIP initialised.)
-// Round 4 re-measured it after the round rework (`gpurun_out/tq`, same box, 2 runs each, 12 500 streams):
-// 6 pipes on 8 queues 629-648 MB/s, with a round target of 8192 630-640, 3 pipes with 8192 651-687; so
-// three pipes everywhere, and small sweeps get the larger round target instead (round_target).
+// Round 4 re-measured it after the round rework (12 500 streams, one box, 4 runs each, `gpurun_out/rts`):
+// 3 pipes 651-675 MB/s, 6 pipes on 8 queues 714-744 (round target 4096) and 707-753 (8192).
 static size_t sweep_pipes(size_t n) {
-  (void)n;
-  static const int cfg = [] {
+  static const std::pair<int, int> cfg = [] {
     const char* e = std::getenv("ATZ_PIPES");
-    return e ? std::max(1, std::min(8, std::atoi(e))) : 3;
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    return std::make_pair(e ? std::max(1, std::min(8, std::atoi(e))) : -1, q ? std::atoi(q) : 4);
   }();
-  return (size_t)cfg;
+  if (cfg.first > 0) return (size_t)cfg.first;
+  return n <= 16000 && cfg.second >= 8 ? 6 : 3;
 }
 // Trials per round and pipe (K = target / the pipe's active streams, 1..32).  ATZ_TARGET overrides.
 // A sweep of few streams -- one rank's share of a file split over 4 or 8 GPUs -- runs the same ~16 rounds
 // as the whole file with a fraction of the trials each, so its rounds are latency-bound and a deeper
-// round pays (same box, 2 runs each: 12 500 streams 677-690 -> 713-763 MB/s, 25 000 928-938 -> 981-994;
-// the whole C4 file: no difference, 1439-1501 vs 1466-1539).
+// round pays on three pipes (same box, 2 runs each: 12 500 streams 677-690 -> 713-763 MB/s, 25 000
+// 928-938 -> 981-994, on another box 926-934 -> 940-965; the whole C4 file: no difference, 1439-1501 vs
+// 1466-1539), and is neutral on six (707-753 vs 714-744).
 static size_t round_target(const atz_ctx* x) {
   static const int env = [] { const char* e = std::getenv("ATZ_TARGET"); return e ? std::max(256, std::atoi(e)) : 0; }();
   if (env) return (size_t)env;

@@ -222,8 +222,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # (One rank's share of a file split over many GPUs is a small sweep, bound by its rounds' slowest
-    # trials: the library sizes its rounds for that itself, atz_accel.cpp round_target, DESIGN s6.)
+    # One rank's share of a file split over many GPUs is a small sweep, bound by its rounds' slowest
+    # trials: the library runs 6 sweep pipes on their own hardware queues there (atz_accel.cpp
+    # sweep_pipes, DESIGN s6), which needs the queues before HIP initialises
+    if args.mode == "file" and world > 1 and args.streams / world <= 16000:
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     import torch
     import torch.distributed as dist
     # ATZ_BENCH_BACKEND=gloo: rehearsal of the N > 1 paths with several ranks on one GPU (RCCL refuses

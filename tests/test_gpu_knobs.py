@@ -5,7 +5,8 @@ the ATZ1 bytes must equal the oracle's (the reference's algorithm, oracle/) for 
   ATZ_REPLAY   0 no symbol replay, 2 save sequences but never replay, 3 replays between budget-free
                trials only (default 1: DESIGN.md s3.5)
   ATZ_DEDUP    0 launch duplicate trials anyway (default 1)
-  ATZ_PIPES    sweep pipes, 1..8 (default 3)
+  ATZ_PIPES    sweep pipes, 1..8 (default 3; 6 for a sweep of <= 16 000 streams when
+               GPU_MAX_HW_QUEUES >= 8, as bench.py sets it for small per-rank shares)
   ATZ_TARGET   trials per round and pipe (speculation depth; default 8192 for a sweep of at most 32 000
                streams, else 4096)
   ATZ_SPEC_CONT 0: the scan waits for the first chunk-boundary continuations (default 1: speculative)
