@@ -7,6 +7,9 @@ set -o pipefail
 tag=${1:-bal}; W=${2:-8}
 out=gpurun_out/$tag; mkdir -p $out
 export ATZ_BENCH_BACKEND=gloo ATZ_BENCH_CACHE=/tmp/atz_bench_cache
+# eight ranks share the one GPU's 288 GB here: the smaller round target keeps their round scratch within
+# it (on a node each rank has a GPU of its own)
+export ATZ_TARGET=${ATZ_TARGET:-4096}
 port=29611
 for wl in ${WLS:-c4 c4c3}; do
   for hint in 1 0; do
