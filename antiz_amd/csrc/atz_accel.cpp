@@ -1466,7 +1466,8 @@ static bool mhint_on(const atz_ctx* x) {
 // the shortcut (~3 positions per symbol, lit_bufsize symbols per block); the rest on demand.
 static uint64_t match_prefix(uint64_t n, int memlevel) {   // 2 x lit_bufsize positions, at least 1024
   static const uint64_t mul = [] { const char* e = std::getenv("ATZ_PREFIX_MUL"); return e ? (uint64_t)std::max(1, std::atoi(e)) : 2ull; }();
-  return std::min(n, std::max<uint64_t>(1024, mul << (memlevel + 6)));
+  static const uint64_t lo = [] { const char* e = std::getenv("ATZ_PREFIX_MIN"); return e ? (uint64_t)std::max(64, std::atoi(e)) : 1024ull; }();
+  return std::min(n, std::max<uint64_t>(lo, mul << (memlevel + 6)));
 }
 
 static uint32_t lazy_host(uint32_t level) {   // max_lazy of levels 7-9 (Z/deflate.c:141-143)
