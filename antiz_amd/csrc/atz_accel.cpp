@@ -1463,10 +1463,13 @@ static bool mhint_on(const atz_ctx* x) {
   return v < 0 ? x->recs.size() > 16000 || hdepth_on() : v != 0;
 }
 // Match-table prefix for a trial that may stop early: enough positions for the blocks that decide
-// the shortcut (~3 positions per symbol, lit_bufsize symbols per block); the rest on demand.
-static uint64_t match_prefix(uint64_t n, int memlevel) {   // 2 x lit_bufsize positions, at least 1024
+// the shortcut (~3 positions per symbol, lit_bufsize symbols per block); the rest on demand.  The
+// floor covers the shortcut's 512 output bytes at memLevel 1-2, whose blocks hold 127-255 symbols: a
+// floor of 1024 left 29 k memLevel 1-2 trials on C4 to run again with the rest of their table, 3072
+// leaves none (same box, 3 runs each: 1521-1540 vs 1443-1454 MB/s; 6144 1463-1569).
+static uint64_t match_prefix(uint64_t n, int memlevel) {   // 2 x lit_bufsize positions, at least 3072
   static const uint64_t mul = [] { const char* e = std::getenv("ATZ_PREFIX_MUL"); return e ? (uint64_t)std::max(1, std::atoi(e)) : 2ull; }();
-  static const uint64_t lo = [] { const char* e = std::getenv("ATZ_PREFIX_MIN"); return e ? (uint64_t)std::max(64, std::atoi(e)) : 1024ull; }();
+  static const uint64_t lo = [] { const char* e = std::getenv("ATZ_PREFIX_MIN"); return e ? (uint64_t)std::max(64, std::atoi(e)) : 3072ull; }();
   return std::min(n, std::max<uint64_t>(lo, mul << (memlevel + 6)));
 }
 
