@@ -15,6 +15,7 @@ the ATZ1 bytes must equal the oracle's (the reference's algorithm, oracle/) for 
   ATZ_INS16    1: fast trials of streams of at most 16384 positions on the 16 Kibit insertion ring (default 0)
   ATZ_MHINT    0 / 1: whole match tables for the first block's memLevel off / on (default: above 16 000 streams)
   ATZ_HDEPTH   1: a round runs a hinted stream's list through its next entry at the hinted memLevel
+  ATZ_PREFIX_MIN the match-table prefix floor in positions (default 3072 above 16 000 streams, else 1024)
   ATZ_FULLK    1: speculative rounds (K > 1) build whole match tables up front
   ATZ_SCHED    flow: one queue shared by the pipes, each stream's next step as soon as its own round is
                done, reruns as the stream's next step (default rounds: every pipe sweeps a fixed share
@@ -38,7 +39,7 @@ SETTINGS = [{"ATZ_REPLAY": "0"}, {"ATZ_REPLAY": "2"}, {"ATZ_REPLAY": "3"}, {"ATZ
             {"ATZ_SCHED": "flow"}, {"ATZ_SCHED": "flow", "ATZ_PIPES": "5", "ATZ_TARGET": "256"},
             {"ATZ_SCHED": "flow", "ATZ_PIPES": "8", "ATZ_TARGET": "65536"}, {"ATZ_PIPES": "8", "ATZ_TARGET": "256"},
             {"ATZ_REBALANCE": "1"}, {"ATZ_KREF": "3", "ATZ_PIPES": "6"}, {"ATZ_XLDS": "4096"}, {"ATZ_FULLK": "1", "ATZ_TARGET": "65536"},
-            {"ATZ_INS16": "1"}, {"ATZ_MHINT": "1"}, {"ATZ_MHINT": "0"}, {"ATZ_HDEPTH": "1"}]
+            {"ATZ_INS16": "1"}, {"ATZ_MHINT": "1"}, {"ATZ_MHINT": "0"}, {"ATZ_HDEPTH": "1"}, {"ATZ_PREFIX_MIN": "3072", "ATZ_MHINT": "1"}]
 
 RUN = r"""
 import hashlib, sys
