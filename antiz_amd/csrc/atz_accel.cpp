@@ -1458,9 +1458,12 @@ static bool hdepth_on() {
   static const bool on = [] { const char* e = std::getenv("ATZ_HDEPTH"); return e && std::atoi(e) != 0; }();
   return on;
 }
+// A small sweep on six pipes (one rank's share at 8 GPUs) gains from it too (12 500 streams, same box,
+// 3 runs each: 697-716 -> 741-776 MB/s; with the 3072 prefix floor 749-802), one on three pipes does not.
+static bool big_sweep(const atz_ctx* x) { return x->recs.size() > 16000 || x->pipes_running >= 6; }
 static bool mhint_on(const atz_ctx* x) {
   static const int v = [] { const char* e = std::getenv("ATZ_MHINT"); return e ? std::atoi(e) : -1; }();
-  return v < 0 ? x->recs.size() > 16000 || hdepth_on() : v != 0;
+  return v < 0 ? big_sweep(x) || hdepth_on() : v != 0;
 }
 // Match-table prefix for a trial that may stop early: enough positions for the blocks that decide
 // the shortcut (~3 positions per symbol, lit_bufsize symbols per block); the rest on demand.  The
@@ -1468,8 +1471,8 @@ static bool mhint_on(const atz_ctx* x) {
 // floor of 1024 left 29 k memLevel 1-2 trials on C4 to run again with the rest of their table, 3072
 // leaves none (same box, 3 runs each: 1521-1540 vs 1443-1454 MB/s; 6144 1463-1569; on another box
 // 1497-1499 vs 1484-1488).  A small sweep's latency-bound rounds prefer the short first pass (12 500
-// streams: 663-687 with 3072 vs 700 with 1024), so the floor is 3072 above 16 000 streams, like
-// mhint_on's (ATZ_PREFIX_MIN overrides).
+// streams on three pipes: 663-687 with 3072 vs 700 with 1024), so the floor is 3072 where mhint_on
+// applies, big_sweep (ATZ_PREFIX_MIN overrides).
 static uint64_t match_prefix(uint64_t n, int memlevel, bool big) {   // 2 x lit_bufsize positions, floor
   static const uint64_t mul = [] { const char* e = std::getenv("ATZ_PREFIX_MUL"); return e ? (uint64_t)std::max(1, std::atoi(e)) : 2ull; }();
   static const uint64_t lo = [] { const char* e = std::getenv("ATZ_PREFIX_MIN"); return e ? (uint64_t)std::max(64, std::atoi(e)) : 0ull; }();
@@ -1663,7 +1666,7 @@ static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, 
       r_tot += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
       // whole tables where the trial must parse the whole stream, and for the memLevel the stream's first
       // block names (its likely winner: no rerun with the rest of the table)
-      t.x_lim = (t.mode & 3) || (mhint_on(x) && t.memlevel == x->recs[t.stream].mhint) ? n : match_prefix(n, t.memlevel, x->recs.size() > 16000);
+      t.x_lim = (t.mode & 3) || (mhint_on(x) && t.memlevel == x->recs[t.stream].mhint) ? n : match_prefix(n, t.memlevel, big_sweep(x));
       MatchJob m{};
       m.infl_off = x->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
       m.p0 = 0; m.p1 = t.x_lim; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
