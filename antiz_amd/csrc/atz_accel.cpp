@@ -242,8 +242,6 @@ struct StreamState {
   std::vector<uint32_t> rawdiff;  // raw positions of the current best
   std::vector<uint8_t> diffval;
   uint32_t trials = 0;
-  uint32_t full_at = ~0u;         // list index whose trial ran past its match-table prefix (flow: rerun as
-                                  // the stream's next step, with its whole table)
   int32_t rp = -1;                // symbol-replay entries (levels 1-9) in the context's rp_pool
   bool recomp = false;
   // levels 7-9 already run budget-free at (window, memLevel): level, longest PL a lazy read improved,
@@ -469,6 +467,10 @@ struct atz_ctx {
   // atz_scan -> atz_sweep hand-off: set by a successful atz_scan, cleared by every call that
   // replaces recs / d_file (precompress, deflate, reconstruct, inflate_batch)
   bool scan_valid = false;
+  // atz_sweep reports every stream's best ident, c, w, m as the reference computes them; the precompress
+  // paths only need what the ATZ1 holds, so they let trials stop once they cannot make their stream
+  // recompressible (elig_floor)
+  bool exact_idents = false;
   std::vector<uint32_t> scan_trailer;   // per record: the stream's Adler-32 trailer (big-endian word)
   bool file_on_device = false;      // d_file holds the current file
   const uint8_t* dev_file = nullptr;
@@ -489,9 +491,8 @@ struct atz_ctx {
   struct Sched {
     std::mutex mu;
     std::condition_variable cv;
-    bool flow = true;                     // one shared queue pair (else: one queue per pipe, rounds)
-    std::vector<std::deque<uint32_t>> q;  // flow: one shared queue; rounds: one per pipe
-    std::vector<size_t> unfinished;       // published streams not done (flow: [0]; rounds: per pipe)
+    std::vector<std::deque<uint32_t>> q;  // one per pipe
+    std::vector<size_t> unfinished;       // published streams not done, per pipe
     bool closed = false;                  // every stream is published
     bool abort = false;
     std::atomic<size_t> published{0};     // streams published to the sweep so far (round_target)
@@ -502,7 +503,7 @@ struct atz_ctx {
   std::atomic<bool> sweep_abort{false};   // the pipes stop at their next round (a withdrawn speculative scan)
   // precompress_dev's large per-call state, kept so its capacity survives the calls
   std::shared_ptr<struct ScanState> scan_keep;
-  // atz_precompress: called once the sweep has every record, with an upper estimate of the ATZ1 size
+  // atz_precompress: called once the sweep has the speculative records, with an estimate of the ATZ1 size
   std::function<void(uint64_t)> on_records;
   std::vector<StreamState> ss_keep;
   std::vector<StreamDev> sd_keep;
@@ -577,8 +578,7 @@ static int upload(C* c, DBuf& b, const void* h, size_t n, size_t slack = 4096) {
 }
 
 static bool sync_debug() {
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_SYNC_DEBUG"); v = e && *e == '1'; }
+  static const int v = [] { const char* e = std::getenv("ATZ_SYNC_DEBUG"); return (int)(e && *e == '1'); }();
   return v == 1;
 }
 // ATZ_SYNC_DEBUG=1: synchronise after every launch and name the kernel that failed
@@ -605,8 +605,7 @@ struct Chunk {
 static constexpr uint64_t ARENA_SLOT = 65536;   // arena slot per scan candidate (longer outputs are re-inflated)
 
 static int timing_level() {   // ATZ_TIMING=1: phase timings, 2: + per-round sweep timeline
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_TIMING"); v = e ? std::atoi(e) : 0; }
+  static const int v = [] { const char* e = std::getenv("ATZ_TIMING"); return (int)(e ? std::atoi(e) : 0); }();
   return v;
 }
 static bool timing_on() { return timing_level() >= 1; }
@@ -1058,6 +1057,10 @@ static int scan_replay(atz_ctx* c, const uint8_t* h, ScanState& S, uint32_t ja, 
         pd.size += ch.len;
         pd.refills++;
         pd.state = (int)rr.status; pd.in = rr.consumed; pd.out = rr.produced;
+        // the first block's memLevel hint: a partial decode has it only if that block ended before the
+        // chunk boundary; the continuation decodes the stream from its header (a shard's blob of another
+        // rank's continuation carries no hint bits: whole tables are then just not built up front)
+        if (!pd.mhint && rr.status == INF_END) pd.mhint = (uint8_t)((rr.err >> INF_HINT_MLEV_SHIFT) & 15u);
         avail = pd.size - rr.consumed;
         st = (int)rr.status;
       } else if (pd.state == INF_END) {  // inflate() in DONE mode returns Z_STREAM_END again
@@ -1186,9 +1189,10 @@ static int inflate_records(atz_ctx* c, const uint8_t* d_file, uint64_t F, size_t
 
 // ---------------------------------------------------------------------------------------------
 // Phase 3
-// Hash buckets per (stream, memLevel), built on demand by k_buckets and cached in HBM for the
-// sweep (8 bytes per position).  When a round would push the cache past its cap the cache is
-// dropped and the round's tables are rebuilt.
+// Hash buckets per (stream, memLevel), built on demand and cached for the sweep (8 bytes per
+// position) in the context's DevArena chain_arena, up to CHAIN_CACHE_CAP.  Past the cap, a round
+// builds its missing tables in its pipe's own d_chains (Pipe::tmp_chains), which forget_tmp_chains
+// drops at the round's end.
 static constexpr uint64_t CHAIN_CACHE_CAP = 48ull << 30;
 static bool bucket_verify() {   // ATZ_BUCKETS_VERIFY=1 (read per call): check k_buckets_sort against the others
   const char* e = std::getenv("ATZ_BUCKETS_VERIFY");
@@ -1451,19 +1455,14 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
 // 1442-1491 MB/s (reruns 105 k -> 29 k, k_trial 648-663 -> 559-565 ms summed); 50 000 streams
 // 1270-1315 vs 1279-1282; 25 000 947-968 vs 938-967; 12 500 669-673 vs 684-686 (a small sweep's rounds
 // are latency-bound, and the hinted trials' whole tables lengthen the first pass).  So: sweeps of more
-// than 16 000 streams (ATZ_MHINT=0 / 1 forces it off / on)
-// ATZ_HDEPTH=1: a round runs a hinted stream's list at least through its next entry at the hinted
-// memLevel (speculation up to the likely winner; its whole table is built whatever the sweep's size)
-static bool hdepth_on() {
-  static const bool on = [] { const char* e = std::getenv("ATZ_HDEPTH"); return e && std::atoi(e) != 0; }();
-  return on;
-}
+// than 16 000 streams (ATZ_MHINT=0 / 1 forces it off / on).  (Speculating through a hinted stream's
+// list up to its next entry at the hinted memLevel measured slower: DESIGN.md s3.6.)
 // A small sweep on six pipes (one rank's share at 8 GPUs) gains from it too (12 500 streams, same box,
 // 3 runs each: 697-716 -> 741-776 MB/s; with the 3072 prefix floor 749-802), one on three pipes does not.
 static bool big_sweep(const atz_ctx* x) { return x->recs.size() > 16000 || x->pipes_running >= 6; }
 static bool mhint_on(const atz_ctx* x) {
   static const int v = [] { const char* e = std::getenv("ATZ_MHINT"); return e ? std::atoi(e) : -1; }();
-  return v < 0 ? big_sweep(x) || hdepth_on() : v != 0;
+  return v < 0 ? big_sweep(x) : v != 0;
 }
 // Match-table prefix for a trial that may stop early: enough positions for the blocks that decide
 // the shortcut (~3 positions per symbol, lit_bufsize symbols per block); the rest on demand.  The
@@ -1553,18 +1552,10 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
 // (k_trial_{fast,slow}_mw: one parse wave, MW_F flusher waves; k_deflate.hip MWSlot).  Their symbols
 // stay in HBM for the whole stream (the flushers read each block at its own offset).
 static uint32_t mw_max_memlevel() {   // ATZ_MW=m: multi-wave up to memLevel m (0: none; tests/test_gpu_knobs.py)
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_MW"); v = e ? std::max(0, std::min(9, std::atoi(e))) : 2; }
+  static const int v = [] { const char* e = std::getenv("ATZ_MW"); return (int)(e ? std::max(0, std::min(9, std::atoi(e))) : 2); }();
   return (uint32_t)v;
 }
 static bool mw_trial(int kind, uint32_t memlevel) { return kind != 0 && memlevel <= mw_max_memlevel(); }
-// ATZ_INS16=1: a fast trial whose stream has at most INS_SMALL positions runs on the 2 KiB insertion
-// ring (more fast trials per CU).  Off by default: measured slower (C4 1295-1332 vs 1476-1482 MB/s,
-// k_trial 814-828 vs 630-646 ms summed; the 12 500-stream share 515-536 vs 670-690; gpurun_out/ins16)
-static bool ins_small(atz_ctx* x, const Trial& t) {
-  static const bool on = [] { const char* e = std::getenv("ATZ_INS16"); return e && std::atoi(e) != 0; }();
-  return on && x->recs[t.stream].infl_len <= INS_SMALL;
-}
 static uint64_t sym_words(int kind, uint32_t memlevel, uint64_t n) {   // symbol buffer of a trial (u32 units)
   return (mw_trial(kind, memlevel) ? n + 64 : 0) + (1ull << (memlevel + 6)) + 64;
 }
@@ -1594,12 +1585,9 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
                (uint64_t)((t.mode & 8) ? 1 : 4);   // replays skip the match walks
       S.perm[k][q] = (uint32_t)q;
     }
-    // (fast kind: then the trials whose insertion ring fits INS_SMALL bits, a launch of their own)
     std::stable_sort(S.perm[k].begin(), S.perm[k].end(), [&](uint32_t a, uint32_t b) {
       const bool ma = mw_trial(k, in[k][a].memlevel), mb = mw_trial(k, in[k][b].memlevel);
-      if (ma != mb) return ma;
-      const bool sa = k == 1 && ins_small(x, in[k][a]), sb = k == 1 && ins_small(x, in[k][b]);
-      return sa != sb ? sa : key[a] > key[b];
+      return ma != mb ? ma : key[a] > key[b];
     });
     S.tr[k].resize(n);
     for (size_t q = 0; q < n; q++) S.tr[k][q] = in[k][S.perm[k][q]];
@@ -1607,11 +1595,10 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
   }
   S.base = 0;
 }
-// the trial kernels over h[0, cnt) (one kind, multi-wave ones first, each group's small-ring fast trials
-// first), at slots [base, base + cnt)
+// the trial kernels over h[0, cnt) (one kind, multi-wave ones first), at slots [base, base + cnt)
 static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepOpts& so, int k, const Trial* h,
                          size_t cnt, size_t base) {
-  auto launch1 = [&](const Trial* hh, size_t n1, size_t b1, bool mw, bool small) -> int {
+  auto launch1 = [&](const Trial* hh, size_t n1, size_t b1, bool mw) -> int {
     HIPCHK(pipe_copy(c, c->d_trials.as<Trial>() + b1, hh, n1 * sizeof(Trial), hipMemcpyHostToDevice));
     SweepArgs A;
     A.file = d_cmp; A.infl = INFL_BASE; A.chains = CHAIN_BASE;
@@ -1620,27 +1607,22 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
     A.res = c->d_tres.as<TrialRes>() + b1; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
     A.adler = x->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)n1;
     dim3 g((uint32_t)n1), b(mw ? MW_THREADS : 64);
-    // ATZ_XLDS=n (diagnostics): n bytes of unused dynamic LDS per trial block, to see how much the
-    // trial kernels' LDS footprint limits the sweep when they share the CUs with the table kernels
-    static const uint32_t xlds = [] { const char* e = std::getenv("ATZ_XLDS"); return e ? (uint32_t)std::atoi(e) : 0u; }();
     kbeg(c, 0);
-    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, xlds, c->st, A);
-    else if (k == 1 && mw && small) hipLaunchKernelGGL(k_trial_fast_mw<INS_SMALL>, g, b, xlds, c->st, A);
-    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw<BITMAP_BITS>, g, b, xlds, c->st, A);
-    else if (k == 1 && small) hipLaunchKernelGGL(k_trial_fast<INS_SMALL>, g, b, xlds, c->st, A);
-    else if (k == 1) hipLaunchKernelGGL(k_trial_fast<BITMAP_BITS>, g, b, xlds, c->st, A);
-    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, xlds, c->st, A);
-    else hipLaunchKernelGGL(k_trial_slow, g, b, xlds, c->st, A);
+    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
+    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw<BITMAP_BITS>, g, b, 0, c->st, A);
+    else if (k == 1) hipLaunchKernelGGL(k_trial_fast<BITMAP_BITS>, g, b, 0, c->st, A);
+    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, 0, c->st, A);
+    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
     kend(c);
     KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
     return 0;
   };
   size_t i = 0;
-  while (i < cnt) {   // runs of equal (multi-wave, small ring): trials_order made them contiguous
-    const bool mw = mw_trial(k, h[i].memlevel), small = k == 1 && ins_small(x, h[i]);
+  while (i < cnt) {   // runs of equal multi-wave-ness: trials_order made them contiguous
+    const bool mw = mw_trial(k, h[i].memlevel);
     size_t j = i + 1;
-    while (j < cnt && mw_trial(k, h[j].memlevel) == mw && (k == 1 && ins_small(x, h[j])) == small) j++;
-    if (int r = launch1(h + i, j - i, base + i, mw, small)) return r;
+    while (j < cnt && mw_trial(k, h[j].memlevel) == mw) j++;
+    if (int r = launch1(h + i, j - i, base + i, mw)) return r;
     i = j;
   }
   return 0;
@@ -1765,8 +1747,7 @@ static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Tri
 // ATZ_REPLAY=0 disables symbol replay (every trial parses); 2 saves sequences but never replays them,
 // 3 replays only between budget-free trials (diagnostics)
 static int replay_mode() {
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_REPLAY"); v = e ? std::atoi(e) : 1; }
+  static const int v = [] { const char* e = std::getenv("ATZ_REPLAY"); return (int)(e ? std::atoi(e) : 1); }();
   return v;
 }
 static bool replay_on() { return replay_mode() != 0; }
@@ -1775,8 +1756,7 @@ static constexpr uint64_t RP_ARENA_CAP = 24ull << 30;   // saved sequences, all 
 // a trial replays entry e's saved sequence: unchecked if budget-free, else against the saved reads
 // ATZ_DEDUP=0: launch duplicate trials anyway (diagnostics)
 static bool dedup_on() {
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_DEDUP"); v = e ? std::atoi(e) : 1; }
+  static const int v = [] { const char* e = std::getenv("ATZ_DEDUP"); return (int)(e ? std::atoi(e) : 1); }();
   return v != 0;
 }
 // A budget-free replay whose saved sequence fits one block of both its own and the saver's
@@ -1910,72 +1890,46 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
   }
 }
 
+// Trials that cannot make their stream recompressible.  The ATZ1 records a stream only if its best
+// trial differs from the original in at most recomp_tresh bytes (main.cpp:454), so a trial whose
+// mismatches already exceed recomp_tresh (ident <= C - recomp_tresh - 1 whatever follows) changes the
+// file only through the stream's running best ident -- and it cannot change that either:
+//  * every recompressible trial's ident exceeds every such trial's, so the recompressible
+//    improvements (and with them the chosen c, w, m and the diffs) are the same with or without it;
+//  * with mismatch_tol <= recomp_tresh it cannot meet the stop rule (ident + tol >= C, main.cpp:700),
+//    nor change the brute-window test (C - ident >= tol, main.cpp:590: true either way).
+// So such a trial may stop as soon as its mismatches pass recomp_tresh: its best_ident is raised to
+// C - recomp_tresh - 1 and the kernels' "cannot beat" exit does the rest (early_exit).  Only the
+// reference's unobservable ident / c, w, m of streams it does not recompress change, which is why
+// atz_sweep (which reports them) keeps the exact rule.  Symbol-saving trials keep it too: their
+// whole sequence serves the stream's replays.  ATZ_ELIG=0 turns it off (tests/test_gpu_knobs.py).
+static uint64_t elig_floor(const atz_ctx* x, uint64_t C) {
+  static const bool on = [] { const char* e = std::getenv("ATZ_ELIG"); return !e || std::atoi(e) != 0; }();
+  if (!on || x->exact_idents || x->o.mismatch_tol > x->o.recomp_tresh || C <= x->o.recomp_tresh) return 0;
+  return C - x->o.recomp_tresh - 1;
+}
+
 // match tables + output scratch of one round, over all pipes
 static constexpr uint64_t ROUND_BUDGET_BYTES = 24ull << 30;
 
-// Sweep scheduling (ATZ_SCHED).  Streams wait in queues for their next step; a pipe takes a batch,
-// runs one round on it (each stream's next K trials: tables, trial launches, the reference's rule per
-// stream) and hands back the streams that have not stopped.
-//  * rounds (default): each pipe sweeps a fixed interleaved share of the streams, all of them in every
-//    round; a trial that parsed past its match-table prefix (TR_NEED_R) is rerun with its whole table
-//    inside the round, before its stream's rule walk goes on.
-//  * flow (ATZ_SCHED=flow): the pipes share one queue and take batches of at most 1/pipes of the
-//    unfinished streams, so a stream's next step starts as soon as its own round is done; a TR_NEED_R
-//    trial reruns as the stream's next step (front of the queue) with its whole table, and speculative
-//    rounds (K > 1) build whole tables up front.  Measured slower than rounds on one MI355X (DESIGN.md
-//    s3.6: C4 1276-1341 vs 1442-1468 MB/s, a 12 500-stream share 504-598 vs 606-672): the trial
-//    kernels are issue-bound with about a thousand trial waves resident, so freeing streams from the
-//    round barrier adds concurrency the GPU cannot use and costs rounds.
-// ATZ_FULLK=1: speculative rounds (K > 1) build whole match tables up front under the rounds scheduler too
-static bool fullk_on() {
-  static const bool v = [] { const char* e = std::getenv("ATZ_FULLK"); return e && std::atoi(e) != 0; }();
-  return v;
-}
-// ATZ_REBALANCE=1: a rounds-scheduler pipe whose share is done takes part of another pipe's (measured
-// neutral on C4 and on a 12 500-stream share, DESIGN.md s3.6: off by default)
-static bool rebalance_on() {
-  static const bool v = [] { const char* e = std::getenv("ATZ_REBALANCE"); return e && std::atoi(e) != 0; }();
-  return v;
-}
-static constexpr size_t SHARE_MIN = 64;
-static size_t kref_pipes() {
-  static const size_t v = [] { const char* e = std::getenv("ATZ_KREF"); return e ? (size_t)std::max(0, std::atoi(e)) : (size_t)0; }();
-  return v;
-}   // streams per part when a pipe splits its share
-static bool sched_flow() {
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_SCHED"); v = e && std::string(e) == "flow"; }
-  return v == 1;
-}
-// Pipe g's next batch into `batch` (false: the sweep is over for this pipe); unf = streams not done.
-static bool sched_take(atz_ctx* x, int g, size_t np, std::vector<uint32_t>& batch, size_t& unf) {
+// Sweep scheduling.  Every pipe sweeps a fixed interleaved share of the streams (sweep_publish), all
+// of them in every round: it takes its queue (sched_take), runs one round on it (each stream's next K
+// trials: tables, trial launches, the reference's rule per stream; a trial that parsed past its
+// match-table prefix, TR_NEED_R, is rerun with its whole table inside the round, before its stream's
+// rule walk goes on) and hands back the streams that have not stopped (sched_give).  Measured and not
+// kept: one queue shared by the pipes with each stream's next step as soon as its own
+// round is done, a done pipe taking part of another's share, whole match tables for speculative rounds.
+// Pipe g's next batch into `batch` (false: the sweep is over for this pipe).
+static bool sched_take(atz_ctx* x, int g, std::vector<uint32_t>& batch) {
   auto& Q = x->sched;
   std::unique_lock<std::mutex> lk(Q.mu);
   batch.clear();
   auto stop = [&] { return Q.abort || x->sweep_abort.load(std::memory_order_relaxed); };
-  if (!Q.flow) {
-    // a pipe whose own streams are done waits for a share of another's (sched_give) until all are done
-    std::deque<uint32_t>& q = Q.q[g];
-    auto all_done = [&] {
-      for (size_t u : Q.unfinished) if (u) return false;
-      return true;
-    };
-    Q.cv.wait(lk, [&] { return stop() || !q.empty() || (Q.closed && all_done()); });
-    if (stop() || q.empty()) return false;
-    batch.assign(q.begin(), q.end());
-    q.clear();
-    unf = 0;   // streams not done, over all pipes
-    for (size_t u : Q.unfinished) unf += u;
-    return true;
-  }
-  std::deque<uint32_t>& q = Q.q[0];
-  Q.cv.wait(lk, [&] { return stop() || !q.empty() || (Q.closed && Q.unfinished[0] == 0); });
+  std::deque<uint32_t>& q = Q.q[g];
+  Q.cv.wait(lk, [&] { return stop() || !q.empty() || (Q.closed && Q.unfinished[g] == 0); });
   if (stop() || q.empty()) return false;
-  unf = Q.unfinished[0];
-  const size_t cap = std::max<size_t>(64, (unf + np - 1) / np);
-  const size_t m = std::min(cap, q.size());
-  batch.assign(q.begin(), q.begin() + (long)m);
-  q.erase(q.begin(), q.begin() + (long)m);
+  batch.assign(q.begin(), q.end());
+  q.clear();
   return true;
 }
 // After a round: the batch's streams that have not stopped go back (`waiting`, which the round's
@@ -1984,41 +1938,11 @@ static void sched_give(atz_ctx* x, int g, const std::vector<StreamState>& ss, co
                        const std::vector<uint32_t>& waiting) {
   auto& Q = x->sched;
   std::lock_guard<std::mutex> lk(Q.mu);
+  std::vector<uint32_t> front(waiting);
   size_t done = 0;
-  if (!Q.flow) {
-    std::vector<uint32_t> front(waiting);
-    for (uint32_t s : active) { if (ss[s].phase == 2) done++; else front.push_back(s); }
-    Q.unfinished[g] -= done;
-    // The pipes' shares finish at different times (two of three pipes share a hardware queue; C4: the
-    // last pipe ended 130 ms after the first), so a pipe with streams left splits them with the pipes
-    // whose own streams are done, interleaved (the same mix of classes for each)
-    std::vector<int> idle;
-    for (int p = 0; p < (int)Q.q.size(); p++)
-      if (p != g && Q.unfinished[p] == 0 && Q.q[p].empty()) idle.push_back(p);
-    const size_t parts = std::min(idle.size() + 1, front.size() / SHARE_MIN);
-    if (parts > 1 && rebalance_on()) {
-      std::vector<uint32_t> keep;
-      for (size_t i = 0; i < front.size(); i++) {
-        const size_t k = i % parts;
-        if (k == 0) { keep.push_back(front[i]); continue; }
-        Q.q[idle[k - 1]].push_back(front[i]);
-        Q.unfinished[idle[k - 1]]++;
-        Q.unfinished[g]--;
-      }
-      front.swap(keep);
-    }
-    Q.q[g].insert(Q.q[g].begin(), front.begin(), front.end());
-    Q.cv.notify_all();
-    return;
-  } else {
-    Q.q[0].insert(Q.q[0].begin(), waiting.begin(), waiting.end());
-    for (uint32_t s : active) {
-      if (ss[s].phase == 2) { done++; continue; }
-      if (ss[s].full_at == ss[s].idx) Q.q[0].push_front(s);   // a rerun: next in line
-      else Q.q[0].push_back(s);
-    }
-  }
-  Q.unfinished[Q.flow ? 0 : g] -= done;
+  for (uint32_t s : active) { if (ss[s].phase == 2) done++; else front.push_back(s); }
+  Q.unfinished[g] -= done;
+  Q.q[g].insert(Q.q[g].begin(), front.begin(), front.end());
   Q.cv.notify_all();
 }
 static void sched_abort(atz_ctx* x) {
@@ -2034,9 +1958,6 @@ static size_t round_target(const atz_ctx* x);
 static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
   auto t0 = std::chrono::steady_clock::now();
   std::vector<uint32_t> active;
-  const bool flow = x->sched.flow;
-  const size_t np = x->pipes_running;
-  size_t unf = 0;
   SweepOpts so{x->o.recomp_tresh, x->o.sizediff_tresh, x->o.shortcut_len, x->o.mismatch_tol};
   uint64_t rounds = 0, ntr = 0, nsc = 0, nhz = 0, nspec = 0;
   std::vector<Trial> tr[3];
@@ -2045,7 +1966,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
   // stops at its j-th trial discards the results of the later ones), K sized so the rounds fill the
   // GPU.  Results are applied per stream strictly in list order, so the outcome is the
   // reference's sequential one; the speculation only changes how much work runs per launch.
-  while (sched_take(x, c->id, np, active, unf)) {
+  while (sched_take(x, c->id, active)) {
     rounds++;
     std::vector<uint32_t> waiting;
     struct Give {   // the batch goes back on every exit from the round (an error aborts the sweep anyway)
@@ -2053,13 +1974,8 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       ~Give() { forget_tmp_chains(x, c); sched_give(x, c->id, ss, a, w); }
     } give{x, c, ss, active, waiting};
     const auto tl0 = std::chrono::steady_clock::now();
-    // speculation depth: `target` trials per round and pipe; ATZ_KREF=n sizes it as if n pipes shared
-    // the unfinished streams (more pipes then overlap more rounds without speculating deeper)
-    const size_t kref = kref_pipes();
-    const size_t target = round_target(x);
-    const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, flow ? target * np / std::max<size_t>(1, unf)
-                                                                       : kref ? target * kref / std::max<size_t>(1, unf)
-                                                                              : target / active.size()));
+    // speculation depth: `target` trials per round and pipe
+    const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, round_target(x) / active.size()));
     std::vector<std::pair<uint32_t, int>> need;
     std::vector<uint32_t> need_b;   // per need entry: the trial's walk budget (replay's budget-free test)
     for (int k = 0; k < 3; k++) tr[k].clear();
@@ -2074,10 +1990,6 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       mbeg[a] = (uint32_t)mine.size();
       const uint32_t s = active[a];
       StreamState& st = ss[s];
-      uint32_t Ks = K;
-      if (hdepth_on() && x->recs[s].mhint)
-        for (uint32_t j = 0; j < 64 && st.idx + j < st.list->size(); j++)
-          if (((*st.list)[st.idx + j] & 0xffu) == x->recs[s].mhint) { Ks = std::max(Ks, j + 1); break; }
       // scratch of a round (match tables, outputs, symbols) is bounded: streams past the budget
       // wait for the next round, where they go first
       if (a > 0 && round_bytes > round_budget) {
@@ -2085,15 +1997,12 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         active.resize(a);
         break;
       }
-      for (uint32_t j = 0; j < Ks && st.idx + j < st.list->size(); j++) {
+      for (uint32_t j = 0; j < K && st.idx + j < st.list->size(); j++) {
         uint32_t p = (*st.list)[st.idx + j];
         int cl = (int)(p >> 16), w = (int)((p >> 8) & 0xff), m = (int)(p & 0xff);
         Trial t{};
         t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
         t.best_ident = st.ident;
-        // host-only bit 1: whole match table up front -- a deferred rerun, or any trial of a speculative
-        // flow round (K > 1: the sweep's tail, where a rerun's extra step would lengthen the stream's chain)
-        if (st.idx + j == st.full_at || (K > 1 && (flow || fullk_on()))) t.mode |= 2;
         t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
         int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
@@ -2123,6 +2032,9 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         for (const Trial& t : tr[k])
           if ((t.mode & 24) != 8 && !(t.mode & 128)) need.push_back({t.stream, (int)t.memlevel});
     }
+    for (int k = 0; k < 3; k++)
+      for (Trial& t : tr[k])
+        if (!(t.mode & 4)) t.best_ident = std::max(t.best_ident, elig_floor(x, x->recs[t.stream].comp_len));
     size_t nbuild = 0;
     for (auto& q : need) nbuild += x->chain_off[q.first][q.second] == ~0ull;
     if (int r = ensure_chains(x, c, need)) return r;   // (stream-ordered before the match walks: no sync)
@@ -2244,12 +2156,6 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         const TrialRes& r = trres[mine[j].first][mine[j].second];
         if (r.state == TR_NEED_R) {
           if (!defer) return ATZ_E_INTERNAL;   // every rerun a walk waits for has run
-          if (flow) {   // rerun as the stream's next step (its later trials of this round are discarded)
-            st.full_at = st.idx;
-            nspec += mbeg[a + 1] - j - 1;
-            c->stats.n_trials_rerun++;
-            break;
-          }
           jpos[a] = j;
           held[a] = 1;
           return 0;
@@ -2282,7 +2188,6 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         if (st.idx >= st.list->size()) {
           if (st.phase == 0 && (C - st.ident) >= x->o.mismatch_tol && x->o.brute_window) {
             st.list = &trial_list(x->recs[s].type, true);
-            st.full_at = ~0u;
             st.idx = 0;
             st.phase = 1;
           } else {
@@ -2532,9 +2437,8 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
   {
     auto& Q = c->sched;
     std::lock_guard<std::mutex> lk(Q.mu);
-    Q.flow = sched_flow();
-    Q.q.assign(Q.flow ? 1 : R.np, std::deque<uint32_t>());
-    Q.unfinished.assign(Q.flow ? 1 : R.np, 0);
+    Q.q.assign(R.np, std::deque<uint32_t>());
+    Q.unfinished.assign(R.np, 0);
     Q.closed = false;
     Q.abort = false;
     Q.published = 0;
@@ -2575,13 +2479,8 @@ static int sweep_publish(atz_ctx* c, SweepRun& R, size_t r0, size_t r1) {
   {
     auto& Q = c->sched;
     std::lock_guard<std::mutex> lk(Q.mu);
-    if (Q.flow) {
-      for (size_t s = r0; s < r1; s++) Q.q[0].push_back((uint32_t)s);
-      Q.unfinished[0] += r1 - r0;
-    } else {
-      // interleaved over the pipes by global index: every pipe gets the same mix of classes and sizes
-      for (size_t s = r0; s < r1; s++) { Q.q[s % R.np].push_back((uint32_t)s); Q.unfinished[s % R.np]++; }
-    }
+    // interleaved over the pipes by global index: every pipe gets the same mix of classes and sizes
+    for (size_t s = r0; s < r1; s++) { Q.q[s % R.np].push_back((uint32_t)s); Q.unfinished[s % R.np]++; }
     Q.published = r1;
     Q.cv.notify_all();
   }
@@ -2804,8 +2703,7 @@ static int write_impl(atz_ctx* c, const uint8_t* d_file, uint64_t F, const std::
 }
 
 static bool spec_cont_on() {   // ATZ_SPEC_CONT=0: the scan waits for the first continuations
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_SPEC_CONT"); v = e ? std::atoi(e) : 1; }
+  static const int v = [] { const char* e = std::getenv("ATZ_SPEC_CONT"); return (int)(e ? std::atoi(e) : 1); }();
   return v != 0;
 }
 static bool spec_abort_test() {   // ATZ_SPEC_ABORT_TEST=1 (read per call): withdraw the speculative sweep
@@ -2873,9 +2771,13 @@ static int precompress_dev(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
     if (int r = inflate_records(c, d_file, F, 0, r1, *c->slabs[0])) return r;
     if (int r = sweep_publish(c, R, 0, r1)) return r;
     TMARK("scan: speculative records out");
-    if (c->on_records) {   // ATZ1 <= header + every record's descriptor (diffs aside) + payload + the file
+    if (c->on_records) {
+      // the ATZ1 size if every speculative record is recompressed with up to recomp_tresh diffs (9 bytes
+      // each: delta + value), plus the whole file as residue.  Records the continuations add are not in
+      // it; HostOut::take reallocates (and says so under ATZ_TIMING) if the file turns out larger.
       uint64_t est = F + 4096;
-      for (size_t s = 0; s < r1; s++) est += c->recs[s].infl_len + 64;
+      for (size_t s = 0; s < r1; s++)
+        est += c->recs[s].infl_len + 64 + 9 * std::min<uint64_t>(c->o.recomp_tresh, c->recs[s].comp_len);
       c->on_records(est);
     }
     if (int r = scan_continuations(c, h, d_file, S, 0, nch)) return r;
@@ -3259,8 +3161,7 @@ static void shard_range(uint32_t nch, int rank, int world, uint32_t& ja, uint32_
 // computes the same split from the same record list (the hints travel in the scan blobs).  Records
 // another rank's scan decoded are inflated again here (their scan output stays in that rank's arena).
 static bool split_hint_on() {   // ATZ_SPLIT_HINT=0: round 3's fixed class weights (class 3: 20), no hint
-  static int v = -1;
-  if (v < 0) { const char* e = std::getenv("ATZ_SPLIT_HINT"); v = e ? std::atoi(e) : 1; }
+  static const int v = [] { const char* e = std::getenv("ATZ_SPLIT_HINT"); return (int)(e ? std::atoi(e) : 1); }();
   return v != 0;
 }
 static uint64_t shard_cost(const Rec& r) {
@@ -3536,7 +3437,10 @@ int atz_sweep(atz_ctx_t* c, const atz_cand_t* cands, uint64_t n, atz_result_t* r
     if (c->slabs.empty()) c->slabs.emplace_back(new DBuf());
     if (int r = inflate_records(c, c->d_file.as<uint8_t>(), c->flen, 0, c->recs.size(), *c->slabs[0])) return r;
     std::vector<StreamState> ss;
-    if (int r = sweep_impl(c, c->d_file.as<uint8_t>(), ss)) return r;
+    c->exact_idents = true;   // every stream's result is reported (elig_floor)
+    const int rs = sweep_impl(c, c->d_file.as<uint8_t>(), ss);
+    c->exact_idents = false;
+    if (rs) return rs;
     uint64_t nd = 0;
     for (auto& s : ss) if (s.recomp) nd += s.rawdiff.size();
     uint64_t* dof = (uint64_t*)std::malloc((nd + 1) * 8);
@@ -3600,6 +3504,9 @@ struct HostOut {
     join();
     uint8_t* r = p;
     if (r && n > cap + 1) {
+      if (timing_on())
+        std::fprintf(stderr, "atz: host ATZ1 buffer: %llu bytes estimated, %llu needed (reallocated, unregistered copy)\n",
+                     (unsigned long long)cap, (unsigned long long)n);
       unreg();
       uint8_t* g = (uint8_t*)std::realloc(r, n);
       if (!g) std::free(r);

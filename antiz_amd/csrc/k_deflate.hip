@@ -906,9 +906,8 @@ struct TrialShared {
   // used while a block is emitted, when the parse is paused (like TreeScratch during build_tree)
 };
 
-// INS: bits of the insertion ring, position mod INS.  32768 serves every stream; a stream of at most
-// 16384 positions never aliases in 16384 bits, and its trials take 2 KiB less LDS (14 waves per CU
-// instead of 11: the fast kind is the LDS-bound one)
+// INS: bits of the insertion ring, position mod INS (BITMAP_BITS serves every stream; a 16 Kibit ring
+// for streams of at most 16384 positions, 2 KiB less LDS, measured slower: DESIGN.md s3.5)
 template <uint32_t INS>
 struct TrialSharedFast {
   static constexpr uint32_t INS_BITS = INS;
@@ -917,7 +916,6 @@ struct TrialSharedFast {
   uint32_t ins[INS / 32];   // insertion ring (InsRing)
   uint32_t holes[HOLE_SLOTS];   // position + 1 of the latest non-inserted position with hash & (SLOTS-1)
 };
-static constexpr uint32_t INS_SMALL = 16384;
 
 static constexpr uint32_t RING_SLOW = 512;   // >= 127 + 2 * 258 + 64: a walk never leaves the ring
 struct TrialSharedSlow {
@@ -2770,7 +2768,7 @@ __global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_stored(SweepArgs
   __shared__ struct { TrialShared t; uint64_t ring[(STAGE_WORDS + 1) / 2]; } shm;   // ring: staging only
   trial_body<0>(A, shm, threadIdx.x);
 }
-template <uint32_t INS>   // INS_SMALL: streams of at most INS_SMALL positions only (host side)
+template <uint32_t INS>
 __global__ __launch_bounds__(64, TRIAL_SLOW_WAVES) void k_trial_fast(SweepArgs A) {
   __shared__ TrialSharedFast<INS> shm;
   trial_body<1>(A, shm, threadIdx.x);

@@ -11,15 +11,11 @@ the ATZ1 bytes must equal the oracle's (the reference's algorithm, oracle/) for 
                streams, else 4096)
   ATZ_SPEC_CONT 0: the scan waits for the first chunk-boundary continuations (default 1: speculative)
   ATZ_MW       multi-wave trials up to this memLevel (default 2; 0: every trial on one wave)
-  ATZ_REBALANCE 1: a pipe whose share is done takes part of another pipe's (default 0)
-  ATZ_INS16    1: fast trials of streams of at most 16384 positions on the 16 Kibit insertion ring (default 0)
-  ATZ_MHINT    0 / 1: whole match tables for the first block's memLevel off / on (default: above 16 000 streams)
-  ATZ_HDEPTH   1: a round runs a hinted stream's list through its next entry at the hinted memLevel
-  ATZ_PREFIX_MIN the match-table prefix floor in positions (default 3072 above 16 000 streams, else 1024)
-  ATZ_FULLK    1: speculative rounds (K > 1) build whole match tables up front
-  ATZ_SCHED    flow: one queue shared by the pipes, each stream's next step as soon as its own round is
-               done, reruns as the stream's next step (default rounds: every pipe sweeps a fixed share
-               of the streams in lock-step rounds; atz_accel.cpp sched_take)
+  ATZ_MHINT    0 / 1: whole match tables for the first block's memLevel off / on (default: above 16 000
+               streams, or on six or more pipes: atz_accel.cpp big_sweep)
+  ATZ_PREFIX_MIN the match-table prefix floor in positions (default 3072 where big_sweep holds, else 1024)
+  ATZ_ELIG     0: every trial keeps the reference's exact rule to its end (default 1: a trial stops once
+               it cannot make its stream recompressible; atz_accel.cpp elig_floor)
 """
 import hashlib
 import os
@@ -36,10 +32,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SETTINGS = [{"ATZ_REPLAY": "0"}, {"ATZ_REPLAY": "2"}, {"ATZ_REPLAY": "3"}, {"ATZ_DEDUP": "0"},
             {"ATZ_PIPES": "1"}, {"ATZ_PIPES": "5"}, {"GPU_MAX_HW_QUEUES": "8"}, {"ATZ_TARGET": "256"}, {"ATZ_TARGET": "65536"},
             {"ATZ_SPEC_CONT": "0"}, {"ATZ_MW": "0"}, {"ATZ_MW": "9"}, {"ATZ_REPLAY": "0", "ATZ_DEDUP": "0", "ATZ_PIPES": "2", "ATZ_SPEC_CONT": "0"},
-            {"ATZ_SCHED": "flow"}, {"ATZ_SCHED": "flow", "ATZ_PIPES": "5", "ATZ_TARGET": "256"},
-            {"ATZ_SCHED": "flow", "ATZ_PIPES": "8", "ATZ_TARGET": "65536"}, {"ATZ_PIPES": "8", "ATZ_TARGET": "256"},
-            {"ATZ_REBALANCE": "1"}, {"ATZ_KREF": "3", "ATZ_PIPES": "6"}, {"ATZ_XLDS": "4096"}, {"ATZ_FULLK": "1", "ATZ_TARGET": "65536"},
-            {"ATZ_INS16": "1"}, {"ATZ_MHINT": "1"}, {"ATZ_MHINT": "0"}, {"ATZ_HDEPTH": "1"}, {"ATZ_PREFIX_MIN": "3072", "ATZ_MHINT": "1"}]
+            {"ATZ_PIPES": "8", "ATZ_TARGET": "256"}, {"ATZ_PIPES": "6", "ATZ_TARGET": "65536"},
+            {"ATZ_MHINT": "1"}, {"ATZ_MHINT": "0"}, {"ATZ_PREFIX_MIN": "3072", "ATZ_MHINT": "1"},
+            {"ATZ_ELIG": "0"}, {"ATZ_ELIG": "0", "ATZ_REPLAY": "0"}]
 
 RUN = r"""
 import hashlib, sys
