@@ -1951,40 +1951,54 @@ static void sched_abort(atz_ctx* x) {
   x->sched.cv.notify_all();
 }
 
-// The sweep work of pipe c: rounds on the batches sched_take hands it (per-kind x level counters:
-// count, cycles total/tree/emit/heap/fallback, parsed bytes, symbols, scan/send cycles, parse window
-// phases).
 static size_t round_target(const atz_ctx* x);
-static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
-  auto t0 = std::chrono::steady_clock::now();
-  std::vector<uint32_t> active;
-  SweepOpts so{x->o.recomp_tresh, x->o.sizediff_tresh, x->o.shortcut_len, x->o.mismatch_tol};
-  uint64_t rounds = 0, ntr = 0, nsc = 0, nhz = 0, nspec = 0;
-  std::vector<Trial> tr[3];
+// One round of pipe c over its batch `active`: the next K list entries of every stream (speculatively:
+// a stream that stops at its j-th trial discards the results of the later ones), K sized so the rounds
+// fill the GPU.  Results are applied per stream strictly in list order, so the outcome is the
+// reference's sequential one; the speculation only changes how much work runs per launch.
+struct Round {
+  atz_ctx* x; Pipe* c; const uint8_t* d_file; std::vector<StreamState>& ss; const SweepOpts& so;
+  std::vector<uint32_t>& active;
+  std::vector<uint32_t>& waiting;   // streams the round's scratch budget left out (next round, first)
+  uint32_t K = 1;
+  std::vector<Trial> tr[3];         // k = 0 stored, 1 fast, 2 slow levels
   std::vector<TrialRes> trres[3];
-  // A round evaluates the next K trials of every stream of the batch (speculatively: a stream that
-  // stops at its j-th trial discards the results of the later ones), K sized so the rounds fill the
-  // GPU.  Results are applied per stream strictly in list order, so the outcome is the
-  // reference's sequential one; the speculation only changes how much work runs per launch.
-  while (sched_take(x, c->id, active)) {
-    rounds++;
-    std::vector<uint32_t> waiting;
-    struct Give {   // the batch goes back on every exit from the round (an error aborts the sweep anyway)
-      atz_ctx* x; Pipe* c; const std::vector<StreamState>& ss; const std::vector<uint32_t>& a, &w;
-      ~Give() { forget_tmp_chains(x, c); sched_give(x, c->id, ss, a, w); }
-    } give{x, c, ss, active, waiting};
-    const auto tl0 = std::chrono::steady_clock::now();
-    // speculation depth: `target` trials per round and pipe
-    const uint32_t K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, round_target(x) / active.size()));
-    std::vector<std::pair<uint32_t, int>> need;
-    std::vector<uint32_t> need_b;   // per need entry: the trial's walk budget (replay's budget-free test)
-    for (int k = 0; k < 3; k++) tr[k].clear();
-    // per stream, its trials of this round in list order: (kind, index in tr[kind])
-    // flat: stream a's trials are mine[mbeg[a] .. mbeg[a + 1])
-    std::vector<std::pair<int, uint32_t>> mine;
-    std::vector<uint32_t> mbeg(active.size() + 1);
+  // per stream, its trials of this round in list order: stream a's are mine[mbeg[a] .. mbeg[a + 1]),
+  // each (kind, index in tr[kind])
+  std::vector<std::pair<int, uint32_t>> mine;
+  std::vector<uint32_t> mbeg;
+  std::vector<std::pair<uint32_t, int>> need;   // (stream, memLevel) pairs whose bucket tables trials read
+  std::vector<uint32_t> need_b;                 // per need entry: the trial's walk budget (budget-free test)
+  std::vector<std::array<uint32_t, 4>> savers;  // (kind, index in tr[kind], rp_pool entry, level - 1)
+  uint64_t out_tot = 0, sym_tot = 0;
+  size_t nbuild = 0;
+  // streams of the batch by index a into active: held[a] = its rule walk waits for a rerun
+  std::vector<uint8_t> held;
+  std::vector<uint32_t> slot_of;   // indices a, sorted by stream (is_held)
+  TrialSet SA, SB;                 // A: every trial neither a duplicate nor waiting for a saver; B: the waiting ones
+  std::vector<uint32_t> ia[3], ib[3];   // their indices in tr[k]
+  bool waiting_trials = false;
+  struct PendDiff { bool live = false; DiffJob d{}; };
+  std::vector<PendDiff> pend;      // a stream's live diff job: its latest improvement within recomp_tresh
+  std::vector<uint32_t> jpos;      // where each stream's rule walk resumes
+  uint64_t ntr = 0, nsc = 0, nhz = 0, nspec = 0;
+
+  Round(atz_ctx* x_, Pipe* c_, const uint8_t* f, std::vector<StreamState>& ss_, const SweepOpts& so_,
+        std::vector<uint32_t>& a_, std::vector<uint32_t>& w_)
+      : x(x_), c(c_), d_file(f), ss(ss_), so(so_), active(a_), waiting(w_) {}
+
+  bool is_held(uint32_t s) const {
+    const size_t i = std::lower_bound(slot_of.begin(), slot_of.end(), s,
+                                      [&](uint32_t e, uint32_t v) { return active[e] < v; }) - slot_of.begin();
+    return held[slot_of[i]] != 0;
+  }
+
+  // The trials of the next K list entries of every stream, within the round's scratch budget.
+  void build_lists() {
+    K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, round_target(x) / active.size()));
+    mbeg.assign(active.size() + 1, 0);
     mine.reserve(active.size() * K);
-    uint64_t out_tot = 0, sym_tot = 0, round_bytes = 0;
+    uint64_t round_bytes = 0;
     const uint64_t round_budget = ROUND_BUDGET_BYTES / x->pipes_running;
     for (size_t a = 0; a < active.size(); a++) {
       mbeg[a] = (uint32_t)mine.size();
@@ -1998,14 +2012,14 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
         break;
       }
       for (uint32_t j = 0; j < K && st.idx + j < st.list->size(); j++) {
-        uint32_t p = (*st.list)[st.idx + j];
-        int cl = (int)(p >> 16), w = (int)((p >> 8) & 0xff), m = (int)(p & 0xff);
+        const uint32_t p = (*st.list)[st.idx + j];
+        const int cl = (int)(p >> 16), w = (int)((p >> 8) & 0xff), m = (int)(p & 0xff);
         Trial t{};
         t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
         t.best_ident = st.ident;
         t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
-        int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
+        const int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
         const uint64_t sw = sym_words(kind, (uint32_t)m, x->recs[s].infl_len);
         t.sym_off = sym_tot; sym_tot += sw;
         round_bytes += 8 * (x->recs[s].infl_len + 320) + t.out_cap + 4 * sw;
@@ -2019,9 +2033,17 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     }
     mbeg.resize(active.size() + 1);
     mbeg[active.size()] = (uint32_t)mine.size();
-    auto ta = std::chrono::steady_clock::now();
-    // replays first (they need the pairs' bucket depths only), then the tables the other trials read
-    std::vector<std::array<uint32_t, 4>> savers;   // (kind, index in tr[kind], rp_pool entry, level - 1)
+    held.assign(active.size(), 0);
+    slot_of.resize(active.size());
+    for (size_t a = 0; a < active.size(); a++) slot_of[a] = (uint32_t)a;
+    std::sort(slot_of.begin(), slot_of.end(), [&](uint32_t p1, uint32_t p2) { return active[p1] < active[p2]; });
+    pend.assign(active.size(), PendDiff{});
+    jpos.assign(mbeg.begin(), mbeg.end() - 1);
+  }
+
+  // Replays first (they need the pairs' bucket depths only), duplicates, the eligibility floor, then the
+  // bucket tables the other trials read (stream-ordered before the match walks: no sync).
+  int plan() {
     if (replay_on() && x->depth_pin.p) {
       if (int r = ensure_depths(x, c, need, need_b)) return r;
       HIPCHK(pipe_sync(c));
@@ -2035,60 +2057,57 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     for (int k = 0; k < 3; k++)
       for (Trial& t : tr[k])
         if (!(t.mode & 4)) t.best_ident = std::max(t.best_ident, elig_floor(x, x->recs[t.stream].comp_len));
-    size_t nbuild = 0;
     for (auto& q : need) nbuild += x->chain_off[q.first][q.second] == ~0ull;
-    if (int r = ensure_chains(x, c, need)) return r;   // (stream-ordered before the match walks: no sync)
-    auto tb = std::chrono::steady_clock::now();
+    if (int r = ensure_chains(x, c, need)) return r;
     for (int k = 1; k < 3; k++)
       for (Trial& t : tr[k]) {
         const uint64_t off = x->chain_off[t.stream][t.memlevel];
         t.chain_off = off == ~0ull ? 0 : off;   // unchecked replays read no table
       }
     for (int k = 1; k < 3; k++)
-      for (const Trial& t : tr[k]) {   // saved sequences stay inside the arena (a bad slot would fault the GPU)
-        if (!(t.mode & 12)) continue;
-        const uint64_t n = x->recs[t.stream].infl_len;
-        const bool tab_ok = !(t.mode & 48) || x->rp_arena.holds(t.rp_tab, 8 * n);
-        if (!x->rp_arena.holds(t.rp_syms, 4 * (n + 64)) || ((t.mode & 8) && t.rp_nsym > n) || !tab_ok) {
-          std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
-          return ATZ_E_INTERNAL;
-        }
-      }
+      for (const Trial& t : tr[k])   // saved sequences stay inside the arena (a bad slot would fault the GPU)
+        if ((t.mode & 12) && !replay_slot_ok(t)) return ATZ_E_INTERNAL;
     if (int r = c->d_out.reserve(out_tot + 4096)) return r;
     if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
-    // streams of the batch by index a into active: held[a] = its rule walk waits for a rerun (rounds)
-    std::vector<uint8_t> held(active.size(), 0);
-    std::vector<uint32_t> slot_of;   // stream -> a (only for the batch's streams)
-    auto a_of = [&](uint32_t s) -> size_t {
-      return std::lower_bound(slot_of.begin(), slot_of.end(), s, [&](uint32_t e, uint32_t v) { return active[e] < v; }) - slot_of.begin();
-    };
-    for (size_t a = 0; a < active.size(); a++) slot_of.push_back((uint32_t)a);
-    std::sort(slot_of.begin(), slot_of.end(), [&](uint32_t p1, uint32_t p2) { return active[p1] < active[p2]; });
-    auto is_held = [&](uint32_t s) -> bool { return held[slot_of[a_of(s)]] != 0; };
-    // a complete saved sequence serves the stream's later trials at that level (held streams' savers wait
-    // for their reruns: a saver stopped by TR_NEED_R runs again)
-    auto finish_savers = [&](bool held_ones) {
-      for (const auto& sv : savers) {
-        const uint32_t s = tr[sv[0]][sv[1]].stream;
-        if (is_held(s) != held_ones) continue;
-        const TrialRes& r = trres[sv[0]][sv[1]];
-        RpEntry& e = x->rp_pool[sv[2]][sv[3]];
-        if (r.state != TR_NEED_R && (r.saved_flags & 1u)) {
-          e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags; e.reads_max = r.reads_max;
-        } else {
-          e.state = 0;   // the slot stays for the next saving trial
-        }
+    return 0;
+  }
+  bool replay_slot_ok(const Trial& t) const {
+    const uint64_t n = x->recs[t.stream].infl_len;
+    const bool syms_ok = !(t.mode & 12) || x->rp_arena.holds(t.rp_syms, 4 * (n + 64));
+    const bool tab_ok = !(t.mode & 48) || x->rp_arena.holds(t.rp_tab, 8 * n);
+    if (syms_ok && tab_ok && !((t.mode & 8) && t.rp_nsym > n)) return true;
+    std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
+    return false;
+  }
+
+  // A complete saved sequence serves the stream's later trials at that level (held streams' savers wait
+  // for their reruns: a saver stopped by TR_NEED_R runs again).
+  void finish_savers(bool held_ones) {
+    for (const auto& sv : savers) {
+      if (is_held(tr[sv[0]][sv[1]].stream) != held_ones) continue;
+      const TrialRes& r = trres[sv[0]][sv[1]];
+      RpEntry& e = x->rp_pool[sv[2]][sv[3]];
+      if (r.state != TR_NEED_R && (r.saved_flags & 1u)) {
+        e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags; e.reads_max = r.reads_max;
+      } else {
+        e.state = 0;   // the slot stays for the next saving trial
       }
-    };
-    // duplicates are not launched; trials waiting for a saver of this round go in a second launch set
-    // (speculative rounds, K > 1: small files, the sweep's tail) once the saver's sequence is in
+    }
+  }
+  void collect(const TrialSet& S, const std::vector<uint32_t>* idx) {
+    std::vector<TrialRes> rr[3];
+    trials_results(S, rr);
+    for (int k = 0; k < 3; k++)
+      for (size_t j = 0; j < idx[k].size(); j++) trres[k][idx[k][j]] = rr[k][j];
+  }
+
+  // First passes.  Duplicates are not launched; trials waiting for a saver of this round go in a second
+  // launch set (speculative rounds, K > 1: small files, the sweep's tail) once the saver's sequence is in.
+  int launch() {
     TrialRes dup{};
     dup.state = TR_CANT_BEAT;
-    bool waiting_trials = false;
     for (int k = 1; k < 3; k++)
       for (const Trial& t : tr[k]) waiting_trials |= (t.mode & 64) != 0;
-    TrialSet SA, SB;                      // A: every trial neither a duplicate nor waiting; B: the waiting ones
-    std::vector<uint32_t> ia[3], ib[3];   // their indices in tr[k]
     {
       std::vector<Trial> ta[3];
       for (int k = 0; k < 3; k++) {
@@ -2101,179 +2120,171 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
       }
       trials_order(x, ta, SA);
     }
-    auto collect = [&](const TrialSet& S, const std::vector<uint32_t>* idx) {
-      std::vector<TrialRes> rr[3];
-      trials_results(S, rr);
-      for (int k = 0; k < 3; k++)
-        for (size_t j = 0; j < idx[k].size(); j++) trres[k][idx[k][j]] = rr[k][j];
-    };
     if (int r = trials_first(x, c, d_file, SA, so)) return r;
-    if (waiting_trials) {   // the savers complete (reruns included) before the trials that wait for them
-      if (int r = trials_rerun(x, c, d_file, SA, so, nullptr)) return r;
+    if (!waiting_trials) {
       collect(SA, ia);
-      finish_savers(false);
-      std::vector<Trial> t3[3];
-      for (int k = 1; k < 3; k++)
-        for (uint32_t q = 0; q < tr[k].size(); q++) {
-          Trial& t = tr[k][q];
-          if (!(t.mode & 64)) continue;
-          t.mode &= ~64u;
-          const RpEntry& e = x->rp_pool[ss[t.stream].rp][t.clevel - 1];
-          if (e.state == 2 && e.window == t.window) replay_from(t, e, replay_free(x, k, t));
-          if (t.mode & 128) continue;
-          const uint64_t n = x->recs[t.stream].infl_len;
-          if ((t.mode & 8) && (!x->rp_arena.holds(t.rp_syms, 4 * (n + 64)) || t.rp_nsym > n ||
-                               ((t.mode & 16) && !x->rp_arena.holds(t.rp_tab, 8 * n)))) {
-            std::fprintf(stderr, "atz: symbol replay slot out of its arena (stream %u)\n", t.stream);
-            return ATZ_E_INTERNAL;
-          }
-          t3[k].push_back(t);
-          ib[k].push_back(q);
-        }
-      trials_order(x, t3, SB);
-      if (int r = trials_first(x, c, d_file, SB, so)) return r;
-      collect(SB, ib);
-    } else {
-      collect(SA, ia);
+      return 0;
     }
-    auto tc = std::chrono::steady_clock::now();
-    // The reference's sequential rule per stream, in list order (main.cpp:685-700), walked up to the
-    // stream's stop; with defer, a walk that reaches a trial still to be rerun (TR_NEED_R) waits there
-    // (held) and resumes after the reruns.  A stream's live diff job (its latest improvement within the
-    // recomp threshold) is extracted by flush_diffs.
-    struct PendDiff { bool live = false; DiffJob d{}; };
-    std::vector<PendDiff> pend(active.size());
-    std::vector<uint32_t> jpos(mbeg.begin(), mbeg.end() - 1);
-    auto walk = [&](size_t a, bool defer) -> int {
-      const uint32_t s = active[a];
-      StreamState& st = ss[s];
-      const uint64_t C = x->recs[s].comp_len;
-      const uint32_t phase0 = st.phase;
-      held[a] = 0;
-      for (uint32_t j = jpos[a]; j < mbeg[a + 1]; j++) {
-        if (st.phase != phase0) { nspec += mbeg[a + 1] - j; break; }   // stopped earlier this round
-        const Trial& t = tr[mine[j].first][mine[j].second];
-        const TrialRes& r = trres[mine[j].first][mine[j].second];
-        if (r.state == TR_NEED_R) {
-          if (!defer) return ATZ_E_INTERNAL;   // every rerun a walk waits for has run
-          jpos[a] = j;
-          held[a] = 1;
-          return 0;
-        }
-        st.trials++;
-        ntr++;
-        if (r.state == TR_SHORTCUT) nsc++;
-        if (r.flags & 1) nhz++;
-        if (r.state == TR_OVERFLOW) return ATZ_E_REF_ABORT;   // deflate() without Z_STREAM_END, main.cpp:663-665
-        bool fullmatch = false;
-        if (r.state == TR_FULL && r.ident > st.ident) {
-          st.ident = r.ident;
-          st.c = t.clevel; st.w = t.window; st.m = t.memlevel;
-          st.first_diff = -1;
-          st.rawdiff.clear(); st.diffval.clear();
-          pend[a].live = false;   // an earlier improvement's diffs are superseded
-          if (r.ident == C) fullmatch = true;
-          else {
-            if (r.ident + x->o.mismatch_tol >= C) fullmatch = true;
-            if (C - r.ident <= x->o.recomp_tresh) {     // diffs are only ever written for recomp streams
-              DiffJob& d = pend[a].d;
-              d.out_off = t.out_off; d.out_len = r.out_len; d.orig_off = x->recs[s].offset;
-              d.comp_len = C; d.dst = 0; d.cap = C - r.ident;
-              pend[a].live = true;
-            }
+    // the savers complete (reruns included) before the trials that wait for them
+    if (int r = trials_rerun(x, c, d_file, SA, so, nullptr)) return r;
+    collect(SA, ia);
+    finish_savers(false);
+    std::vector<Trial> t3[3];
+    for (int k = 1; k < 3; k++)
+      for (uint32_t q = 0; q < tr[k].size(); q++) {
+        Trial& t = tr[k][q];
+        if (!(t.mode & 64)) continue;
+        t.mode &= ~64u;
+        const RpEntry& e = x->rp_pool[ss[t.stream].rp][t.clevel - 1];
+        if (e.state == 2 && e.window == t.window) replay_from(t, e, replay_free(x, k, t));
+        if (t.mode & 128) continue;
+        if ((t.mode & 8) && !replay_slot_ok(t)) return ATZ_E_INTERNAL;
+        t3[k].push_back(t);
+        ib[k].push_back(q);
+      }
+    trials_order(x, t3, SB);
+    if (int r = trials_first(x, c, d_file, SB, so)) return r;
+    collect(SB, ib);
+    return 0;
+  }
+
+  // The reference's sequential rule for stream a, in list order (main.cpp:685-700), walked up to the
+  // stream's stop; with defer, a walk that reaches a trial still to be rerun (TR_NEED_R) waits there
+  // (held) and resumes after the reruns.
+  int walk(size_t a, bool defer) {
+    const uint32_t s = active[a];
+    StreamState& st = ss[s];
+    const uint64_t C = x->recs[s].comp_len;
+    const uint32_t phase0 = st.phase;
+    held[a] = 0;
+    for (uint32_t j = jpos[a]; j < mbeg[a + 1]; j++) {
+      if (st.phase != phase0) { nspec += mbeg[a + 1] - j; break; }   // stopped earlier this round
+      const Trial& t = tr[mine[j].first][mine[j].second];
+      const TrialRes& r = trres[mine[j].first][mine[j].second];
+      if (r.state == TR_NEED_R) {
+        if (!defer) return ATZ_E_INTERNAL;   // every rerun a walk waits for has run
+        jpos[a] = j;
+        held[a] = 1;
+        return 0;
+      }
+      st.trials++;
+      ntr++;
+      if (r.state == TR_SHORTCUT) nsc++;
+      if (r.flags & 1) nhz++;
+      if (r.state == TR_OVERFLOW) return ATZ_E_REF_ABORT;   // deflate() without Z_STREAM_END, main.cpp:663-665
+      bool fullmatch = false;
+      if (r.state == TR_FULL && r.ident > st.ident) {
+        st.ident = r.ident;
+        st.c = t.clevel; st.w = t.window; st.m = t.memlevel;
+        st.first_diff = -1;
+        st.rawdiff.clear(); st.diffval.clear();
+        pend[a].live = false;   // an earlier improvement's diffs are superseded
+        if (r.ident == C) fullmatch = true;
+        else {
+          if (r.ident + x->o.mismatch_tol >= C) fullmatch = true;
+          if (C - r.ident <= x->o.recomp_tresh) {     // diffs are only ever written for recomp streams
+            DiffJob& d = pend[a].d;
+            d.out_off = t.out_off; d.out_len = r.out_len; d.orig_off = x->recs[s].offset;
+            d.comp_len = C; d.dst = 0; d.cap = C - r.ident;
+            pend[a].live = true;
           }
         }
-        st.idx++;
-        if (fullmatch) st.idx = (uint32_t)st.list->size();   // testParamRange/tryParams return
-        if (st.idx >= st.list->size()) {
-          if (st.phase == 0 && (C - st.ident) >= x->o.mismatch_tol && x->o.brute_window) {
-            st.list = &trial_list(x->recs[s].type, true);
-            st.idx = 0;
-            st.phase = 1;
-          } else {
-            st.phase = 2;
-          }
+      }
+      st.idx++;
+      if (fullmatch) st.idx = (uint32_t)st.list->size();   // testParamRange/tryParams return
+      if (st.idx >= st.list->size()) {
+        if (st.phase == 0 && (C - st.ident) >= x->o.mismatch_tol && x->o.brute_window) {
+          st.list = &trial_list(x->recs[s].type, true);
+          st.idx = 0;
+          st.phase = 1;
+        } else {
+          st.phase = 2;
         }
       }
-      jpos[a] = mbeg[a + 1];
-      return 0;
-    };
-    // mismatch lists (main.cpp:699-714) of the live diff jobs of streams `which`, from the trials' outputs
-    auto flush_diffs = [&](const std::vector<size_t>& which) -> int {
-      std::vector<DiffJob> dj;
-      std::vector<size_t> dja;
-      uint64_t dpos = 0;
-      for (size_t a : which) {
-        if (!pend[a].live) continue;
-        pend[a].live = false;
-        DiffJob d = pend[a].d;
-        d.dst = dpos;
-        dpos += d.cap;
-        dj.push_back(d);
-        dja.push_back(a);
-      }
-      if (dj.empty()) return 0;
-      if (int r = upload(c, c->d_diffjobs, dj.data(), dj.size() * sizeof(DiffJob))) return r;
-      if (int r = c->d_diffpos.reserve(dpos * 4 + 64)) return r;
-      if (int r = c->d_diffval.reserve(dpos + 64)) return r;
-      if (int r = c->d_diffcnt.reserve(dj.size() * 8 + 64)) return r;
-      kbeg(c, 3);
-      hipLaunchKernelGGL(k_diffs, dim3((uint32_t)dj.size()), dim3(64), 0, c->st, c->d_out.as<uint8_t>(), d_file,
-                         c->d_diffjobs.as<DiffJob>(), c->d_diffpos.as<uint32_t>(), c->d_diffval.as<uint8_t>(),
-                         c->d_diffcnt.as<uint64_t>(), (uint32_t)dj.size());
-      kend(c);
-      KCHECK("k_diffs");
-      std::vector<uint32_t> pos(dpos);
-      std::vector<uint8_t> val(dpos);
-      std::vector<uint64_t> cnt(dj.size());
-      HIPCHK(pipe_copy(c, pos.data(), c->d_diffpos.p, dpos * 4, hipMemcpyDeviceToHost));
-      HIPCHK(pipe_copy(c, val.data(), c->d_diffval.p, dpos, hipMemcpyDeviceToHost));
-      HIPCHK(pipe_copy(c, cnt.data(), c->d_diffcnt.p, dj.size() * 8, hipMemcpyDeviceToHost));
-      HIPCHK(pipe_sync(c));
-      kcollect(c);
-      for (size_t q = 0; q < dj.size(); q++) {
-        if (cnt[q] != dj[q].cap) return ATZ_E_INTERNAL;
-        StreamState& st = ss[active[dja[q]]];
-        st.rawdiff.assign(pos.begin() + dj[q].dst, pos.begin() + dj[q].dst + dj[q].cap);
-        st.diffval.assign(val.begin() + dj[q].dst, val.begin() + dj[q].dst + dj[q].cap);
-        st.first_diff = st.rawdiff.empty() ? -1 : (int64_t)st.rawdiff[0];
-      }
-      return 0;
-    };
-    // the bookkeeping that reads or writes a stream's state, for streams that are done with this round
-    auto settle = [&](bool held_ones) {
-      finish_savers(held_ones);
-      if (dedup_on() && x->depth_pin.p)
-        level_record(x, ss, tr[2], trres[2], [&](uint32_t s) { return is_held(s) == held_ones; });
-    };
+    }
+    jpos[a] = mbeg[a + 1];
+    return 0;
+  }
+
+  // The bookkeeping that reads or writes a stream's state, for streams that are done with this round.
+  void settle(bool held_ones) {
+    finish_savers(held_ones);
+    if (dedup_on() && x->depth_pin.p)
+      level_record(x, ss, tr[2], trres[2], [&](uint32_t s) { return is_held(s) == held_ones; });
+  }
+
+  // Every stream's walk; the reruns of the held streams (every TR_NEED_R trial of theirs: which ones the
+  // walk needs depends on the trials before), then their walks' rest.
+  int apply() {
     for (size_t a = 0; a < active.size(); a++)
       if (int r = walk(a, true)) return r;
     settle(false);
     bool any_held = false;
     for (uint8_t h : held) any_held |= h != 0;
-    if (any_held) {   // rounds: the reruns of the held streams (every TR_NEED_R trial of theirs: which ones
-                      // the walk needs depends on the trials before)
-      auto want = [&](const Trial& t) { return is_held(t.stream); };
-      if (int r = trials_rerun(x, c, d_file, SA, so, want)) return r;
-      collect(SA, ia);
-      if (waiting_trials) {
-        if (int r = trials_rerun(x, c, d_file, SB, so, want)) return r;
-        collect(SB, ib);
+    if (!any_held) return 0;
+    auto want = [&](const Trial& t) { return is_held(t.stream); };
+    if (int r = trials_rerun(x, c, d_file, SA, so, want)) return r;
+    collect(SA, ia);
+    if (waiting_trials) {
+      if (int r = trials_rerun(x, c, d_file, SB, so, want)) return r;
+      collect(SB, ib);
+    }
+    for (size_t a = 0; a < active.size(); a++)
+      if (held[a]) {
+        held[a] = 0;
+        if (int r = walk(a, false)) return r;
+        held[a] = 1;   // (settle's selector)
       }
-      for (size_t a = 0; a < active.size(); a++)
-        if (held[a]) {
-          held[a] = 0;
-          if (int r = walk(a, false)) return r;
-          held[a] = 1;   // (settle's selector)
-        }
-      settle(true);
+    settle(true);
+    return 0;
+  }
+
+  // Mismatch lists (main.cpp:699-714) of the live diff jobs, from the trials' outputs.
+  int flush_diffs() {
+    std::vector<DiffJob> dj;
+    std::vector<size_t> dja;
+    uint64_t dpos = 0;
+    for (size_t a = 0; a < active.size(); a++) {
+      if (!pend[a].live) continue;
+      pend[a].live = false;
+      DiffJob d = pend[a].d;
+      d.dst = dpos;
+      dpos += d.cap;
+      dj.push_back(d);
+      dja.push_back(a);
     }
-    {
-      std::vector<size_t> all(active.size());
-      for (size_t a = 0; a < active.size(); a++) all[a] = a;
-      if (int r = flush_diffs(all)) return r;
+    if (dj.empty()) return 0;
+    if (int r = upload(c, c->d_diffjobs, dj.data(), dj.size() * sizeof(DiffJob))) return r;
+    if (int r = c->d_diffpos.reserve(dpos * 4 + 64)) return r;
+    if (int r = c->d_diffval.reserve(dpos + 64)) return r;
+    if (int r = c->d_diffcnt.reserve(dj.size() * 8 + 64)) return r;
+    kbeg(c, 3);
+    hipLaunchKernelGGL(k_diffs, dim3((uint32_t)dj.size()), dim3(64), 0, c->st, c->d_out.as<uint8_t>(), d_file,
+                       c->d_diffjobs.as<DiffJob>(), c->d_diffpos.as<uint32_t>(), c->d_diffval.as<uint8_t>(),
+                       c->d_diffcnt.as<uint64_t>(), (uint32_t)dj.size());
+    kend(c);
+    KCHECK("k_diffs");
+    std::vector<uint32_t> pos(dpos);
+    std::vector<uint8_t> val(dpos);
+    std::vector<uint64_t> cnt(dj.size());
+    HIPCHK(pipe_copy(c, pos.data(), c->d_diffpos.p, dpos * 4, hipMemcpyDeviceToHost));
+    HIPCHK(pipe_copy(c, val.data(), c->d_diffval.p, dpos, hipMemcpyDeviceToHost));
+    HIPCHK(pipe_copy(c, cnt.data(), c->d_diffcnt.p, dj.size() * 8, hipMemcpyDeviceToHost));
+    HIPCHK(pipe_sync(c));
+    kcollect(c);
+    for (size_t q = 0; q < dj.size(); q++) {
+      if (cnt[q] != dj[q].cap) return ATZ_E_INTERNAL;
+      StreamState& st = ss[active[dja[q]]];
+      st.rawdiff.assign(pos.begin() + dj[q].dst, pos.begin() + dj[q].dst + dj[q].cap);
+      st.diffval.assign(val.begin() + dj[q].dst, val.begin() + dj[q].dst + dj[q].cap);
+      st.first_diff = st.rawdiff.empty() ? -1 : (int64_t)st.rawdiff[0];
     }
-    auto td = std::chrono::steady_clock::now();
+    return 0;
+  }
+
+  // The pipe's counters (per-kind x level: count, cycles total/tree/emit/heap/fallback, parsed bytes,
+  // symbols, scan/send cycles, parse window phases) and diagnostics.
+  void account(uint64_t round) {
     for (int k = 1; k < 3; k++)
       for (size_t q = 0; q < tr[k].size(); q++) {
         c->stats.n_trials_replayed += (trres[k][q].saved_flags >> 2) & 1u;
@@ -2284,15 +2295,6 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
           c->diag_need[tr[k][q].stream] |= (uint16_t)(1u << tr[k][q].memlevel);
         }
       }
-    c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
-    c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
-    if (timing_level() >= 2)
-      std::fprintf(stderr, "atz: pipe %d round %llu at %.1f ms: active %zu K %u trials %zu/%zu/%zu list %.1f chains %.1f (%zu builds) trials %.1f ms, reruns+apply %.1f ms\n",
-                   c->id, (unsigned long long)rounds, std::chrono::duration<double, std::milli>(ta - t0).count(), active.size(), K,
-                   tr[0].size(), tr[1].size(), tr[2].size(), std::chrono::duration<double, std::milli>(ta - tl0).count(),
-                   std::chrono::duration<double, std::milli>(tb - ta).count(), nbuild,
-                   std::chrono::duration<double, std::milli>(tc - tb).count(),
-                   std::chrono::duration<double, std::milli>(td - tc).count());
     for (int k = 0; k < 3; k++)
       for (size_t q = 0; q < tr[k].size(); q++) {
         const TrialRes& r = trres[k][q];
@@ -2314,26 +2316,64 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
                                         : x->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
         if (timing_level() >= 3 && !(tr[k][q].mode & 128)) c->diag_rt.push_back({r.rt0, r.rt1});
       }
-    if (timing_on()) {   // slowest trials of the round (diagnostics)
-      std::vector<std::pair<uint64_t, std::pair<int, size_t>>> top;
-      for (int k = 0; k < 3; k++)
-        for (size_t q = 0; q < tr[k].size(); q++) top.push_back({trres[k][q].cyc_total, {k, q}});
-      std::sort(top.begin(), top.end(), [](auto& a, auto& b) { return a.first > b.first; });
-      for (size_t i = 0; i < top.size() && i < 3; i++) {
-        const Trial& t = tr[top[i].second.first][top[i].second.second];
-        const TrialRes& r = trres[top[i].second.first][top[i].second.second];
-        std::fprintf(stderr, "atz: round %llu slow trial: stream %u I=%llu c%u w%u m%u state %u cyc %.1fM syms %llu blocks %llu "
-                     "fallbacks %llu tree %.1fM emit %.1fM (heap %.1fM scan %.1fM send %.1fM fb %.1fM)\n", (unsigned long long)rounds, t.stream,
-                     (unsigned long long)x->recs[t.stream].infl_len, t.clevel, t.window, t.memlevel, r.state,
-                     r.cyc_total / 1e6, (unsigned long long)r.symbols, (unsigned long long)r.blocks,
-                     (unsigned long long)(r.fallbacks & 0xffffffffull), r.cyc_tree / 1e6, r.cyc_emit / 1e6, r.cyc_heap / 1e6,
-                     r.cyc_scan / 1e6, r.cyc_send / 1e6, r.cyc_fallback / 1e6);
-      }
+    if (!timing_on()) return;
+    // slowest trials of the round (diagnostics)
+    std::vector<std::pair<uint64_t, std::pair<int, size_t>>> top;
+    for (int k = 0; k < 3; k++)
+      for (size_t q = 0; q < tr[k].size(); q++) top.push_back({trres[k][q].cyc_total, {k, q}});
+    std::sort(top.begin(), top.end(), [](auto& p1, auto& p2) { return p1.first > p2.first; });
+    for (size_t i = 0; i < top.size() && i < 3; i++) {
+      const Trial& t = tr[top[i].second.first][top[i].second.second];
+      const TrialRes& r = trres[top[i].second.first][top[i].second.second];
+      std::fprintf(stderr, "atz: round %llu slow trial: stream %u I=%llu c%u w%u m%u state %u cyc %.1fM syms %llu blocks %llu "
+                   "fallbacks %llu tree %.1fM emit %.1fM (heap %.1fM scan %.1fM send %.1fM fb %.1fM)\n", (unsigned long long)round, t.stream,
+                   (unsigned long long)x->recs[t.stream].infl_len, t.clevel, t.window, t.memlevel, r.state,
+                   r.cyc_total / 1e6, (unsigned long long)r.symbols, (unsigned long long)r.blocks,
+                   (unsigned long long)(r.fallbacks & 0xffffffffull), r.cyc_tree / 1e6, r.cyc_emit / 1e6, r.cyc_heap / 1e6,
+                   r.cyc_scan / 1e6, r.cyc_send / 1e6, r.cyc_fallback / 1e6);
     }
-    c->t_apply += ms_since(tc);
   }
-  c->stats.n_trials += ntr; c->stats.n_trials_shortcut += nsc; c->stats.n_rounds = rounds; c->stats.n_hazard += nhz;
-  c->stats.n_trials_speculative += nspec;
+};
+
+// The sweep work of pipe c: rounds on the batches sched_take hands it.
+static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint32_t> active;
+  const SweepOpts so{x->o.recomp_tresh, x->o.sizediff_tresh, x->o.shortcut_len, x->o.mismatch_tol};
+  uint64_t rounds = 0;
+  while (sched_take(x, c->id, active)) {
+    rounds++;
+    std::vector<uint32_t> waiting;
+    struct Give {   // the batch goes back on every exit from the round (an error aborts the sweep anyway)
+      atz_ctx* x; Pipe* c; const std::vector<StreamState>& ss; const std::vector<uint32_t>& a, &w;
+      ~Give() { forget_tmp_chains(x, c); sched_give(x, c->id, ss, a, w); }
+    } give{x, c, ss, active, waiting};
+    Round R(x, c, d_file, ss, so, active, waiting);
+    const auto tl0 = std::chrono::steady_clock::now();
+    R.build_lists();
+    const auto ta = std::chrono::steady_clock::now();
+    if (int r = R.plan()) return r;
+    const auto tb = std::chrono::steady_clock::now();
+    if (int r = R.launch()) return r;
+    const auto tc = std::chrono::steady_clock::now();
+    if (int r = R.apply()) return r;
+    if (int r = R.flush_diffs()) return r;
+    const auto td = std::chrono::steady_clock::now();
+    c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
+    c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
+    if (timing_level() >= 2)
+      std::fprintf(stderr, "atz: pipe %d round %llu at %.1f ms: active %zu K %u trials %zu/%zu/%zu list %.1f chains %.1f (%zu builds) trials %.1f ms, reruns+apply %.1f ms\n",
+                   c->id, (unsigned long long)rounds, std::chrono::duration<double, std::milli>(ta - t0).count(), active.size(), R.K,
+                   R.tr[0].size(), R.tr[1].size(), R.tr[2].size(), std::chrono::duration<double, std::milli>(ta - tl0).count(),
+                   std::chrono::duration<double, std::milli>(tb - ta).count(), R.nbuild,
+                   std::chrono::duration<double, std::milli>(tc - tb).count(),
+                   std::chrono::duration<double, std::milli>(td - tc).count());
+    R.account(rounds);
+    c->t_apply += ms_since(tc);
+    c->stats.n_trials += R.ntr; c->stats.n_trials_shortcut += R.nsc; c->stats.n_hazard += R.nhz;
+    c->stats.n_trials_speculative += R.nspec;
+  }
+  c->stats.n_rounds = rounds;
   c->stats.sweep_ms = ms_since(t0);
   return 0;
 }

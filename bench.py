@@ -346,10 +346,15 @@ def main():
             "alg_bytes_per_launch": int(alg / launches)}
 
     # parity of the timed run's own output: the ATZ1 SHA-256 of the last step against the real reference's
-    # (tests/golden/full_configs.json: oracle/_ref/uncomp on the same generated file), full-size C4/C5 only
+    # on the same generated file (oracle/_ref/uncomp): tests/golden/full_configs.json for the full-size
+    # configs, tests/golden/share_configs.json for the per-rank share files (--streams 12500 / 25000 /
+    # 50000) and the C4 + C3 cluster file
     atz_check = None
-    if rank == 0 and args.streams == 100000 and last_out[0] is not None and (args.mode == "file" or not extra):
-        ref = json.load(open(os.path.join(ROOT, "tests", "golden", "full_configs.json"))).get(args.workload)
+    if rank == 0 and last_out[0] is not None and (args.mode == "file" or not extra):
+        gold = os.path.join(ROOT, "tests", "golden")
+        ref = json.load(open(os.path.join(gold, "share_configs.json"))).get("%s:%d" % (args.workload, args.streams))
+        if ref is None and args.streams == 100000:
+            ref = json.load(open(os.path.join(gold, "full_configs.json"))).get(args.workload)
         if ref and len(data) == ref["input_bytes"]:
             h = torch.empty(n, dtype=torch.uint8)
             if isinstance(last_out[0], int):
@@ -359,7 +364,8 @@ def main():
                 h.copy_(last_out[0][:n].cpu())
             sha = hashlib.sha256(h.numpy().tobytes()).hexdigest()
             atz_check = {"atz_sha256": sha[:16], "identical_to_reference": sha == ref["atz_sha256"],
-                         "reference": "oracle/_ref/uncomp on the same file (tests/golden/full_configs.json)"}
+                         "reference": "oracle/_ref/uncomp on the same file (tests/golden/%s)"
+                                      % ("share_configs.json" if "workload" in ref else "full_configs.json")}
             if sha != ref["atz_sha256"]:
                 log("PARITY FAILURE: the timed run's ATZ1 differs from the reference's")
 
