@@ -352,7 +352,8 @@ def main():
     atz_check = None
     if rank == 0 and last_out[0] is not None and (args.mode == "file" or not extra):
         gold = os.path.join(ROOT, "tests", "golden")
-        ref = json.load(open(os.path.join(gold, "share_configs.json"))).get("%s:%d" % (args.workload, args.streams))
+        sp = os.path.join(gold, "share_configs.json")
+        ref = (json.load(open(sp)) if os.path.exists(sp) else {}).get("%s:%d" % (args.workload, args.streams))
         if ref is None and args.streams == 100000:
             ref = json.load(open(os.path.join(gold, "full_configs.json"))).get(args.workload)
         if ref and len(data) == ref["input_bytes"]:
