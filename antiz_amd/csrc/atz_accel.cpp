@@ -173,6 +173,43 @@ __global__ __launch_bounds__(64) void k_diffs(const uint8_t* __restrict__ out, c
   if (lane == 0) count[j] = k;
 }
 
+// The mismatch lists of pre-run trials (PreLane), decided on the device from each trial's result: a trial
+// that can become its stream's recompression (TR_FULL, ident < C_s, C_s - ident <= tresh) gets its list at
+// dst (C_s - ident entries, at most cap); the others count 0.
+__global__ __launch_bounds__(64) void k_diffs_pre(const uint8_t* __restrict__ out, const uint8_t* __restrict__ file,
+                                                 const DiffJob* __restrict__ jobs, const TrialRes* __restrict__ res,
+                                                 uint64_t tresh, uint32_t* __restrict__ pos, uint8_t* __restrict__ val,
+                                                 uint64_t* __restrict__ count, uint32_t n) {
+  const uint32_t j = blockIdx.x;
+  if (j >= n) return;
+  const int lane = threadIdx.x;
+  const DiffJob d = jobs[j];
+  const TrialRes r = res[j];
+  const bool want = r.state == TR_FULL && r.ident < d.comp_len && d.comp_len - r.ident <= tresh;
+  if (!want) { if (lane == 0) count[j] = 0; return; }
+  const uint8_t* o = out + d.out_off;
+  const uint8_t* f = file + d.orig_off;
+  const uint64_t sm = r.out_len < d.comp_len ? r.out_len : d.comp_len;
+  uint64_t k = 0;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (uint64_t b = 0; b < d.comp_len; b += 64) {
+    const uint64_t i = b + lane;
+    bool m = false;
+    uint8_t v = 0;
+    if (i < d.comp_len) {
+      v = f[i];
+      m = i < sm ? o[i] != v : true;
+    }
+    const uint64_t bal = __ballot(m);
+    if (m) {
+      const uint64_t at = k + __popcll(bal & lt);
+      if (at < d.cap) { pos[d.dst + at] = (uint32_t)i; val[d.dst + at] = v; }
+    }
+    k += __popcll(bal);
+  }
+  if (lane == 0) count[j] = k;
+}
+
 #define HIPCHK(x)                                                     \
   do {                                                                \
     hipError_t e_ = (x);                                              \
@@ -181,6 +218,20 @@ __global__ __launch_bounds__(64) void k_diffs(const uint8_t* __restrict__ out, c
       return ATZ_E_HIP;                                               \
     }                                                                 \
   } while (0)
+
+// Device bytes the library holds in this process (every DBuf: the contexts' buffers, their pipes' scratch,
+// the arenas' chunks), and the peak since the last dev_mark_call(): atz_stats_t dev_bytes_*.
+struct DevAcct {
+  std::atomic<uint64_t> cur{0}, peak{0};
+  void add(uint64_t n) {
+    const uint64_t v = cur.fetch_add(n) + n;
+    uint64_t p = peak.load();
+    while (v > p && !peak.compare_exchange_weak(p, v)) {}
+  }
+  void sub(uint64_t n) { cur.fetch_sub(n); }
+};
+DevAcct g_dev;
+void dev_mark_call() { g_dev.peak.store(g_dev.cur.load()); }
 
 struct DBuf {              // device buffer, freed with its owner (atz_close deletes the context)
   void* p = nullptr;
@@ -191,15 +242,18 @@ struct DBuf {              // device buffer, freed with its owner (atz_close del
   ~DBuf() { release(); }
   int reserve(size_t need) {
     if (need <= n) return 0;
-    if (p) hipFree(p);
-    p = nullptr;
-    n = 0;
+    release();
     size_t cap = need + need / 4 + 65536;
-    if (hipMalloc(&p, cap) != hipSuccess) return ATZ_E_NOMEM;
+    if (hipMalloc(&p, cap) != hipSuccess) { p = nullptr; return ATZ_E_NOMEM; }
     n = cap;
+    g_dev.add(n);
     return 0;
   }
-  void release() { if (p) hipFree(p); p = nullptr; n = 0; }
+  void release() {
+    if (p) { hipFree(p); g_dev.sub(n); }
+    p = nullptr;
+    n = 0;
+  }
   template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
@@ -231,6 +285,17 @@ struct Rec {
   uint8_t mhint = 0;            // k_inflate's first-block memLevel (0: none; whole match tables for it)
 };
 
+// A trial of a stream's list run ahead of its turn by the pipe's pre-run lane (PreLane): its result and,
+// where it can become the stream's recompression (C - ident <= recomp_tresh), its mismatch list.
+struct PreRun {
+  uint32_t idx = 0;               // list index (phase 0)
+  uint8_t c = 0, w = 0, m = 0;
+  bool ready = false;             // the result is in
+  TrialRes r{};
+  std::vector<uint32_t> pos;      // raw mismatch positions (main.cpp:699-714)
+  std::vector<uint8_t> val;
+};
+
 struct StreamState {
   // sweep
   const std::vector<uint32_t>* list = nullptr;   // packed (c<<16)|(w<<8)|m: the header type's shared list
@@ -247,6 +312,12 @@ struct StreamState {
   // levels 7-9 already run budget-free at (window, memLevel): level, longest PL a lazy read improved,
   // longest length read (cross-level duplicates, see level_dups)
   std::vector<std::array<uint16_t, 5>> xl;   // {window, memLevel, level, imp, len}
+  std::vector<PreRun> pre;        // its trials run ahead by the pre-run lane, by list index
+  const PreRun* pre_at(uint32_t i) const {
+    if (phase != 0) return nullptr;
+    for (const PreRun& p : pre) if (p.idx == i) return &p;
+    return nullptr;
+  }
 };
 
 
@@ -449,6 +520,45 @@ struct Pipe {
   }
 };
 
+// Trials of one launch group, kept between their first pass and their reruns: tr[k] (k = 0 stored,
+// 1 fast, 2 slow levels) in launch order (LPT, see trials_order), perm[k][q] = the caller's index of
+// tr[k][q], res[k] in launch order.  Match tables are built for a prefix of each trial's positions; a
+// trial that parses past it stops with TR_NEED_R, and trials_rerun completes its table and runs it
+// again.
+struct TrialSet {
+  std::vector<Trial> tr[3];
+  std::vector<uint32_t> perm[3];
+  std::vector<TrialRes> res[3];
+  size_t base = 0;   // next free slot of d_trials / d_tres
+};
+
+// A pipe's pre-run lane: the likely winners of its hinted streams, run ahead of their turn on the pipe's
+// second HIP stream while the rounds go on (run_prelane).  Its own scratch and kernel timers (a Pipe whose
+// stream is the owner's pst); results and mismatch lists land in pinned memory.
+struct PreLane {
+  std::unique_ptr<Pipe> p;
+  int state = 0;                           // 0 none, 1 launched, 2 results in
+  hipEvent_t ev_chains = nullptr, ev_done = nullptr;
+  TrialSet S;
+  std::vector<std::pair<uint32_t, uint32_t>> who[3];   // per launched trial: (stream, index in its pre[])
+  std::vector<DiffJob> dj;                 // per launched trial, launch order over the kinds
+  size_t bases[3] = {0, 0, 0};             // kind k's results at bases[k] in launch order
+  PinBuf pres, ppos, pval, pcnt;
+  uint64_t n_launched = 0, n_used = 0;
+  // the launches after the bucket tables run on a thread of their own: uploads from pageable memory wait
+  // for the lane's earlier kernels, which the pipe's rounds must not
+  std::thread th;
+  std::atomic<bool> enqueued{false};   // ev_done is recorded
+  int rc = 0;
+  void join() { if (th.joinable()) th.join(); }
+  ~PreLane() {
+    join();
+    if (p) { if (p->st) (void)hipStreamSynchronize(p->st); p->st = nullptr; }   // the owner destroys it
+    if (ev_chains) (void)hipEventDestroy(ev_chains);
+    if (ev_done) (void)hipEventDestroy(ev_done);
+  }
+};
+
 struct atz_ctx {
   KTimer kt;
   atz_opts_t o{};
@@ -498,6 +608,7 @@ struct atz_ctx {
     std::atomic<size_t> published{0};     // streams published to the sweep so far (round_target)
   } sched;
   std::vector<std::unique_ptr<Pipe>> pipes;
+  std::vector<std::unique_ptr<PreLane>> lanes;   // per pipe (destroyed before the pipes: declared after)
   std::vector<std::unique_ptr<DBuf>> slabs;   // inflated records, one allocation per scan piece
   size_t pipes_running = 1;
   std::atomic<bool> sweep_abort{false};   // the pipes stop at their next round (a withdrawn speculative scan)
@@ -1560,17 +1671,6 @@ static uint64_t sym_words(int kind, uint32_t memlevel, uint64_t n) {   // symbol
   return (mw_trial(kind, memlevel) ? n + 64 : 0) + (1ull << (memlevel + 6)) + 64;
 }
 
-// Trials of one launch group, kept between their first pass and their reruns: tr[k] (k = 0 stored,
-// 1 fast, 2 slow levels) in launch order (LPT, see trials_order), perm[k][q] = the caller's index of
-// tr[k][q], res[k] in launch order.  Match tables are built for a prefix of each trial's positions; a
-// trial that parses past it stops with TR_NEED_R, and trials_rerun completes its table and runs it
-// again.
-struct TrialSet {
-  std::vector<Trial> tr[3];
-  std::vector<uint32_t> perm[3];
-  std::vector<TrialRes> res[3];
-  size_t base = 0;   // next free slot of d_trials / d_tres
-};
 // A launch lasts as long as its slowest wave, so the trials go in longest-expected-first order
 // (classic LPT): low memLevels mean many blocks (one tree build each), fast levels mean hole
 // fallbacks, and the work grows with the stream.  Multi-wave trials lead each kind (a launch of their own).
@@ -1627,8 +1727,9 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
   }
   return 0;
 }
-// First pass: match-table prefixes, every trial once.  Chain tables must exist.
-static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, const SweepOpts& so) {
+// The launches of a first pass (match tables, trials); results at d_tres + bases[k] in launch order.
+static int trials_first_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, const SweepOpts& so,
+                               size_t bases[3]) {
   std::vector<Trial>* tr = S.tr;
   std::vector<TrialRes>* res = S.res;
   uint64_t r_tot = 0;
@@ -1660,7 +1761,6 @@ static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, 
   if (int r = c->d_trials.reserve(2 * tot_trials * sizeof(Trial) + 64)) return r;
   if (int r = c->d_tres.reserve(2 * tot_trials * sizeof(TrialRes) + 64)) return r;
   size_t base = 0;
-  size_t bases[3];
   for (int k = 0; k < 3; k++) {
     bases[k] = base;
     res[k].resize(tr[k].size());
@@ -1668,12 +1768,20 @@ static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, 
     if (int r = trials_launch(x, c, d_cmp, so, k, tr[k].data(), tr[k].size(), base)) return r;
     base += tr[k].size();
   }
+  S.base = base;
+  return 0;
+}
+// First pass: match-table prefixes, every trial once, results read back.  Chain tables must exist.
+static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, const SweepOpts& so) {
+  std::vector<Trial>* tr = S.tr;
+  std::vector<TrialRes>* res = S.res;
+  size_t bases[3];
+  if (int r = trials_first_launch(x, c, d_cmp, S, so, bases)) return r;
   for (int k = 0; k < 3; k++)
     if (!tr[k].empty())
       HIPCHK(pipe_copy(c, res[k].data(), c->d_tres.as<TrialRes>() + bases[k], tr[k].size() * sizeof(TrialRes), hipMemcpyDeviceToHost));
   HIPCHK(pipe_sync(c));
   kcollect(c);
-  S.base = base;
   return 0;
 }
 // Reruns: the TR_NEED_R trials for which want(trial) holds get the rest of their match table and run
@@ -1952,6 +2060,197 @@ static void sched_abort(atz_ctx* x) {
 }
 
 static size_t round_target(const atz_ctx* x);
+// Per-trial counters of pipe c (per kind x level: count, cycles total/tree/emit/heap/fallback, parsed
+// bytes, symbols, scan/send cycles, parse window phases) and the algorithmic bytes.
+static void account_trial(atz_ctx* x, Pipe* c, int k, const Trial& t, const TrialRes& r) {
+  const uint64_t C = x->recs[t.stream].comp_len;
+  c->stats.trial_parsed_bytes += r.parsed;
+  c->stats.n_fast_fallbacks += r.fallbacks & 0xffffffffull;
+  c->stats.n_fast_restarts += r.fallbacks >> 32;
+  c->stats.trial_cyc_total += r.cyc_total; c->stats.trial_cyc_tree += r.cyc_tree;
+  c->stats.trial_cyc_emit += r.cyc_emit; c->stats.trial_blocks += r.blocks;
+  c->stats.trial_cyc_heap += r.cyc_heap; c->stats.trial_cyc_fallback += r.cyc_fallback;
+  c->stats.trial_symbols += r.symbols;
+  uint64_t* gk = c->kind[k][t.clevel];
+  gk[0]++; gk[1] += r.cyc_total; gk[2] += r.cyc_tree; gk[3] += r.cyc_emit; gk[4] += r.cyc_heap;
+  gk[5] += r.cyc_fallback; gk[6] += r.parsed; gk[7] += r.symbols; gk[8] += r.cyc_scan; gk[9] += r.cyc_send;
+  for (int i = 0; i < 4; i++) gk[10 + i] += r.cyc_sec[i];
+  // trial input read + compare read (bytes emitted and compared against the original)
+  if (!(t.mode & 128))   // duplicates are not launched; a trial never rerun stopped at its prefix
+    c->stats.k_trial_alg_bytes += r.state == TR_NEED_R ? r.parsed
+                                  : x->recs[t.stream].infl_len + (r.out_len < C ? r.out_len : C);
+  if (timing_level() >= 3 && !(t.mode & 128)) c->diag_rt.push_back({r.rt0, r.rt1});
+}
+// the kernel counters of `from` (a pre-run lane's) added to `to`'s, and cleared
+static void fold_kernel_stats(atz_stats_t& to, atz_stats_t& from) {
+  to.k_trial_ms += from.k_trial_ms; to.k_chains_ms += from.k_chains_ms; to.k_other_ms += from.k_other_ms;
+  to.k_match_ms += from.k_match_ms; to.k_trial_launches += from.k_trial_launches;
+  to.k_chains_launches += from.k_chains_launches; to.k_match_launches += from.k_match_launches;
+  to.k_chains_alg_bytes += from.k_chains_alg_bytes; to.k_match_positions += from.k_match_positions;
+  from = atz_stats_t{};
+}
+
+// Pre-runs.  A multi-block stream's first block names its memLevel (k_inflate's hint), and its header
+// names its clevel group, so the trials of that group at that memLevel hold the stream's likely
+// winner.  When they sit deep in the stream's list (index >= ATZ_PRERUN, default 8: FLEVEL 1 streams
+// at memLevel <= 6, FLEVEL 3 at <= 5 ...), the rounds reach them late, and they are the round's slowest
+// trials there (whole-stream parses at small memLevels: many blocks, many fast-level chain walks), which
+// every round waits for.  So each pipe runs them at the start of its sweep on its second HIP stream,
+// beside the rounds (a pre-run lane), and the rule walk uses their results when it gets there.  A
+// pre-run is the same trial: whole match table, no symbol saving or replay, best ident the eligibility
+// floor (elig_floor; 0 for atz_sweep's exact idents), so its result is the one the trial would give at
+// its turn -- a "cannot beat" stop under a lower best ident also cannot beat the higher one the stream
+// has by then -- and its mismatch list is extracted on the device whenever it can become the stream's
+// recompression.  A stream whose next trial is a pre-run still in flight waits a round.
+static uint32_t prerun_min() {
+  static const uint32_t v = [] { const char* e = std::getenv("ATZ_PRERUN"); return e ? (uint32_t)std::max(0, std::atoi(e)) : 0u; }();
+  return v;
+}
+static bool prerun_group(int type, int clevel) {   // the clevels of a header's FLEVEL (Z/deflate.c:748-755)
+  switch (type & 3) {
+    case 0: return clevel <= 1;
+    case 1: return clevel >= 2 && clevel <= 5;
+    case 2: return clevel == 6;
+    default: return clevel >= 7;
+  }
+}
+// prelane_launch's second half, on the lane's thread: the match tables, the trials, their mismatch lists
+// and the read-backs into pinned memory, then ev_done.
+static int prelane_enqueue(atz_ctx* x, PreLane& L, Pipe* lp, const uint8_t* d_file, const SweepOpts& so,
+                           std::vector<Trial>* in, std::vector<std::pair<uint32_t, uint32_t>>* win, size_t nt) {
+  trials_order(x, in, L.S);
+  if (int r = trials_first_launch(x, lp, d_file, L.S, so, L.bases)) return r;
+  // per launched trial (launch order): who it is, and its mismatch-list job
+  L.dj.assign(nt, DiffJob{});
+  uint64_t dpos = 0;
+  for (int k = 0; k < 3; k++) {
+    L.who[k].resize(L.S.tr[k].size());
+    for (size_t q = 0; q < L.S.tr[k].size(); q++) {
+      const Trial& t = L.S.tr[k][q];
+      L.who[k][q] = win[k][L.S.perm[k][q]];
+      DiffJob& d = L.dj[L.bases[k] + q];
+      d.out_off = t.out_off; d.orig_off = x->recs[t.stream].offset; d.comp_len = x->recs[t.stream].comp_len;
+      d.dst = dpos; d.cap = std::min<uint64_t>(d.comp_len, x->o.recomp_tresh);
+      dpos += d.cap;
+    }
+  }
+  if (int r = upload(lp, lp->d_diffjobs, L.dj.data(), nt * sizeof(DiffJob))) return r;
+  if (int r = lp->d_diffpos.reserve(dpos * 4 + 64)) return r;
+  if (int r = lp->d_diffval.reserve(dpos + 64)) return r;
+  if (int r = lp->d_diffcnt.reserve(nt * 8 + 64)) return r;
+  kbeg(lp, 3);
+  hipLaunchKernelGGL(k_diffs_pre, dim3((uint32_t)nt), dim3(64), 0, lp->st, lp->d_out.as<uint8_t>(), d_file,
+                     lp->d_diffjobs.as<DiffJob>(), lp->d_tres.as<TrialRes>(), x->o.recomp_tresh,
+                     lp->d_diffpos.as<uint32_t>(), lp->d_diffval.as<uint8_t>(), lp->d_diffcnt.as<uint64_t>(), (uint32_t)nt);
+  kend(lp);
+  {
+    Pipe* c = lp;   // (KCHECK's stream)
+    KCHECK("k_diffs_pre");
+  }
+  if (int r = L.pres.reserve(nt * sizeof(TrialRes) + 64)) return r;
+  if (int r = L.ppos.reserve(dpos * 4 + 64)) return r;
+  if (int r = L.pval.reserve(dpos + 64)) return r;
+  if (int r = L.pcnt.reserve(nt * 8 + 64)) return r;
+  HIPCHK(hipMemcpyAsync(L.pres.p, lp->d_tres.p, nt * sizeof(TrialRes), hipMemcpyDeviceToHost, lp->st));
+  if (dpos) {
+    HIPCHK(hipMemcpyAsync(L.ppos.p, lp->d_diffpos.p, dpos * 4, hipMemcpyDeviceToHost, lp->st));
+    HIPCHK(hipMemcpyAsync(L.pval.p, lp->d_diffval.p, dpos, hipMemcpyDeviceToHost, lp->st));
+  }
+  HIPCHK(hipMemcpyAsync(L.pcnt.p, lp->d_diffcnt.p, nt * 8, hipMemcpyDeviceToHost, lp->st));
+  HIPCHK(hipEventRecord(L.ev_done, lp->st));
+  return 0;
+}
+static int prelane_launch(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss,
+                          const std::vector<uint32_t>& batch, const SweepOpts& so) {
+  PreLane& L = *x->lanes[(size_t)c->id];
+  L.state = 0; L.n_launched = L.n_used = 0;
+  const uint32_t pmin = prerun_min();
+  if (!pmin || x->o.recomp_tresh > 4096) return 0;   // (mismatch lists of at most recomp_tresh entries each)
+  Pipe* lp = L.p.get();
+  HIPCHK(hipStreamSynchronize(lp->st));
+  std::vector<Trial> in[3];
+  std::vector<std::pair<uint32_t, uint32_t>> win[3];
+  std::vector<std::pair<uint32_t, int>> need;
+  uint64_t out_tot = 0, sym_tot = 0;
+  for (uint32_t s : batch) {
+    StreamState& st = ss[s];
+    st.pre.clear();
+    const uint32_t m = x->recs[s].mhint;
+    const uint64_t n = x->recs[s].infl_len;
+    if (!m || st.phase != 0 || st.idx != 0 || n >= (1ull << 31)) continue;
+    const std::vector<uint32_t>& l = *st.list;
+    for (uint32_t i = pmin; i < l.size(); i++) {
+      const int cl = (int)(l[i] >> 16), w = (int)((l[i] >> 8) & 0xff), mm = (int)(l[i] & 0xff);
+      if ((uint32_t)mm != m || !prerun_group(x->recs[s].type, cl)) continue;
+      const int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
+      Trial t{};
+      t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)mm;
+      t.mode = 2;   // host-only: whole match table (no rerun)
+      t.best_ident = elig_floor(x, x->recs[s].comp_len);
+      t.out_off = out_tot; t.out_cap = bound(n, w, mm) + 64;
+      out_tot += (t.out_cap + 255) & ~255ull;
+      const uint64_t sw = sym_words(kind, (uint32_t)mm, n);
+      t.sym_off = sym_tot; sym_tot += sw;
+      PreRun pr;
+      pr.idx = i; pr.c = (uint8_t)cl; pr.w = (uint8_t)w; pr.m = (uint8_t)mm;
+      win[kind].push_back({s, (uint32_t)st.pre.size()});
+      st.pre.push_back(std::move(pr));
+      in[kind].push_back(t);
+      if (kind) need.push_back({s, mm});
+    }
+  }
+  const size_t nt = in[0].size() + in[1].size() + in[2].size();
+  if (!nt) return 0;
+  if (int r = ensure_chains(x, lp, need)) return r;
+  HIPCHK(hipEventRecord(L.ev_chains, lp->st));   // the rounds' match walks wait for these tables
+  for (int k = 1; k < 3; k++)
+    for (Trial& t : in[k]) t.chain_off = x->chain_off[t.stream][t.memlevel];
+  if (int r = lp->d_out.reserve(out_tot + 4096)) return r;
+  if (int r = lp->d_syms.reserve(sym_tot * 4 + 4096)) return r;
+  L.state = 1;
+  L.n_launched = nt;
+  L.enqueued = false;
+  L.rc = 0;
+  L.th = std::thread([x, &L, lp, d_file, so, in = std::move(in), win = std::move(win), nt]() mutable {
+    if (hipSetDevice(x->dev) != hipSuccess) { L.rc = ATZ_E_HIP; L.enqueued = true; return; }
+    L.rc = prelane_enqueue(x, L, lp, d_file, so, in, win, nt);
+    L.enqueued = true;
+  });
+  return 0;
+}
+// The pre-run results, once in (block: wait for them): into the streams' PreRun entries.
+static int prelane_poll(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, bool block) {
+  PreLane& L = *x->lanes[(size_t)c->id];
+  if (L.state != 1) return 0;
+  if (!block && !L.enqueued.load()) return 0;
+  L.join();
+  if (L.rc) { L.state = 0; return L.rc; }
+  const hipError_t e = block ? hipEventSynchronize(L.ev_done) : hipEventQuery(L.ev_done);
+  if (e == hipErrorNotReady) { (void)hipGetLastError(); return 0; }
+  HIPCHK(e);
+  Pipe* lp = L.p.get();
+  kcollect(lp);
+  fold_kernel_stats(c->stats, lp->stats);
+  const TrialRes* R = L.pres.as<TrialRes>();
+  const uint32_t* pos = L.ppos.as<uint32_t>();
+  const uint8_t* val = L.pval.as<uint8_t>();
+  const uint64_t* cnt = L.pcnt.as<uint64_t>();
+  for (int k = 0; k < 3; k++)
+    for (size_t q = 0; q < L.S.tr[k].size(); q++) {
+      const size_t g = L.bases[k] + q;
+      PreRun& pr = ss[L.who[k][q].first].pre[L.who[k][q].second];
+      pr.r = R[g];
+      if (pr.r.state == TR_NEED_R || cnt[g] > L.dj[g].cap) return ATZ_E_INTERNAL;   // whole tables: never
+      pr.pos.assign(pos + L.dj[g].dst, pos + L.dj[g].dst + cnt[g]);
+      pr.val.assign(val + L.dj[g].dst, val + L.dj[g].dst + cnt[g]);
+      pr.ready = true;
+      account_trial(x, c, k, L.S.tr[k][q], pr.r);
+    }
+  forget_tmp_chains(x, lp);
+  L.state = 2;
+  return 0;
+}
+
 // One round of pipe c over its batch `active`: the next K list entries of every stream (speculatively:
 // a stream that stops at its j-th trial discards the results of the later ones), K sized so the rounds
 // fill the GPU.  Results are applied per stream strictly in list order, so the outcome is the
@@ -1981,7 +2280,8 @@ struct Round {
   struct PendDiff { bool live = false; DiffJob d{}; };
   std::vector<PendDiff> pend;      // a stream's live diff job: its latest improvement within recomp_tresh
   std::vector<uint32_t> jpos;      // where each stream's rule walk resumes
-  uint64_t ntr = 0, nsc = 0, nhz = 0, nspec = 0;
+  std::vector<const PreRun*> vir;  // mine entries of kind 3: list entries whose pre-run result is in
+  uint64_t ntr = 0, nsc = 0, nhz = 0, nspec = 0, npre = 0;
 
   Round(atz_ctx* x_, Pipe* c_, const uint8_t* f, std::vector<StreamState>& ss_, const SweepOpts& so_,
         std::vector<uint32_t>& a_, std::vector<uint32_t>& w_)
@@ -1995,6 +2295,17 @@ struct Round {
 
   // The trials of the next K list entries of every stream, within the round's scratch budget.
   void build_lists() {
+    // a stream whose next trial is a pre-run still in flight waits for the next round
+    if (x->lanes[(size_t)c->id]->state == 1) {
+      size_t keep = 0;
+      for (size_t a = 0; a < active.size(); a++) {
+        const PreRun* pr = ss[active[a]].pre_at(ss[active[a]].idx);
+        if (pr && !pr->ready) waiting.push_back(active[a]);
+        else active[keep++] = active[a];
+      }
+      active.resize(keep);
+    }
+    if (active.empty()) { mbeg.assign(1, 0); return; }
     K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, round_target(x) / active.size()));
     mbeg.assign(active.size() + 1, 0);
     mine.reserve(active.size() * K);
@@ -2012,6 +2323,12 @@ struct Round {
         break;
       }
       for (uint32_t j = 0; j < K && st.idx + j < st.list->size(); j++) {
+        if (const PreRun* pr = st.pre_at(st.idx + j)) {   // run ahead: its result, when in
+          if (!pr->ready) break;
+          mine.push_back({3, (uint32_t)vir.size()});
+          vir.push_back(pr);
+          continue;
+        }
         const uint32_t p = (*st.list)[st.idx + j];
         const int cl = (int)(p >> 16), w = (int)((p >> 8) & 0xff), m = (int)(p & 0xff);
         Trial t{};
@@ -2044,6 +2361,8 @@ struct Round {
   // Replays first (they need the pairs' bucket depths only), duplicates, the eligibility floor, then the
   // bucket tables the other trials read (stream-ordered before the match walks: no sync).
   int plan() {
+    PreLane& L = *x->lanes[(size_t)c->id];
+    if (L.state == 1) HIPCHK(hipStreamWaitEvent(c->st, L.ev_chains, 0));   // tables the lane registered
     if (replay_on() && x->depth_pin.p) {
       if (int r = ensure_depths(x, c, need, need_b)) return r;
       HIPCHK(pipe_sync(c));
@@ -2159,8 +2478,11 @@ struct Round {
     held[a] = 0;
     for (uint32_t j = jpos[a]; j < mbeg[a + 1]; j++) {
       if (st.phase != phase0) { nspec += mbeg[a + 1] - j; break; }   // stopped earlier this round
-      const Trial& t = tr[mine[j].first][mine[j].second];
-      const TrialRes& r = trres[mine[j].first][mine[j].second];
+      const bool virt = mine[j].first == 3;
+      const PreRun* pr = virt ? vir[mine[j].second] : nullptr;
+      const Trial* tp = virt ? nullptr : &tr[mine[j].first][mine[j].second];
+      const TrialRes& r = virt ? pr->r : trres[mine[j].first][mine[j].second];
+      npre += virt;
       if (r.state == TR_NEED_R) {
         if (!defer) return ATZ_E_INTERNAL;   // every rerun a walk waits for has run
         jpos[a] = j;
@@ -2175,7 +2497,8 @@ struct Round {
       bool fullmatch = false;
       if (r.state == TR_FULL && r.ident > st.ident) {
         st.ident = r.ident;
-        st.c = t.clevel; st.w = t.window; st.m = t.memlevel;
+        if (virt) { st.c = pr->c; st.w = pr->w; st.m = pr->m; }
+        else { st.c = tp->clevel; st.w = tp->window; st.m = tp->memlevel; }
         st.first_diff = -1;
         st.rawdiff.clear(); st.diffval.clear();
         pend[a].live = false;   // an earlier improvement's diffs are superseded
@@ -2183,10 +2506,16 @@ struct Round {
         else {
           if (r.ident + x->o.mismatch_tol >= C) fullmatch = true;
           if (C - r.ident <= x->o.recomp_tresh) {     // diffs are only ever written for recomp streams
-            DiffJob& d = pend[a].d;
-            d.out_off = t.out_off; d.out_len = r.out_len; d.orig_off = x->recs[s].offset;
-            d.comp_len = C; d.dst = 0; d.cap = C - r.ident;
-            pend[a].live = true;
+            if (virt) {   // extracted by the lane (k_diffs_pre)
+              if (pr->pos.size() != C - r.ident) return ATZ_E_INTERNAL;
+              st.rawdiff = pr->pos; st.diffval = pr->val;
+              st.first_diff = st.rawdiff.empty() ? -1 : (int64_t)st.rawdiff[0];
+            } else {
+              DiffJob& d = pend[a].d;
+              d.out_off = tp->out_off; d.out_len = r.out_len; d.orig_off = x->recs[s].offset;
+              d.comp_len = C; d.dst = 0; d.cap = C - r.ident;
+              pend[a].live = true;
+            }
           }
         }
       }
@@ -2296,27 +2625,21 @@ struct Round {
         }
       }
     for (int k = 0; k < 3; k++)
-      for (size_t q = 0; q < tr[k].size(); q++) {
-        const TrialRes& r = trres[k][q];
-        const uint64_t C = x->recs[tr[k][q].stream].comp_len;
-        c->stats.trial_parsed_bytes += r.parsed;
-        c->stats.n_fast_fallbacks += r.fallbacks & 0xffffffffull;
-        c->stats.n_fast_restarts += r.fallbacks >> 32;
-        c->stats.trial_cyc_total += r.cyc_total; c->stats.trial_cyc_tree += r.cyc_tree;
-        c->stats.trial_cyc_emit += r.cyc_emit; c->stats.trial_blocks += r.blocks;
-        c->stats.trial_cyc_heap += r.cyc_heap; c->stats.trial_cyc_fallback += r.cyc_fallback;
-        c->stats.trial_symbols += r.symbols;
-        uint64_t* gk = c->kind[k][tr[k][q].clevel];
-        gk[0]++; gk[1] += r.cyc_total; gk[2] += r.cyc_tree; gk[3] += r.cyc_emit; gk[4] += r.cyc_heap;
-        gk[5] += r.cyc_fallback; gk[6] += r.parsed; gk[7] += r.symbols; gk[8] += r.cyc_scan; gk[9] += r.cyc_send;
-        for (int i = 0; i < 4; i++) gk[10 + i] += r.cyc_sec[i];
-        // trial input read + compare read (bytes emitted and compared against the original)
-        if (!(tr[k][q].mode & 128))   // duplicates are not launched; a trial never rerun stopped at its prefix
-          c->stats.k_trial_alg_bytes += r.state == TR_NEED_R ? r.parsed
-                                        : x->recs[tr[k][q].stream].infl_len + (r.out_len < C ? r.out_len : C);
-        if (timing_level() >= 3 && !(tr[k][q].mode & 128)) c->diag_rt.push_back({r.rt0, r.rt1});
-      }
+      for (size_t q = 0; q < tr[k].size(); q++) account_trial(x, c, k, tr[k][q], trres[k][q]);
     if (!timing_on()) return;
+    if (timing_level() >= 3) {   // when the round's first-pass trials ended, from the first one's start (us)
+      std::vector<uint32_t> st0, en;
+      for (int k = 0; k < 3; k++)
+        for (size_t q = 0; q < tr[k].size(); q++)
+          if (!(tr[k][q].mode & 128) && trres[k][q].rt1) { st0.push_back(trres[k][q].rt0); en.push_back(trres[k][q].rt1); }
+      if (!en.empty()) {
+        const uint32_t b = *std::min_element(st0.begin(), st0.end());
+        std::sort(en.begin(), en.end());
+        auto q = [&](double f) { return (en[std::min(en.size() - 1, (size_t)(f * (double)en.size()))] - b) / 100.0; };
+        std::fprintf(stderr, "atz: pipe %d round %llu ends (us after the first start): n %zu p50 %.0f p90 %.0f p95 %.0f p98 %.0f p99 %.0f max %.0f\n",
+                     c->id, (unsigned long long)round, en.size(), q(0.5), q(0.9), q(0.95), q(0.98), q(0.99), q(1.0));
+      }
+    }
     // slowest trials of the round (diagnostics)
     std::vector<std::pair<uint64_t, std::pair<int, size_t>>> top;
     for (int k = 0; k < 3; k++)
@@ -2341,7 +2664,19 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
   std::vector<uint32_t> active;
   const SweepOpts so{x->o.recomp_tresh, x->o.sizediff_tresh, x->o.shortcut_len, x->o.mismatch_tol};
   uint64_t rounds = 0;
+  PreLane& L = *x->lanes[(size_t)c->id];
+  struct LaneDrain {   // nothing of the lane stays in flight past the sweep (its buffers serve the next one)
+    PreLane& L;
+    ~LaneDrain() { L.join(); if (L.state == 1) (void)hipStreamSynchronize(L.p->st); }
+  } drain{L};
+  L.state = 0;
+  bool first = true;
   while (sched_take(x, c->id, active)) {
+    if (first) {   // the pipe's first batch is all its streams published so far
+      first = false;
+      if (int r = prelane_launch(x, c, d_file, ss, active, so)) return r;
+    }
+    if (int r = prelane_poll(x, c, ss, false)) return r;
     rounds++;
     std::vector<uint32_t> waiting;
     struct Give {   // the batch goes back on every exit from the round (an error aborts the sweep anyway)
@@ -2351,6 +2686,11 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     Round R(x, c, d_file, ss, so, active, waiting);
     const auto tl0 = std::chrono::steady_clock::now();
     R.build_lists();
+    if (active.empty()) {   // every stream waits for the pre-run lane
+      rounds--;
+      if (int r = prelane_poll(x, c, ss, true)) return r;
+      continue;
+    }
     const auto ta = std::chrono::steady_clock::now();
     if (int r = R.plan()) return r;
     const auto tb = std::chrono::steady_clock::now();
@@ -2372,7 +2712,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     c->t_apply += ms_since(tc);
     c->stats.n_trials += R.ntr; c->stats.n_trials_shortcut += R.nsc; c->stats.n_hazard += R.nhz;
     c->stats.n_trials_speculative += R.nspec;
+    L.n_used += R.npre;
   }
+  if (int r = prelane_poll(x, c, ss, true)) return r;
+  c->stats.n_trials_speculative += L.n_launched - L.n_used;   // pre-runs past their stream's stop
   c->stats.n_rounds = rounds;
   c->stats.sweep_ms = ms_since(t0);
   return 0;
@@ -2388,7 +2731,16 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
     // the idle second stream (see Pipe::pst): with it two pipes share a hardware queue and their
     // kernels run back to back, so fewer LDS-heavy kernels co-run (measured faster)
     if (hipStreamCreateWithFlags(&p->pst, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
+    // its pre-run lane runs on that stream (prelane_launch)
+    std::unique_ptr<PreLane> L(new PreLane());
+    L->p.reset(new Pipe());
+    L->p->st = p->pst;
+    L->p->id = p->id;
+    if (hipEventCreateWithFlags(&L->ev_chains, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&L->ev_done, hipEventDisableTiming) != hipSuccess)
+      return ATZ_E_HIP;
     c->pipes.push_back(std::move(p));
+    c->lanes.push_back(std::move(L));
   }
   return 0;
 }
@@ -3580,6 +3932,7 @@ int atz_precompress(atz_ctx_t* c, const uint8_t* file, uint64_t len, uint8_t** a
   return guarded([&]() -> int {
     (void)hipGetLastError();
     if (!c || (!file && len) || !atz || !atz_len) return ATZ_E_ARG;
+    dev_mark_call();
     const auto t0 = std::chrono::steady_clock::now();
     if (int r = upload(c, c->d_file, file, len)) return r;
     HIPCHK(hipStreamSynchronize(c->st));
@@ -3602,6 +3955,7 @@ int atz_precompress(atz_ctx_t* c, const uint8_t* file, uint64_t len, uint8_t** a
                    "register %.1f ms on the helper), D2H %.1f ms, unregister %.1f ms\n", t_up, t_dev - t_up,
                    t_take - t_dev, ho.t_reg, t_d2h - t_take, ms_since(t0) - t_d2h);
     *atz = h; *atz_len = al;
+    c->stats.dev_bytes_peak = g_dev.peak.load(); c->stats.dev_bytes_held = g_dev.cur.load();
     if (stats) *stats = c->stats;
     return ATZ_OK;
   });
@@ -3612,6 +3966,7 @@ int atz_precompress_device(atz_ctx_t* c, const uint8_t* d_file, const uint8_t* h
   return guarded([&]() -> int {
     (void)hipGetLastError();
     if (!c || !d_file || !h_file || !d_atz || !atz_len) return ATZ_E_ARG;
+    dev_mark_call();
     uint64_t al = 0;
     auto tc = std::chrono::steady_clock::now();
     if (int r = precompress_dev(c, d_file, h_file, len, &al, nullptr)) return r;
@@ -3619,6 +3974,7 @@ int atz_precompress_device(atz_ctx_t* c, const uint8_t* d_file, const uint8_t* h
       std::fprintf(stderr, "atz: precompress call %.2f ms (inside: %.2f ms)\n", ms_since(tc), c->stats.total_ms);
     *d_atz = c->d_atz.as<uint8_t>();
     *atz_len = al;
+    c->stats.dev_bytes_peak = g_dev.peak.load(); c->stats.dev_bytes_held = g_dev.cur.load();
     if (stats) *stats = c->stats;
     return ATZ_OK;
   });
@@ -3697,6 +4053,7 @@ int atz_shard_scan(atz_ctx_t* c, const uint8_t* d_file, const uint8_t* h_file, u
   return guarded([&]() -> int {
     (void)hipGetLastError();
     if (!c || !d_file || !h_file || !blob || !blob_len || world < 1 || rank < 0 || rank >= world) return ATZ_E_ARG;
+    dev_mark_call();   // (the peak runs on through atz_shard_sweep, whose stats report it)
     std::vector<uint64_t> b;
     if (int r = shard_scan_impl(c, d_file, h_file, len, rank, world, b)) { c->shard.stage = 0; return r; }
     uint8_t* p = (uint8_t*)std::malloc(b.size() * 8 + 1);
@@ -3723,6 +4080,7 @@ int atz_shard_sweep(atz_ctx_t* c, const uint8_t* d_file, const uint8_t* h_file, 
     if (!f.empty()) std::memcpy(p, f.data(), f.size());
     *recomp_flags = p; *n_flags = f.size();
     *piece_len = c->shard.piece_len;
+    c->stats.dev_bytes_peak = g_dev.peak.load(); c->stats.dev_bytes_held = g_dev.cur.load();
     if (stats) *stats = c->stats;
     return ATZ_OK;
   });

@@ -8,8 +8,13 @@ over the C ABI's atz_shard_* calls (include/atz_accel.h).  The data path has two
   2. gather of the ATZ1 pieces (descriptors + inflated payloads of each rank's recompressed streams,
      main.cpp:805-831) to rank 0, one point-to-point transfer per rank, received in place at its
      offset in rank 0's output buffer; rank 0 then writes the header and the residue (main.cpp:764-801).
-The ATZ1 bytes equal the one-GPU result.
+The ATZ1 bytes equal the one-GPU result.  precompress_sharded keeps the ATZ1 in rank 0's HBM (the
+metric's device-resident output); precompress_sharded_to_file is the host path (the CLI's output file):
+each rank copies its own piece device -> host into the file at its offset (payloads go to
+the host per GPU, not over xGMI), and rank 0 writes only the header and the residue.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -81,18 +86,71 @@ def gather_pieces(ctx, piece_lens, out, out_device="cuda", group=None):
             w.wait()
 
 
+def _scan_and_sweep(ctx, d_file, data, group):
+    """Exchange 1 and the sweep of this rank's share: (piece_lens, all recomp flags, recompressed total, stats)."""
+    dptr = d_file.data_ptr()
+    blob = ctx.shard_scan(dptr, data, dist.get_rank(group), dist.get_world_size(group))
+    blobs = allgather_bytes(blob, group)
+    piece_len, flags, n_recomp, st = ctx.shard_sweep(dptr, data, blobs)
+    meta = allgather_ints([piece_len, n_recomp, len(flags)], group)
+    return [m[0] for m in meta], b"".join(allgather_bytes(flags, group)), sum(m[1] for m in meta), st
+
+
+def precompress_sharded_to_file(ctx, d_file, data, path, group=None, device="cuda"):
+    """Precompress `data` over every rank of `group` into the file `path` (one node: the ranks share the
+    filesystem).  Rank r copies its piece (descriptors + payloads of its recompressed streams) from its
+    own HBM into the file at 28 + the lengths of the pieces before it; rank 0 assembles the header and
+    the residue in its HBM and writes just those two ranges.  Returns (atz_len, stats); atz_len on every
+    rank once the file is complete.  (device: where the pieces are staged, "cpu" for the host-logic tests.)"""
+    rank = dist.get_rank(group)
+    piece_lens, flags, n_recomp, st = _scan_and_sweep(ctx, d_file, data, group)
+    pieces = sum(piece_lens)
+    if rank == 0:
+        with open(path, "wb"):
+            pass
+    dist.barrier(group)
+    off = HEADER + sum(piece_lens[:rank])
+    if piece_lens[rank]:
+        piece = torch.empty(piece_lens[rank], dtype=torch.uint8, device=device)
+        ctx.shard_piece(piece.data_ptr())
+        host = torch.empty(piece_lens[rank], dtype=torch.uint8, pin_memory=device != "cpu")
+        host.copy_(piece)
+        del piece
+        fd = os.open(path, os.O_WRONLY)
+        try:
+            mv, done = memoryview(host.numpy()), 0
+            while done < len(mv):
+                done += os.pwrite(fd, mv[done:], off + done)
+        finally:
+            os.close(fd)
+    n = 0
+    if rank == 0:
+        cap = HEADER + pieces + len(data) + 4096
+        out = torch.empty(cap, dtype=torch.uint8, device=device)   # only the header and the residue are written
+        n = ctx.shard_assemble(d_file.data_ptr(), len(data), flags, n_recomp, pieces, out.data_ptr(), cap)
+        head = out[:HEADER].cpu().numpy().tobytes()
+        tail = out[HEADER + pieces:n].cpu().numpy().tobytes()
+        del out
+        fd = os.open(path, os.O_WRONLY)
+        try:
+            os.pwrite(fd, head, 0)
+            done = 0
+            while done < len(tail):
+                done += os.pwrite(fd, memoryview(tail)[done:], HEADER + pieces + done)
+            os.ftruncate(fd, n)
+        finally:
+            os.close(fd)
+    n = allgather_ints([n], group)[0][0]
+    return n, st
+
+
 def precompress_sharded(ctx, d_file, data, group=None, out_device="cuda"):
     """Precompress `data` (host bytes; d_file: the same bytes resident on this rank's GPU, a uint8 tensor
     with >= 4096 bytes of slack) over every rank of `group`.  Returns (atz tensor, atz_len, stats) on
     rank 0 (ATZ1 bytes = atz[:atz_len], on out_device) and (None, 0, stats) elsewhere."""
-    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    rank = dist.get_rank(group)
     dptr = d_file.data_ptr()
-    blob = ctx.shard_scan(dptr, data, rank, world)
-    blobs = allgather_bytes(blob, group)
-    piece_len, flags, n_recomp, st = ctx.shard_sweep(dptr, data, blobs)
-    meta = allgather_ints([piece_len, n_recomp, len(flags)], group)
-    piece_lens = [m[0] for m in meta]
-    all_flags = allgather_bytes(flags, group)
+    piece_lens, flags, n_recomp, st = _scan_and_sweep(ctx, d_file, data, group)
     out = None
     if rank == 0:
         cap = HEADER + sum(piece_lens) + len(data) + 4096   # the residue is at most the whole file
@@ -100,6 +158,5 @@ def precompress_sharded(ctx, d_file, data, group=None, out_device="cuda"):
     gather_pieces(ctx, piece_lens, out, out_device, group)
     if rank != 0:
         return None, 0, st
-    n = ctx.shard_assemble(dptr, len(data), b"".join(all_flags), sum(m[1] for m in meta), sum(piece_lens),
-                           out.data_ptr(), out.numel())
+    n = ctx.shard_assemble(dptr, len(data), flags, n_recomp, sum(piece_lens), out.data_ptr(), out.numel())
     return out, n, st

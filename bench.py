@@ -414,6 +414,31 @@ def main():
         h2h = {"value": round(len(data) / 1e6 / ts[-1], 3), "unit": "MB/s", "ms": round(ts[-1] * 1000, 2),
                "atz_bytes": n.value, "what": "atz_precompress: host file bytes -> host ATZ1 bytes (H2D of the input, "
                                              "D2H of the ATZ1 included), the uncomp CLI's path; not the metric's value"}
+    elif world > 1 and args.mode == "file" and not args.no_h2h:
+        # the host path at N > 1 (antiz_amd.shard.precompress_sharded_to_file): every rank copies its own
+        # piece from its HBM into the output file at its offset, rank 0 writes the header and the residue
+        from antiz_amd import shard
+        opath = os.path.join("/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir(),
+                             "atz_bench_%d.atz" % os.getppid())
+        ts = []
+        for _ in range(2):   # the first call sizes the pinned staging
+            dist.barrier()
+            t1 = time.perf_counter()
+            hn, _ = shard.precompress_sharded_to_file(ctx, dev, data, opath, group=group)
+            dist.barrier()
+            ts.append(time.perf_counter() - t1)
+        if rank == 0:
+            with open(opath, "rb") as f:
+                hsha = hashlib.sha256(f.read()).hexdigest()
+            h2h = {"value": round(len(data) / 1e6 / ts[-1], 3), "unit": "MB/s", "ms": round(ts[-1] * 1000, 2),
+                   "atz_bytes": hn, "atz_sha256": hsha[:16],
+                   "identical_to_reference": (atz_check or {}).get("atz_sha256") == hsha[:16]
+                                             and bool((atz_check or {}).get("identical_to_reference")),
+                   "what": "the host path over %d GPUs: device-resident input -> ATZ1 file (each rank writes its own "
+                           "piece device -> host at its offset; SURVEY s8e); not the metric's value" % world}
+        dist.barrier()
+        if rank == 0:
+            os.remove(opath)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -84,6 +84,9 @@ typedef struct {
     uint64_t n_replay_checked;                           /* replays offered under a match-table check (passed or not) */
     uint64_t n_trials_duplicate;                         /* replays whose output equals their saver's: not launched */
     uint64_t n_fast_restarts;                            /* fast-level exact walks that changed the parse path */
+    /* device memory the library held in this process (every context's buffers): the peak during the call,
+       and what stays allocated after it (kept for the next call's reuse) */
+    uint64_t dev_bytes_peak, dev_bytes_held;
 } atz_stats_t;
 
 enum {

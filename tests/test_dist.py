@@ -103,15 +103,19 @@ class FakeShardCtx:
         return 28 + pieces_len + flen
 
 
-def _shard_worker(rank, world, port, q):
+def _shard_worker(rank, world, port, q, path=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from antiz_amd import shard
     data = b"x" * 11
     fake = FakeShardCtx(rank, world)
-    out, n, st = shard.precompress_sharded(fake, torch.zeros(16, dtype=torch.uint8), data, out_device="cpu")
-    q.put((rank, None if out is None else out[:n].numpy().tobytes(), n, st, fake.calls))
+    if path is None:
+        out, n, st = shard.precompress_sharded(fake, torch.zeros(16, dtype=torch.uint8), data, out_device="cpu")
+        q.put((rank, None if out is None else out[:n].numpy().tobytes(), n, st, fake.calls))
+    else:   # the host path: every rank writes its piece into the file
+        n, st = shard.precompress_sharded_to_file(fake, torch.zeros(16, dtype=torch.uint8), data, path, device="cpu")
+        q.put((rank, open(path, "rb").read() if rank == 0 else None, n, st, fake.calls))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -135,3 +139,25 @@ def test_precompress_sharded_exchanges(world):
         assert res[r][2] == {"rank": r} and res[r][3] == ["scan", "sweep"]
         if r:
             assert res[r][0] is None and res[r][1] == 0
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_precompress_sharded_to_file(world, tmp_path):
+    """The host path: each rank writes its own piece into the output file at its prefix
+    offset; rank 0 writes the header and the residue around them.  The file equals rank 0's assembled ATZ1."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    path = str(tmp_path / "out.atz")
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q, path)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (atz, n, st, calls) for r, atz, n, st, calls in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    fake = FakeShardCtx(0, world)
+    want = b"H" * 28 + b"".join(bytes([0x10 + r]) * fake.piece_len(r) for r in range(world)) + b"R" * 11
+    assert res[0][0] == want
+    for r in range(world):
+        assert res[r][1] == len(want) and res[r][2] == {"rank": r} and res[r][3] == ["scan", "sweep"]

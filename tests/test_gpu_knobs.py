@@ -16,6 +16,8 @@ the ATZ1 bytes must equal the oracle's (the reference's algorithm, oracle/) for 
   ATZ_PREFIX_MIN the match-table prefix floor in positions (default 3072 where big_sweep holds, else 1024)
   ATZ_ELIG     0: every trial keeps the reference's exact rule to its end (default 1: a trial stops once
                it cannot make its stream recompressible; atz_accel.cpp elig_floor)
+  ATZ_PRERUN   i: a hinted stream's likely winners at list index >= i run ahead on the pipe's pre-run
+               lane (default 8; 0: none; atz_accel.cpp prelane_launch)
 """
 import hashlib
 import os
@@ -34,7 +36,9 @@ SETTINGS = [{"ATZ_REPLAY": "0"}, {"ATZ_REPLAY": "2"}, {"ATZ_REPLAY": "3"}, {"ATZ
             {"ATZ_SPEC_CONT": "0"}, {"ATZ_MW": "0"}, {"ATZ_MW": "9"}, {"ATZ_REPLAY": "0", "ATZ_DEDUP": "0", "ATZ_PIPES": "2", "ATZ_SPEC_CONT": "0"},
             {"ATZ_PIPES": "8", "ATZ_TARGET": "256"}, {"ATZ_PIPES": "6", "ATZ_TARGET": "65536"},
             {"ATZ_MHINT": "1"}, {"ATZ_MHINT": "0"}, {"ATZ_PREFIX_MIN": "3072", "ATZ_MHINT": "1"},
-            {"ATZ_ELIG": "0"}, {"ATZ_ELIG": "0", "ATZ_REPLAY": "0"}]
+            {"ATZ_ELIG": "0"}, {"ATZ_ELIG": "0", "ATZ_REPLAY": "0"},
+            {"ATZ_PRERUN": "0"}, {"ATZ_PRERUN": "1"}, {"ATZ_PRERUN": "1", "ATZ_ELIG": "0", "ATZ_PIPES": "1"},
+            {"ATZ_PRERUN": "2", "ATZ_TARGET": "65536"}]
 
 RUN = r"""
 import hashlib, sys

@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, path, chunksize, q):
+def _worker(rank, world, port, path, chunksize, q, out_path=None):
     try:
         sys.path.insert(0, ROOT)
         os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -40,8 +40,12 @@ def _worker(rank, world, port, path, chunksize, q):
         data = open(path, "rb").read()
         d = torch.frombuffer(bytearray(data) + bytearray(4096), dtype=torch.uint8).to("cuda")
         with antiz_amd.Context(chunksize=chunksize, device=0) as ctx:
-            out, n, st = shard.precompress_sharded(ctx, d, data, out_device="cuda")
-            atz = out[:n].cpu().numpy().tobytes() if out is not None else None
+            if out_path is None:
+                out, n, st = shard.precompress_sharded(ctx, d, data, out_device="cuda")
+                atz = out[:n].cpu().numpy().tobytes() if out is not None else None
+            else:   # the host path: each rank writes its piece into the file
+                n, st = shard.precompress_sharded_to_file(ctx, d, data, out_path)
+                atz = open(out_path, "rb").read() if rank == 0 else None
         q.put((rank, atz, st["n_streams"], st["n_recomp"], st["k_trial_alg_bytes"], None))
         dist.barrier()
         dist.destroy_process_group()
@@ -49,12 +53,12 @@ def _worker(rank, world, port, path, chunksize, q):
         q.put((rank, None, 0, 0, 0, repr(e)))
 
 
-def _run(world, path, chunksize):
+def _run(world, path, chunksize, out_path=None):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, path, chunksize, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, path, chunksize, q, out_path)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -191,3 +195,14 @@ def test_sharded_cost_split_on_clustered_input(clustered, world):
     assert counts[-1] < len(recs) // world
     work = [res[r][3] for r in range(world)]
     assert max(work) <= 2.0 * sum(work) / world, work
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_host_output_equals_oracle(sample, world, tmp_path):
+    """The host path: every rank copies its own piece from its HBM into the output file at
+    its offset, rank 0 writes the header and the residue; the file equals the oracle's ATZ1."""
+    path, data = sample
+    rc, ref, _ = _libs.ora_precompress(data, chunksize=65536)
+    assert rc == 0
+    res = _run(world, path, 65536, out_path=str(tmp_path / "out.atz"))
+    assert hashlib.sha256(res[0][0]).hexdigest() == hashlib.sha256(ref).hexdigest()
