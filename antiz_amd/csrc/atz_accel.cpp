@@ -34,6 +34,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <functional>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/atz_accel.h"
@@ -173,43 +174,6 @@ __global__ __launch_bounds__(64) void k_diffs(const uint8_t* __restrict__ out, c
   if (lane == 0) count[j] = k;
 }
 
-// The mismatch lists of pre-run trials (PreLane), decided on the device from each trial's result: a trial
-// that can become its stream's recompression (TR_FULL, ident < C_s, C_s - ident <= tresh) gets its list at
-// dst (C_s - ident entries, at most cap); the others count 0.
-__global__ __launch_bounds__(64) void k_diffs_pre(const uint8_t* __restrict__ out, const uint8_t* __restrict__ file,
-                                                 const DiffJob* __restrict__ jobs, const TrialRes* __restrict__ res,
-                                                 uint64_t tresh, uint32_t* __restrict__ pos, uint8_t* __restrict__ val,
-                                                 uint64_t* __restrict__ count, uint32_t n) {
-  const uint32_t j = blockIdx.x;
-  if (j >= n) return;
-  const int lane = threadIdx.x;
-  const DiffJob d = jobs[j];
-  const TrialRes r = res[j];
-  const bool want = r.state == TR_FULL && r.ident < d.comp_len && d.comp_len - r.ident <= tresh;
-  if (!want) { if (lane == 0) count[j] = 0; return; }
-  const uint8_t* o = out + d.out_off;
-  const uint8_t* f = file + d.orig_off;
-  const uint64_t sm = r.out_len < d.comp_len ? r.out_len : d.comp_len;
-  uint64_t k = 0;
-  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  for (uint64_t b = 0; b < d.comp_len; b += 64) {
-    const uint64_t i = b + lane;
-    bool m = false;
-    uint8_t v = 0;
-    if (i < d.comp_len) {
-      v = f[i];
-      m = i < sm ? o[i] != v : true;
-    }
-    const uint64_t bal = __ballot(m);
-    if (m) {
-      const uint64_t at = k + __popcll(bal & lt);
-      if (at < d.cap) { pos[d.dst + at] = (uint32_t)i; val[d.dst + at] = v; }
-    }
-    k += __popcll(bal);
-  }
-  if (lane == 0) count[j] = k;
-}
-
 #define HIPCHK(x)                                                     \
   do {                                                                \
     hipError_t e_ = (x);                                              \
@@ -285,17 +249,6 @@ struct Rec {
   uint8_t mhint = 0;            // k_inflate's first-block memLevel (0: none; whole match tables for it)
 };
 
-// A trial of a stream's list run ahead of its turn by the pipe's pre-run lane (PreLane): its result and,
-// where it can become the stream's recompression (C - ident <= recomp_tresh), its mismatch list.
-struct PreRun {
-  uint32_t idx = 0;               // list index (phase 0)
-  uint8_t c = 0, w = 0, m = 0;
-  bool ready = false;             // the result is in
-  TrialRes r{};
-  std::vector<uint32_t> pos;      // raw mismatch positions (main.cpp:699-714)
-  std::vector<uint8_t> val;
-};
-
 struct StreamState {
   // sweep
   const std::vector<uint32_t>* list = nullptr;   // packed (c<<16)|(w<<8)|m: the header type's shared list
@@ -312,12 +265,6 @@ struct StreamState {
   // levels 7-9 already run budget-free at (window, memLevel): level, longest PL a lazy read improved,
   // longest length read (cross-level duplicates, see level_dups)
   std::vector<std::array<uint16_t, 5>> xl;   // {window, memLevel, level, imp, len}
-  std::vector<PreRun> pre;        // its trials run ahead by the pre-run lane, by list index
-  const PreRun* pre_at(uint32_t i) const {
-    if (phase != 0) return nullptr;
-    for (const PreRun& p : pre) if (p.idx == i) return &p;
-    return nullptr;
-  }
 };
 
 
@@ -448,21 +395,37 @@ struct RpEntry {
 // Device memory in 1 GiB chunks (allocated on demand, kept across sweeps), handed out by a bump
 // pointer that each sweep resets: the context's hash-bucket cache and its saved symbol sequences.
 // Shared by the sweep's pipes (a stream's tables, built by whichever pipe ran its step, are read by
-// the next one), hence the lock; addresses are absolute.
+// the next one), hence the lock; addresses are absolute.  Sizes are rounded to 4 KiB classes, and a
+// released block (a finished stream's bucket tables: release_tables) serves the next request of its class.
 struct DevArena {
   static constexpr uint64_t CHUNK = 1ull << 30;
   std::mutex mu;
   std::vector<std::unique_ptr<DBuf>> chunks;
   std::vector<std::pair<uint64_t, uint64_t>> span;   // [lo, hi) of each chunk (holds() without the lock's allocator state)
+  std::unordered_map<uint64_t, std::vector<uint64_t>> freel;   // size class -> released addresses
   size_t cur = 0;
   uint64_t used = 0, total = 0, cap = 0;   // bytes in chunks[cur]; bytes handed out this sweep; limit
+  uint64_t reused = 0;                     // bytes served from released blocks this sweep
+  static uint64_t cls(uint64_t bytes) { return (bytes + 4095) & ~4095ull; }
   void reset(uint64_t cap_) {
     std::lock_guard<std::mutex> lk(mu);
-    cur = 0; used = 0; total = 0; cap = cap_;
+    cur = 0; used = 0; total = 0; cap = cap_; reused = 0;
+    freel.clear();
+  }
+  void release(uint64_t a, uint64_t bytes) {
+    std::lock_guard<std::mutex> lk(mu);
+    freel[cls(bytes)].push_back(a);
   }
   uint64_t alloc(uint64_t bytes) {   // device address (256-byte aligned), 0: none (cap reached, no memory)
-    bytes = (bytes + 255) & ~255ull;
+    bytes = cls(bytes);
     std::lock_guard<std::mutex> lk(mu);
+    auto it = freel.find(bytes);
+    if (it != freel.end() && !it->second.empty()) {
+      const uint64_t a = it->second.back();
+      it->second.pop_back();
+      reused += bytes;
+      return a;
+    }
     if (total + bytes > cap) return 0;
     while (cur < chunks.size() && used + bytes > chunks[cur]->n) { cur++; used = 0; }
     if (cur == chunks.size()) {
@@ -494,7 +457,16 @@ struct Pipe {
   hipStream_t st = nullptr;
   KTimer kt;
   atz_stats_t stats{};
-  DBuf d_trials, d_tres, d_out, d_syms, d_R, d_mjobs, d_chains, d_diffjobs, d_diffpos, d_diffval, d_diffcnt, d_djobs;
+  DBuf d_trials, d_tres, d_out, d_syms, d_R, d_mjobs, d_diffjobs, d_diffpos, d_diffval, d_diffcnt, d_djobs;
+  // round-local bucket tables (the context's cache is full): one buffer per ensure_chains call of the
+  // round (a later call must not move an earlier call's tables), kept for the next rounds' reuse
+  std::vector<std::unique_ptr<DBuf>> d_chains;
+  size_t chains_next = 0;
+  // ATZ_KSTREAMS=1: the fast and slow trial launches of a round on streams of their own (fork after the
+  // tables, join before the results), so their tails overlap instead of adding up
+  hipStream_t kst[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
+  bool joined[2] = {true, true};
   ChainBufs cb;
   // a second stream that stays idle: it only shifts how the process's GPU_MAX_HW_QUEUES (4) hardware
   // queues are shared by the pipes' streams (two pipes then share a queue, which measured faster
@@ -514,6 +486,11 @@ struct Pipe {
   uint64_t n_copy = 0, n_sync = 0;
   uint64_t kind[3][10][14] = {};
   ~Pipe() {
+    for (int i = 0; i < 2; i++) {
+      if (kst[i]) { hipStreamSynchronize(kst[i]); hipStreamDestroy(kst[i]); }
+      if (ev_join[i]) hipEventDestroy(ev_join[i]);
+    }
+    if (ev_fork) hipEventDestroy(ev_fork);
     if (pst) { hipStreamSynchronize(pst); hipStreamDestroy(pst); }
     if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
     for (hipEvent_t e : kt.pool) hipEventDestroy(e);
@@ -530,33 +507,6 @@ struct TrialSet {
   std::vector<uint32_t> perm[3];
   std::vector<TrialRes> res[3];
   size_t base = 0;   // next free slot of d_trials / d_tres
-};
-
-// A pipe's pre-run lane: the likely winners of its hinted streams, run ahead of their turn on the pipe's
-// second HIP stream while the rounds go on (run_prelane).  Its own scratch and kernel timers (a Pipe whose
-// stream is the owner's pst); results and mismatch lists land in pinned memory.
-struct PreLane {
-  std::unique_ptr<Pipe> p;
-  int state = 0;                           // 0 none, 1 launched, 2 results in
-  hipEvent_t ev_chains = nullptr, ev_done = nullptr;
-  TrialSet S;
-  std::vector<std::pair<uint32_t, uint32_t>> who[3];   // per launched trial: (stream, index in its pre[])
-  std::vector<DiffJob> dj;                 // per launched trial, launch order over the kinds
-  size_t bases[3] = {0, 0, 0};             // kind k's results at bases[k] in launch order
-  PinBuf pres, ppos, pval, pcnt;
-  uint64_t n_launched = 0, n_used = 0;
-  // the launches after the bucket tables run on a thread of their own: uploads from pageable memory wait
-  // for the lane's earlier kernels, which the pipe's rounds must not
-  std::thread th;
-  std::atomic<bool> enqueued{false};   // ev_done is recorded
-  int rc = 0;
-  void join() { if (th.joinable()) th.join(); }
-  ~PreLane() {
-    join();
-    if (p) { if (p->st) (void)hipStreamSynchronize(p->st); p->st = nullptr; }   // the owner destroys it
-    if (ev_chains) (void)hipEventDestroy(ev_chains);
-    if (ev_done) (void)hipEventDestroy(ev_done);
-  }
 };
 
 struct atz_ctx {
@@ -608,7 +558,6 @@ struct atz_ctx {
     std::atomic<size_t> published{0};     // streams published to the sweep so far (round_target)
   } sched;
   std::vector<std::unique_ptr<Pipe>> pipes;
-  std::vector<std::unique_ptr<PreLane>> lanes;   // per pipe (destroyed before the pipes: declared after)
   std::vector<std::unique_ptr<DBuf>> slabs;   // inflated records, one allocation per scan piece
   size_t pipes_running = 1;
   std::atomic<bool> sweep_abort{false};   // the pipes stop at their next round (a withdrawn speculative scan)
@@ -633,14 +582,14 @@ struct atz_ctx {
 
 // kind: 0 trial, 1 inflate, 2 chains, 3 other, 4 match tables
 template <class C>
-static void kbeg(C* c, int kind) {
+static void kbeg(C* c, int kind, hipStream_t st = nullptr) {
   hipEvent_t a = c->kt.get(), b = c->kt.get();
-  (void)hipEventRecord(a, c->st);
+  (void)hipEventRecord(a, st ? st : c->st);
   c->kt.pending.push_back({a, b});
   c->kt.kind.push_back(kind);
 }
 template <class C>
-static void kend(C* c) { (void)hipEventRecord(c->kt.pending.back().second, c->st); }
+static void kend(C* c, hipStream_t st = nullptr) { (void)hipEventRecord(c->kt.pending.back().second, st ? st : c->st); }
 // after a stream synchronisation: fold elapsed times into the stats
 template <class C>
 static void kcollect(C* c) {
@@ -871,6 +820,9 @@ struct ScanState {
   uint64_t max_records() const { return cands.size() + chunks.size() + 1; }
 };
 
+static uint64_t arena_cap_for(uint64_t scanned) {
+  return std::min<uint64_t>(64ull << 30, std::max<uint64_t>(1ull << 30, 8 * scanned));
+}
 static int scan_plan(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64_t F, ScanState& S) {
   auto tm_ = std::chrono::steady_clock::now();
   const uint64_t cs = c->o.chunksize;
@@ -955,8 +907,9 @@ static int scan_plan(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64
   S.need_more = false;
   S.pd = ScanPend{};
   // a slot (ARENA_SLOT) is claimed at a candidate's first flush (4 KiB of output): room for a slot
-  // per ~64 input bytes, capped -- slots are only written as far as the output goes
-  S.arena_cap = std::min<uint64_t>(64ull << 30, std::max<uint64_t>(1ull << 30, 16 * F));
+  // per 8 KiB of input (C4: 6.5 GB of slots for 1 GB), capped; a candidate that finds the arena full
+  // keeps no output and is inflated again if it becomes a record (n_reinflated)
+  S.arena_cap = arena_cap_for(F);
   c->stats.n_candidates = S.cands.size();
   TMARK("scan: candidates");
   return 0;
@@ -1480,6 +1433,7 @@ static int build_bucket_jobs(atz_ctx* x, Pipe* c, ChainBufs& B, std::vector<Chai
 static void forget_tmp_chains(atz_ctx* x, Pipe* c) {
   for (auto& q : c->tmp_chains) x->chain_off[q.first][q.second] = ~0ull;
   c->tmp_chains.clear();
+  c->chains_next = 0;
 }
 static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need, ChainBufs& B) {
   auto bytes = [&](uint32_t s) { return 8 * ((x->recs[s].infl_len + 63) & ~63ull); };
@@ -1511,9 +1465,11 @@ static int ensure_chains_on(atz_ctx* x, Pipe* c, const std::vector<std::pair<uin
     c->diag_builds++;
   }
   if (jobs.empty()) return 0;
-  if (!tmp.empty()) {   // the round's own tables: d_chains is free (the pipe's earlier rounds are done)
-    if (int r = c->d_chains.reserve(tmp_bytes + 4096)) return r;
-    const uint64_t base = (uint64_t)(uintptr_t)c->d_chains.p >> 2;
+  if (!tmp.empty()) {   // the round's own tables (the pipe's earlier rounds are done with these buffers)
+    if (c->chains_next == c->d_chains.size()) c->d_chains.emplace_back(new DBuf());
+    DBuf& tb = *c->d_chains[c->chains_next++];
+    if (int r = tb.reserve(tmp_bytes + 4096)) return r;
+    const uint64_t base = (uint64_t)(uintptr_t)tb.p >> 2;
     for (size_t k : tmp) {
       jobs[k].chain_off += base;
       x->chain_off[(uint32_t)(jobs[k].dslot / 10)][jobs[k].memlevel] = jobs[k].chain_off;
@@ -1696,10 +1652,49 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
   S.base = 0;
 }
 // the trial kernels over h[0, cnt) (one kind, multi-wave ones first), at slots [base, base + cnt)
+static bool kstreams_on() {
+  static const bool v = [] { const char* e = std::getenv("ATZ_KSTREAMS"); return e && std::atoi(e) != 0; }();
+  return v;
+}
+// The stream kind k's trial launches go to (ATZ_KSTREAMS: fast and slow levels forked off the pipe's
+// stream after everything enqueued so far, i.e. their tables); trials_join puts the pipe's stream after them.
+static hipStream_t trials_fork(Pipe* c, int k) {
+  if (!kstreams_on() || k == 0) return c->st;
+  const int i = k - 1;
+  if (!c->kst[i]) {
+    if (hipStreamCreateWithFlags(&c->kst[i], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+    if (!c->ev_fork && hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+  }
+  if (hipEventRecord(c->ev_fork, c->st) != hipSuccess || hipStreamWaitEvent(c->kst[i], c->ev_fork, 0) != hipSuccess)
+    return nullptr;
+  c->joined[i] = false;
+  return c->kst[i];
+}
+static int trials_join(Pipe* c) {
+  for (int i = 0; i < 2; i++) {
+    if (c->joined[i]) continue;
+    HIPCHK(hipEventRecord(c->ev_join[i], c->kst[i]));
+    HIPCHK(hipStreamWaitEvent(c->st, c->ev_join[i], 0));
+    c->joined[i] = true;
+  }
+  return 0;
+}
 static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepOpts& so, int k, const Trial* h,
                          size_t cnt, size_t base) {
+  // the trial descriptors first (on the pipe's stream), then the launches, forked for kinds 1-2
+  for (size_t i = 0; i < cnt;) {
+    const bool mw = mw_trial(k, h[i].memlevel);
+    size_t j = i + 1;
+    while (j < cnt && mw_trial(k, h[j].memlevel) == mw) j++;
+    HIPCHK(pipe_copy(c, c->d_trials.as<Trial>() + base + i, h + i, (j - i) * sizeof(Trial), hipMemcpyHostToDevice));
+    i = j;
+  }
+  const hipStream_t ls = trials_fork(c, k);
+  if (!ls) return ATZ_E_HIP;
   auto launch1 = [&](const Trial* hh, size_t n1, size_t b1, bool mw) -> int {
-    HIPCHK(pipe_copy(c, c->d_trials.as<Trial>() + b1, hh, n1 * sizeof(Trial), hipMemcpyHostToDevice));
+    (void)hh;
     SweepArgs A;
     A.file = d_cmp; A.infl = INFL_BASE; A.chains = CHAIN_BASE;
     A.R = c->d_R.as<uint2>();
@@ -1707,13 +1702,13 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
     A.res = c->d_tres.as<TrialRes>() + b1; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
     A.adler = x->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)n1;
     dim3 g((uint32_t)n1), b(mw ? MW_THREADS : 64);
-    kbeg(c, 0);
-    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
-    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw<BITMAP_BITS>, g, b, 0, c->st, A);
-    else if (k == 1) hipLaunchKernelGGL(k_trial_fast<BITMAP_BITS>, g, b, 0, c->st, A);
-    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, 0, c->st, A);
-    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
-    kend(c);
+    kbeg(c, 0, ls);
+    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, ls, A);
+    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw<BITMAP_BITS>, g, b, 0, ls, A);
+    else if (k == 1) hipLaunchKernelGGL(k_trial_fast<BITMAP_BITS>, g, b, 0, ls, A);
+    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, 0, ls, A);
+    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, ls, A);
+    kend(c, ls);
     KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
     return 0;
   };
@@ -1769,7 +1764,7 @@ static int trials_first_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialS
     base += tr[k].size();
   }
   S.base = base;
-  return 0;
+  return trials_join(c);
 }
 // First pass: match-table prefixes, every trial once, results read back.  Chain tables must exist.
 static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, const SweepOpts& so) {
@@ -1820,6 +1815,7 @@ static int trials_rerun(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, 
     rr[k].resize(again[k].size());
     base += again[k].size();
   }
+  if (int r = trials_join(c)) return r;
   for (int k = 1; k < 3; k++)
     if (!again[k].empty())
       HIPCHK(pipe_copy(c, rr[k].data(), c->d_tres.as<TrialRes>() + bases[k], again[k].size() * sizeof(TrialRes), hipMemcpyDeviceToHost));
@@ -2081,176 +2077,6 @@ static void account_trial(atz_ctx* x, Pipe* c, int k, const Trial& t, const Tria
                                   : x->recs[t.stream].infl_len + (r.out_len < C ? r.out_len : C);
   if (timing_level() >= 3 && !(t.mode & 128)) c->diag_rt.push_back({r.rt0, r.rt1});
 }
-// the kernel counters of `from` (a pre-run lane's) added to `to`'s, and cleared
-static void fold_kernel_stats(atz_stats_t& to, atz_stats_t& from) {
-  to.k_trial_ms += from.k_trial_ms; to.k_chains_ms += from.k_chains_ms; to.k_other_ms += from.k_other_ms;
-  to.k_match_ms += from.k_match_ms; to.k_trial_launches += from.k_trial_launches;
-  to.k_chains_launches += from.k_chains_launches; to.k_match_launches += from.k_match_launches;
-  to.k_chains_alg_bytes += from.k_chains_alg_bytes; to.k_match_positions += from.k_match_positions;
-  from = atz_stats_t{};
-}
-
-// Pre-runs.  A multi-block stream's first block names its memLevel (k_inflate's hint), and its header
-// names its clevel group, so the trials of that group at that memLevel hold the stream's likely
-// winner.  When they sit deep in the stream's list (index >= ATZ_PRERUN, default 8: FLEVEL 1 streams
-// at memLevel <= 6, FLEVEL 3 at <= 5 ...), the rounds reach them late, and they are the round's slowest
-// trials there (whole-stream parses at small memLevels: many blocks, many fast-level chain walks), which
-// every round waits for.  So each pipe runs them at the start of its sweep on its second HIP stream,
-// beside the rounds (a pre-run lane), and the rule walk uses their results when it gets there.  A
-// pre-run is the same trial: whole match table, no symbol saving or replay, best ident the eligibility
-// floor (elig_floor; 0 for atz_sweep's exact idents), so its result is the one the trial would give at
-// its turn -- a "cannot beat" stop under a lower best ident also cannot beat the higher one the stream
-// has by then -- and its mismatch list is extracted on the device whenever it can become the stream's
-// recompression.  A stream whose next trial is a pre-run still in flight waits a round.
-static uint32_t prerun_min() {
-  static const uint32_t v = [] { const char* e = std::getenv("ATZ_PRERUN"); return e ? (uint32_t)std::max(0, std::atoi(e)) : 0u; }();
-  return v;
-}
-static bool prerun_group(int type, int clevel) {   // the clevels of a header's FLEVEL (Z/deflate.c:748-755)
-  switch (type & 3) {
-    case 0: return clevel <= 1;
-    case 1: return clevel >= 2 && clevel <= 5;
-    case 2: return clevel == 6;
-    default: return clevel >= 7;
-  }
-}
-// prelane_launch's second half, on the lane's thread: the match tables, the trials, their mismatch lists
-// and the read-backs into pinned memory, then ev_done.
-static int prelane_enqueue(atz_ctx* x, PreLane& L, Pipe* lp, const uint8_t* d_file, const SweepOpts& so,
-                           std::vector<Trial>* in, std::vector<std::pair<uint32_t, uint32_t>>* win, size_t nt) {
-  trials_order(x, in, L.S);
-  if (int r = trials_first_launch(x, lp, d_file, L.S, so, L.bases)) return r;
-  // per launched trial (launch order): who it is, and its mismatch-list job
-  L.dj.assign(nt, DiffJob{});
-  uint64_t dpos = 0;
-  for (int k = 0; k < 3; k++) {
-    L.who[k].resize(L.S.tr[k].size());
-    for (size_t q = 0; q < L.S.tr[k].size(); q++) {
-      const Trial& t = L.S.tr[k][q];
-      L.who[k][q] = win[k][L.S.perm[k][q]];
-      DiffJob& d = L.dj[L.bases[k] + q];
-      d.out_off = t.out_off; d.orig_off = x->recs[t.stream].offset; d.comp_len = x->recs[t.stream].comp_len;
-      d.dst = dpos; d.cap = std::min<uint64_t>(d.comp_len, x->o.recomp_tresh);
-      dpos += d.cap;
-    }
-  }
-  if (int r = upload(lp, lp->d_diffjobs, L.dj.data(), nt * sizeof(DiffJob))) return r;
-  if (int r = lp->d_diffpos.reserve(dpos * 4 + 64)) return r;
-  if (int r = lp->d_diffval.reserve(dpos + 64)) return r;
-  if (int r = lp->d_diffcnt.reserve(nt * 8 + 64)) return r;
-  kbeg(lp, 3);
-  hipLaunchKernelGGL(k_diffs_pre, dim3((uint32_t)nt), dim3(64), 0, lp->st, lp->d_out.as<uint8_t>(), d_file,
-                     lp->d_diffjobs.as<DiffJob>(), lp->d_tres.as<TrialRes>(), x->o.recomp_tresh,
-                     lp->d_diffpos.as<uint32_t>(), lp->d_diffval.as<uint8_t>(), lp->d_diffcnt.as<uint64_t>(), (uint32_t)nt);
-  kend(lp);
-  {
-    Pipe* c = lp;   // (KCHECK's stream)
-    KCHECK("k_diffs_pre");
-  }
-  if (int r = L.pres.reserve(nt * sizeof(TrialRes) + 64)) return r;
-  if (int r = L.ppos.reserve(dpos * 4 + 64)) return r;
-  if (int r = L.pval.reserve(dpos + 64)) return r;
-  if (int r = L.pcnt.reserve(nt * 8 + 64)) return r;
-  HIPCHK(hipMemcpyAsync(L.pres.p, lp->d_tres.p, nt * sizeof(TrialRes), hipMemcpyDeviceToHost, lp->st));
-  if (dpos) {
-    HIPCHK(hipMemcpyAsync(L.ppos.p, lp->d_diffpos.p, dpos * 4, hipMemcpyDeviceToHost, lp->st));
-    HIPCHK(hipMemcpyAsync(L.pval.p, lp->d_diffval.p, dpos, hipMemcpyDeviceToHost, lp->st));
-  }
-  HIPCHK(hipMemcpyAsync(L.pcnt.p, lp->d_diffcnt.p, nt * 8, hipMemcpyDeviceToHost, lp->st));
-  HIPCHK(hipEventRecord(L.ev_done, lp->st));
-  return 0;
-}
-static int prelane_launch(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<StreamState>& ss,
-                          const std::vector<uint32_t>& batch, const SweepOpts& so) {
-  PreLane& L = *x->lanes[(size_t)c->id];
-  L.state = 0; L.n_launched = L.n_used = 0;
-  const uint32_t pmin = prerun_min();
-  if (!pmin || x->o.recomp_tresh > 4096) return 0;   // (mismatch lists of at most recomp_tresh entries each)
-  Pipe* lp = L.p.get();
-  HIPCHK(hipStreamSynchronize(lp->st));
-  std::vector<Trial> in[3];
-  std::vector<std::pair<uint32_t, uint32_t>> win[3];
-  std::vector<std::pair<uint32_t, int>> need;
-  uint64_t out_tot = 0, sym_tot = 0;
-  for (uint32_t s : batch) {
-    StreamState& st = ss[s];
-    st.pre.clear();
-    const uint32_t m = x->recs[s].mhint;
-    const uint64_t n = x->recs[s].infl_len;
-    if (!m || st.phase != 0 || st.idx != 0 || n >= (1ull << 31)) continue;
-    const std::vector<uint32_t>& l = *st.list;
-    for (uint32_t i = pmin; i < l.size(); i++) {
-      const int cl = (int)(l[i] >> 16), w = (int)((l[i] >> 8) & 0xff), mm = (int)(l[i] & 0xff);
-      if ((uint32_t)mm != m || !prerun_group(x->recs[s].type, cl)) continue;
-      const int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
-      Trial t{};
-      t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)mm;
-      t.mode = 2;   // host-only: whole match table (no rerun)
-      t.best_ident = elig_floor(x, x->recs[s].comp_len);
-      t.out_off = out_tot; t.out_cap = bound(n, w, mm) + 64;
-      out_tot += (t.out_cap + 255) & ~255ull;
-      const uint64_t sw = sym_words(kind, (uint32_t)mm, n);
-      t.sym_off = sym_tot; sym_tot += sw;
-      PreRun pr;
-      pr.idx = i; pr.c = (uint8_t)cl; pr.w = (uint8_t)w; pr.m = (uint8_t)mm;
-      win[kind].push_back({s, (uint32_t)st.pre.size()});
-      st.pre.push_back(std::move(pr));
-      in[kind].push_back(t);
-      if (kind) need.push_back({s, mm});
-    }
-  }
-  const size_t nt = in[0].size() + in[1].size() + in[2].size();
-  if (!nt) return 0;
-  if (int r = ensure_chains(x, lp, need)) return r;
-  HIPCHK(hipEventRecord(L.ev_chains, lp->st));   // the rounds' match walks wait for these tables
-  for (int k = 1; k < 3; k++)
-    for (Trial& t : in[k]) t.chain_off = x->chain_off[t.stream][t.memlevel];
-  if (int r = lp->d_out.reserve(out_tot + 4096)) return r;
-  if (int r = lp->d_syms.reserve(sym_tot * 4 + 4096)) return r;
-  L.state = 1;
-  L.n_launched = nt;
-  L.enqueued = false;
-  L.rc = 0;
-  L.th = std::thread([x, &L, lp, d_file, so, in = std::move(in), win = std::move(win), nt]() mutable {
-    if (hipSetDevice(x->dev) != hipSuccess) { L.rc = ATZ_E_HIP; L.enqueued = true; return; }
-    L.rc = prelane_enqueue(x, L, lp, d_file, so, in, win, nt);
-    L.enqueued = true;
-  });
-  return 0;
-}
-// The pre-run results, once in (block: wait for them): into the streams' PreRun entries.
-static int prelane_poll(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, bool block) {
-  PreLane& L = *x->lanes[(size_t)c->id];
-  if (L.state != 1) return 0;
-  if (!block && !L.enqueued.load()) return 0;
-  L.join();
-  if (L.rc) { L.state = 0; return L.rc; }
-  const hipError_t e = block ? hipEventSynchronize(L.ev_done) : hipEventQuery(L.ev_done);
-  if (e == hipErrorNotReady) { (void)hipGetLastError(); return 0; }
-  HIPCHK(e);
-  Pipe* lp = L.p.get();
-  kcollect(lp);
-  fold_kernel_stats(c->stats, lp->stats);
-  const TrialRes* R = L.pres.as<TrialRes>();
-  const uint32_t* pos = L.ppos.as<uint32_t>();
-  const uint8_t* val = L.pval.as<uint8_t>();
-  const uint64_t* cnt = L.pcnt.as<uint64_t>();
-  for (int k = 0; k < 3; k++)
-    for (size_t q = 0; q < L.S.tr[k].size(); q++) {
-      const size_t g = L.bases[k] + q;
-      PreRun& pr = ss[L.who[k][q].first].pre[L.who[k][q].second];
-      pr.r = R[g];
-      if (pr.r.state == TR_NEED_R || cnt[g] > L.dj[g].cap) return ATZ_E_INTERNAL;   // whole tables: never
-      pr.pos.assign(pos + L.dj[g].dst, pos + L.dj[g].dst + cnt[g]);
-      pr.val.assign(val + L.dj[g].dst, val + L.dj[g].dst + cnt[g]);
-      pr.ready = true;
-      account_trial(x, c, k, L.S.tr[k][q], pr.r);
-    }
-  forget_tmp_chains(x, lp);
-  L.state = 2;
-  return 0;
-}
-
 // One round of pipe c over its batch `active`: the next K list entries of every stream (speculatively:
 // a stream that stops at its j-th trial discards the results of the later ones), K sized so the rounds
 // fill the GPU.  Results are applied per stream strictly in list order, so the outcome is the
@@ -2280,8 +2106,7 @@ struct Round {
   struct PendDiff { bool live = false; DiffJob d{}; };
   std::vector<PendDiff> pend;      // a stream's live diff job: its latest improvement within recomp_tresh
   std::vector<uint32_t> jpos;      // where each stream's rule walk resumes
-  std::vector<const PreRun*> vir;  // mine entries of kind 3: list entries whose pre-run result is in
-  uint64_t ntr = 0, nsc = 0, nhz = 0, nspec = 0, npre = 0;
+  uint64_t ntr = 0, nsc = 0, nhz = 0, nspec = 0;
 
   Round(atz_ctx* x_, Pipe* c_, const uint8_t* f, std::vector<StreamState>& ss_, const SweepOpts& so_,
         std::vector<uint32_t>& a_, std::vector<uint32_t>& w_)
@@ -2295,17 +2120,6 @@ struct Round {
 
   // The trials of the next K list entries of every stream, within the round's scratch budget.
   void build_lists() {
-    // a stream whose next trial is a pre-run still in flight waits for the next round
-    if (x->lanes[(size_t)c->id]->state == 1) {
-      size_t keep = 0;
-      for (size_t a = 0; a < active.size(); a++) {
-        const PreRun* pr = ss[active[a]].pre_at(ss[active[a]].idx);
-        if (pr && !pr->ready) waiting.push_back(active[a]);
-        else active[keep++] = active[a];
-      }
-      active.resize(keep);
-    }
-    if (active.empty()) { mbeg.assign(1, 0); return; }
     K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, round_target(x) / active.size()));
     mbeg.assign(active.size() + 1, 0);
     mine.reserve(active.size() * K);
@@ -2323,12 +2137,6 @@ struct Round {
         break;
       }
       for (uint32_t j = 0; j < K && st.idx + j < st.list->size(); j++) {
-        if (const PreRun* pr = st.pre_at(st.idx + j)) {   // run ahead: its result, when in
-          if (!pr->ready) break;
-          mine.push_back({3, (uint32_t)vir.size()});
-          vir.push_back(pr);
-          continue;
-        }
         const uint32_t p = (*st.list)[st.idx + j];
         const int cl = (int)(p >> 16), w = (int)((p >> 8) & 0xff), m = (int)(p & 0xff);
         Trial t{};
@@ -2361,10 +2169,35 @@ struct Round {
   // Replays first (they need the pairs' bucket depths only), duplicates, the eligibility floor, then the
   // bucket tables the other trials read (stream-ordered before the match walks: no sync).
   int plan() {
-    PreLane& L = *x->lanes[(size_t)c->id];
-    if (L.state == 1) HIPCHK(hipStreamWaitEvent(c->st, L.ev_chains, 0));   // tables the lane registered
     if (replay_on() && x->depth_pin.p) {
-      if (int r = ensure_depths(x, c, need, need_b)) return r;
+      // Replay planning reads the pairs' deepest buckets.  A trial that can only parse (its stream has no
+      // saved sequence at its (level, window) to replay, nor a higher level's run to duplicate) needs its
+      // table whatever the plan, and the table's build yields the depth: those pairs are built now, and
+      // only the others get a depth pass first (k_bucket_depth), to spare the tables of trials that
+      // will replay.  (Round 1 of a sweep has no saved sequences: no depth passes at all.)
+      std::vector<std::pair<uint32_t, int>> dfirst, direct;
+      std::vector<uint32_t> dfirst_b;
+      for (int k = 1; k < 3; k++)
+        for (const Trial& t : tr[k]) {
+          const StreamState& st = ss[t.stream];
+          bool maybe = false;
+          if (st.rp >= 0) {
+            const RpEntry& e = x->rp_pool[st.rp][t.clevel - 1];
+            maybe = e.state == 2 && e.window == t.window;
+          }
+          if (!maybe && k == 2 && t.clevel >= 7)
+            for (const auto& r : st.xl) maybe |= r[0] == t.window && r[1] == t.memlevel && r[2] > t.clevel;
+          static const bool all_first = [] { const char* e = std::getenv("ATZ_DFIRST"); return e && std::atoi(e) == 0; }();
+          if (maybe || all_first) {
+            dfirst.push_back({t.stream, (int)t.memlevel});
+            dfirst_b.push_back((uint32_t)(c_cfg_host(t.clevel) >> (k == 1 ? 0 : 2)));
+          } else {
+            direct.push_back({t.stream, (int)t.memlevel});
+          }
+        }
+      for (auto& q : direct) nbuild += x->chain_off[q.first][q.second] == ~0ull;
+      if (int r = ensure_depths(x, c, dfirst, dfirst_b)) return r;
+      if (int r = ensure_chains(x, c, direct)) return r;
       HIPCHK(pipe_sync(c));
       if (dedup_on()) level_dups(x, ss, tr[2]);
       for (int k = 1; k < 3; k++) plan_replay(x, c, ss, k, tr[k], savers);
@@ -2377,7 +2210,7 @@ struct Round {
       for (Trial& t : tr[k])
         if (!(t.mode & 4)) t.best_ident = std::max(t.best_ident, elig_floor(x, x->recs[t.stream].comp_len));
     for (auto& q : need) nbuild += x->chain_off[q.first][q.second] == ~0ull;
-    if (int r = ensure_chains(x, c, need)) return r;
+    if (int r = ensure_chains(x, c, need)) return r;   // (stream-ordered before the match walks: no sync)
     for (int k = 1; k < 3; k++)
       for (Trial& t : tr[k]) {
         const uint64_t off = x->chain_off[t.stream][t.memlevel];
@@ -2478,11 +2311,8 @@ struct Round {
     held[a] = 0;
     for (uint32_t j = jpos[a]; j < mbeg[a + 1]; j++) {
       if (st.phase != phase0) { nspec += mbeg[a + 1] - j; break; }   // stopped earlier this round
-      const bool virt = mine[j].first == 3;
-      const PreRun* pr = virt ? vir[mine[j].second] : nullptr;
-      const Trial* tp = virt ? nullptr : &tr[mine[j].first][mine[j].second];
-      const TrialRes& r = virt ? pr->r : trres[mine[j].first][mine[j].second];
-      npre += virt;
+      const Trial& t = tr[mine[j].first][mine[j].second];
+      const TrialRes& r = trres[mine[j].first][mine[j].second];
       if (r.state == TR_NEED_R) {
         if (!defer) return ATZ_E_INTERNAL;   // every rerun a walk waits for has run
         jpos[a] = j;
@@ -2497,8 +2327,7 @@ struct Round {
       bool fullmatch = false;
       if (r.state == TR_FULL && r.ident > st.ident) {
         st.ident = r.ident;
-        if (virt) { st.c = pr->c; st.w = pr->w; st.m = pr->m; }
-        else { st.c = tp->clevel; st.w = tp->window; st.m = tp->memlevel; }
+        st.c = t.clevel; st.w = t.window; st.m = t.memlevel;
         st.first_diff = -1;
         st.rawdiff.clear(); st.diffval.clear();
         pend[a].live = false;   // an earlier improvement's diffs are superseded
@@ -2506,16 +2335,10 @@ struct Round {
         else {
           if (r.ident + x->o.mismatch_tol >= C) fullmatch = true;
           if (C - r.ident <= x->o.recomp_tresh) {     // diffs are only ever written for recomp streams
-            if (virt) {   // extracted by the lane (k_diffs_pre)
-              if (pr->pos.size() != C - r.ident) return ATZ_E_INTERNAL;
-              st.rawdiff = pr->pos; st.diffval = pr->val;
-              st.first_diff = st.rawdiff.empty() ? -1 : (int64_t)st.rawdiff[0];
-            } else {
-              DiffJob& d = pend[a].d;
-              d.out_off = tp->out_off; d.out_len = r.out_len; d.orig_off = x->recs[s].offset;
-              d.comp_len = C; d.dst = 0; d.cap = C - r.ident;
-              pend[a].live = true;
-            }
+            DiffJob& d = pend[a].d;
+            d.out_off = t.out_off; d.out_len = r.out_len; d.orig_off = x->recs[s].offset;
+            d.comp_len = C; d.dst = 0; d.cap = C - r.ident;
+            pend[a].live = true;
           }
         }
       }
@@ -2566,6 +2389,21 @@ struct Round {
       }
     settle(true);
     return 0;
+  }
+
+  // The bucket tables of the streams this round finished go back to the cache's free lists (no kernel
+  // reads them any more).
+  void release_done() {
+    for (uint32_t s : active) {
+      if (ss[s].phase != 2) continue;
+      const uint64_t bytes = 8 * ((x->recs[s].infl_len + 63) & ~63ull);
+      for (int m = 1; m <= 9; m++) {
+        uint64_t& off = x->chain_off[s][m];
+        if (off == ~0ull) continue;
+        if (x->chain_arena.holds(off << 2, bytes)) x->chain_arena.release(off << 2, bytes);
+        off = ~0ull;
+      }
+    }
   }
 
   // Mismatch lists (main.cpp:699-714) of the live diff jobs, from the trials' outputs.
@@ -2664,19 +2502,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
   std::vector<uint32_t> active;
   const SweepOpts so{x->o.recomp_tresh, x->o.sizediff_tresh, x->o.shortcut_len, x->o.mismatch_tol};
   uint64_t rounds = 0;
-  PreLane& L = *x->lanes[(size_t)c->id];
-  struct LaneDrain {   // nothing of the lane stays in flight past the sweep (its buffers serve the next one)
-    PreLane& L;
-    ~LaneDrain() { L.join(); if (L.state == 1) (void)hipStreamSynchronize(L.p->st); }
-  } drain{L};
-  L.state = 0;
-  bool first = true;
   while (sched_take(x, c->id, active)) {
-    if (first) {   // the pipe's first batch is all its streams published so far
-      first = false;
-      if (int r = prelane_launch(x, c, d_file, ss, active, so)) return r;
-    }
-    if (int r = prelane_poll(x, c, ss, false)) return r;
     rounds++;
     std::vector<uint32_t> waiting;
     struct Give {   // the batch goes back on every exit from the round (an error aborts the sweep anyway)
@@ -2686,11 +2512,6 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     Round R(x, c, d_file, ss, so, active, waiting);
     const auto tl0 = std::chrono::steady_clock::now();
     R.build_lists();
-    if (active.empty()) {   // every stream waits for the pre-run lane
-      rounds--;
-      if (int r = prelane_poll(x, c, ss, true)) return r;
-      continue;
-    }
     const auto ta = std::chrono::steady_clock::now();
     if (int r = R.plan()) return r;
     const auto tb = std::chrono::steady_clock::now();
@@ -2698,6 +2519,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     const auto tc = std::chrono::steady_clock::now();
     if (int r = R.apply()) return r;
     if (int r = R.flush_diffs()) return r;
+    R.release_done();
     const auto td = std::chrono::steady_clock::now();
     c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
     c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
@@ -2712,10 +2534,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     c->t_apply += ms_since(tc);
     c->stats.n_trials += R.ntr; c->stats.n_trials_shortcut += R.nsc; c->stats.n_hazard += R.nhz;
     c->stats.n_trials_speculative += R.nspec;
-    L.n_used += R.npre;
   }
-  if (int r = prelane_poll(x, c, ss, true)) return r;
-  c->stats.n_trials_speculative += L.n_launched - L.n_used;   // pre-runs past their stream's stop
   c->stats.n_rounds = rounds;
   c->stats.sweep_ms = ms_since(t0);
   return 0;
@@ -2723,7 +2542,33 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
 
 // Phase 3 driver: streams partitioned over the context's pipes (interleaved, so every pipe gets
 // the same mix of header classes and sizes), one host thread per pipe.
+// ATZ_QMAP=1: the pipes' main streams are created before their second ones, so that (with enough hardware
+// queues) no two pipes share a queue; 0 (default): interleaved, two pipes share one
+static int qmap_mode() {
+  static const int v = [] { const char* e = std::getenv("ATZ_QMAP"); return e ? std::atoi(e) : 0; }();
+  return v;
+}
 static int ensure_pipes(atz_ctx* c, size_t np) {
+  if (qmap_mode() == 1 && c->pipes.size() < np) {   // main streams first (HIP maps streams to queues in turn)
+    std::vector<hipStream_t> mains;
+    for (size_t g = c->pipes.size(); g < np; g++) {
+      hipStream_t st;
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
+      mains.push_back(st);
+    }
+    for (hipStream_t st : mains) {
+      std::unique_ptr<Pipe> p(new Pipe());
+      p->id = (int)c->pipes.size();
+      p->st = st;
+      c->pipes.push_back(std::move(p));
+    }
+    for (size_t g = 0; g < c->pipes.size(); g++) {
+      Pipe* p = c->pipes[g].get();
+      if (p->pst) continue;
+      if (hipStreamCreateWithFlags(&p->pst, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
+    }
+    return 0;
+  }
   while (c->pipes.size() < np) {
     std::unique_ptr<Pipe> p(new Pipe());
     p->id = (int)c->pipes.size();
@@ -2731,16 +2576,7 @@ static int ensure_pipes(atz_ctx* c, size_t np) {
     // the idle second stream (see Pipe::pst): with it two pipes share a hardware queue and their
     // kernels run back to back, so fewer LDS-heavy kernels co-run (measured faster)
     if (hipStreamCreateWithFlags(&p->pst, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
-    // its pre-run lane runs on that stream (prelane_launch)
-    std::unique_ptr<PreLane> L(new PreLane());
-    L->p.reset(new Pipe());
-    L->p->st = p->pst;
-    L->p->id = p->id;
-    if (hipEventCreateWithFlags(&L->ev_chains, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&L->ev_done, hipEventDisableTiming) != hipSuccess)
-      return ATZ_E_HIP;
     c->pipes.push_back(std::move(p));
-    c->lanes.push_back(std::move(L));
   }
   return 0;
 }
@@ -2848,7 +2684,13 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
   for (size_t g = 0; g < R.np; g++)
     R.th.emplace_back([c, &R, &ss, g]() {
       if (hipSetDevice(c->dev) != hipSuccess) { R.rc[g] = ATZ_E_HIP; sched_abort(c); return; }
-      R.rc[g] = sweep_pipe(c, c->pipes[g].get(), R.d_file, ss);
+      try {   // no exception may leave a thread (guarded() covers the calling one)
+        R.rc[g] = sweep_pipe(c, c->pipes[g].get(), R.d_file, ss);
+      } catch (const std::bad_alloc&) {
+        R.rc[g] = ATZ_E_NOMEM;
+      } catch (...) {
+        R.rc[g] = ATZ_E_INTERNAL;
+      }
       if (R.rc[g]) sched_abort(c);   // the other pipes stop too (streams this one held never come back)
     });
   return 0;
@@ -2924,8 +2766,10 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
       p->diag_builds = 0;
       p->diag_need.clear();
     }
-    std::fprintf(stderr, "atz: bucket builds %llu, (stream, memLevel) pairs a table-reading trial used %llu\n",
-                 (unsigned long long)nb, (unsigned long long)nn);
+    std::fprintf(stderr, "atz: bucket builds %llu, (stream, memLevel) pairs a table-reading trial used %llu; bucket cache "
+                 "%.2f GB allocated, %.2f GB served from released tables; saved sequences %.2f GB; device peak %.2f GB\n",
+                 (unsigned long long)nb, (unsigned long long)nn, c->chain_arena.total / 1e9, c->chain_arena.reused / 1e9,
+                 c->rp_arena.total / 1e9, g_dev.peak.load() / 1e9);
   }
   if (timing_level() >= 3) {   // trials running at once over the sweep (first passes only: reruns overwrite)
     std::vector<std::pair<uint32_t, int>> ev;
@@ -2942,9 +2786,10 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
       uint32_t last = t0;
       std::vector<double> bin((size_t)((t1 - t0) / 500000u) + 1, 0.0);   // 5 ms bins (100 MHz clock)
       for (auto& e : ev) {
-        for (uint32_t a = last; a < e.first;) {
-          const uint32_t b = std::min<uint32_t>(e.first, (a / 500000u + 1u) * 500000u);
-          bin[(size_t)((a - t0) / 500000u)] += (double)cur * (b - a);
+        // bins relative to t0, in 64 bits (the next 5 ms boundary of an absolute time near 2^32 would wrap)
+        for (uint64_t a = last - t0; a < (uint64_t)(e.first - t0);) {
+          const uint64_t b = std::min<uint64_t>(e.first - t0, (a / 500000u + 1u) * 500000u);
+          bin[(size_t)(a / 500000u)] += (double)cur * (double)(b - a);
           a = b;
         }
         area += (double)cur * (e.first - last);
@@ -3275,6 +3120,7 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
     for (auto& a2 : c->chain_off) a2.fill(~0ull);
     c->chain_arena.reset(CHAIN_CACHE_CAP);   // the last batch's kernels are done (run_trials synchronised)
     p->tmp_chains.clear();
+    p->chains_next = 0;
     std::vector<std::pair<uint32_t, int>> need;
     for (size_t s = s0; s < s1; s++) if ((params[s] >> 16) > 0) need.push_back({(uint32_t)s, (int)(params[s] & 0xff)});
     if (int r = ensure_chains(c, p, need)) return r;
@@ -3589,6 +3435,8 @@ static int shard_scan_impl(atz_ctx* c, const uint8_t* d_file, const uint8_t* h, 
   if (int r = scan_plan(c, h, d_file, F, S)) return r;
   const uint32_t nch = (uint32_t)S.chunks.size();
   shard_range(nch, rank, world, sh.ja, sh.jb);
+  if (sh.jb > sh.ja)   // the arena holds this rank's candidates only
+    S.arena_cap = arena_cap_for(S.chunks[sh.jb - 1].co + S.chunks[sh.jb - 1].len - S.chunks[sh.ja].co);
   if (int r = scan_inflate(c, h, d_file, S, sh.ja, sh.jb)) return r;
   const size_t k0 = S.cbeg[sh.ja], k1 = S.cbeg[sh.jb];
   blob.assign(SHARD_HDR, 0);

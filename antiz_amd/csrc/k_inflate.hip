@@ -36,6 +36,23 @@ static_assert(INF_RING_SMALL >= 2048 && (INF_RING_SMALL & (INF_RING_SMALL - 1)) 
 #ifndef ATZ_INF_LITRUN
 #define ATZ_INF_LITRUN 1   // fast path: short-code literals in their own tight loop
 #endif
+// The first block's symbol count (the sweep's memLevel hint): bytes produced - sum(length - 1) over its
+// matches.  The decode loop is bound by the CU's one scalar unit, so the per-match add goes to the VALU:
+// 2 (default) a v_add3 into a VGPR, 1 an SGPR add, 0 no hint.  C4 A/B (gpurun_out/pre_f, 2 runs each):
+// k_inflate 75.6 ms with 2, 82.1 with 1, 75.9 with 0.
+#ifndef ATZ_INF_MLS
+#define ATZ_INF_MLS 2
+#endif
+#if ATZ_INF_MLS == 2
+#define MLS_ADD(len) asm volatile("v_add3_u32 %0, %0, %1, -1" : "+v"(mls) : "s"(len))
+#define MLS_GET() ((uint32_t)__builtin_amdgcn_readfirstlane((int)mls))
+#elif ATZ_INF_MLS == 1
+#define MLS_ADD(len) (mls += (len) - 1u)
+#define MLS_GET() mls
+#else
+#define MLS_ADD(len) ((void)0)
+#define MLS_GET() 0x7fffffffu
+#endif
 #ifndef ATZ_INF_CLOCKS
 #define ATZ_INF_CLOCKS 0                       // 1: per-job clocks and symbol counts in InfRes
 #endif
@@ -540,7 +557,9 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
   uint64_t errneed = 0;
   uint32_t errcode = 0;
   uint32_t hint = 0;   // INF_HINT_NOSHORT (see the dynamic header below) | INF_HINT_MLEV
-  uint32_t mls = 0;    // sum of (length - 1) over the block's matches: symbols = bytes - mls
+  // sum of (length - 1) over the block's matches: symbols = bytes - mls.  ATZ_INF_MLS 2 keeps it in a
+  // VGPR (one VALU add per match; the decode loop is bound by the CU's scalar issue), 1 in an SGPR
+  uint32_t mls = 0;
 #define NEEDB(k) do { if (!has(k)) return R_NEED; } while (0)
 #define FAIL(code, needpos) do { errneed = (needpos); errcode = (code); return R_ERR; } while (0)
 
@@ -642,7 +661,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
             nst = 0;
           }
           if ((uint64_t)dist > prod) { used = sym0; redo = true; break; }   // too far back
-          mls += len - 1u;
+          MLS_ADD(len);
           if (!copy_at(len, dist)) { rc = R_RETRY; break; }
           prod += len;
           if (prod - flushed >= FLUSH_AT) flush(false);
@@ -679,7 +698,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
       drop(de);
       stage_flush();
       if ((uint64_t)dist > prod) FAIL(14, pos);            // invalid distance too far back
-      mls += len - 1u;
+      MLS_ADD(len);
       if (!copy(len, dist)) return R_RETRY;
     }
   };
@@ -847,7 +866,7 @@ __global__ __launch_bounds__(64, RING == INF_RING_FULL ? 1 : INF_SMALL_WAVES) vo
           // Sweep hint, part of no output: zlib flushes a block when its symbol buffer is full
           // (_tr_tally, Z/trees.c:1050, Z/deflate.h:328-338), so a first block that is not the last holds exactly
           // lit_bufsize - 1 = 2^(memLevel + 6) - 1 symbols
-          const uint64_t syms = prod + nst - b0 - mls;
+          const uint64_t syms = prod + nst - b0 - MLS_GET();
           if (syms >= 127 && syms <= 32767 && ((syms + 1) & syms) == 0)
             hint |= (uint32_t)(__builtin_ctzll(syms + 1) - 6) << INF_HINT_MLEV_SHIFT;
         }

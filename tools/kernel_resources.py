@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Register, spill, scratch, LDS and occupancy figures of every kernel in libatz_accel, from the
 compiler's own report (hipcc -Rpass-analysis=kernel-resource-usage, gfx950).
-usage: python3 tools/kernel_resources.py [out.txt]   (compiles to a temporary .so; ~40 s)"""
+usage: python3 tools/kernel_resources.py [out.txt]   (compiles to a temporary .so; ~40 s; ATZ_HIPFLAGS: extra flags)"""
 import os
 import re
 import subprocess
@@ -19,7 +19,7 @@ def main():
     with tempfile.TemporaryDirectory() as td:
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-x", "hip",
                "-Wno-unused-result", "-Wno-unused-value", "-Rpass-analysis=kernel-resource-usage", src,
-               "-o", os.path.join(td, "lib.so")]
+               "-o", os.path.join(td, "lib.so")] + os.environ.get("ATZ_HIPFLAGS", "").split()
         r = subprocess.run(cmd, capture_output=True, text=True, check=True)
     rows, cur = [], None
     for line in r.stderr.splitlines():
