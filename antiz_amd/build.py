@@ -35,7 +35,7 @@ def build(force=False, verbose=False):
     srcs.append(os.path.join(os.path.dirname(HERE), "include", "atz_accel.h"))
     if force or _newer(LIB, srcs):
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-x", "hip",
-               "-Wno-unused-result", "-Wno-unused-value",
+               "-Wno-unused-result", "-Wno-unused-value", "-Xarch_host", "-gline-tables-only",
                os.path.join(CSRC, "atz_accel.cpp"), "-o", LIB] + os.environ.get("ATZ_HIPFLAGS", "").split()
         if verbose:
             print(" ".join(cmd))

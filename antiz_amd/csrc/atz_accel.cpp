@@ -36,6 +36,10 @@
 #include <functional>
 #include <unordered_map>
 #include <vector>
+#include <dlfcn.h>
+#include <signal.h>
+#include <sys/time.h>
+#include <ucontext.h>
 
 #include "../../include/atz_accel.h"
 
@@ -196,6 +200,103 @@ struct DevAcct {
 };
 DevAcct g_dev;
 void dev_mark_call() { g_dev.peak.store(g_dev.cur.load()); }
+
+// ATZ_HOSTPROF=<file> (diagnostics): wall-clock sampling of the call's host threads (the caller's and
+// the sweep's pipe threads register themselves): a sampler thread signals each one every 100 us and the
+// handler records the interrupted instruction (a blocked thread's is its system call).  Appended to
+// <file> as "count thread object offset symbol" lines (tools/hostprof.py resolves them).
+struct HostProf {
+  static constexpr size_t MAXS = 1u << 22;
+  static constexpr int MAXT = 64;
+  static std::atomic<size_t>& n() { static std::atomic<size_t> v{0}; return v; }
+  static uint64_t* pcs() { static uint64_t* b = new uint64_t[MAXS]; return b; }
+  static std::atomic<int>& nthr() { static std::atomic<int> v{0}; return v; }
+  static pthread_t* thr() { static pthread_t t[MAXT]; return t; }
+  static std::atomic<bool>& on() { static std::atomic<bool> v{false}; return v; }
+  static int& my_slot() { thread_local int s = -1; return s; }
+  static std::mutex& mu() { static std::mutex m; return m; }   // held while signalling: leave() waits for it
+  static bool* alive() { static bool a[MAXT]; return a; }
+  static void on_sig(int, siginfo_t*, void* uc) {
+    const int slot = my_slot();
+    if (slot < 0) return;
+    const size_t i = n().fetch_add(1, std::memory_order_relaxed);
+    if (i < MAXS) pcs()[i] = (uint64_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RIP] | ((uint64_t)slot << 56);
+  }
+  static void enroll() {   // the calling thread is sampled while a profile runs (until leave())
+    if (!on().load() || my_slot() >= 0) return;
+    std::lock_guard<std::mutex> lk(mu());
+    const int k = nthr().load();
+    if (k >= MAXT) return;
+    thr()[k] = pthread_self();
+    alive()[k] = true;
+    my_slot() = k;
+    nthr().store(k + 1);
+  }
+  static void leave() {
+    if (my_slot() < 0) return;
+    std::lock_guard<std::mutex> lk(mu());
+    alive()[my_slot()] = false;
+    my_slot() = -1;
+  }
+  struct Enroll { Enroll() { enroll(); } ~Enroll() { leave(); } };
+  const char* path = nullptr;
+  std::thread sampler;
+  std::atomic<bool> stop{false};
+  HostProf() {
+    path = std::getenv("ATZ_HOSTPROF");
+    if (!path || !*path) { path = nullptr; return; }
+    pcs();
+    n().store(0);
+    struct sigaction sa{};
+    sa.sa_sigaction = on_sig;
+    sa.sa_flags = SA_SIGINFO | SA_RESTART;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGPROF, &sa, nullptr);
+    {
+      std::lock_guard<std::mutex> lk(mu());
+      nthr().store(0);
+    }
+    on().store(true);
+    enroll();
+    sampler = std::thread([this] {
+      while (!stop.load()) {
+        {
+          std::lock_guard<std::mutex> lk(mu());
+          const int k = std::min(nthr().load(), MAXT);
+          for (int i = 0; i < k; i++)
+            if (alive()[i]) pthread_kill(thr()[i], SIGPROF);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+      }
+    });
+  }
+  ~HostProf() {
+    if (!path) return;
+    stop.store(true);
+    sampler.join();
+    on().store(false);
+    const size_t cnt = std::min(n().load(), MAXS);
+    std::unordered_map<uint64_t, uint64_t> hist;
+    for (size_t i = 0; i < cnt; i++) hist[pcs()[i]]++;
+    FILE* f = std::fopen(path, "a");
+    if (f) {
+      std::fprintf(f, "# call: %zu samples, %d threads\n", cnt, nthr().load());
+      for (const auto& kv : hist) {
+        const uint64_t pc = kv.first & ((1ull << 56) - 1);
+        Dl_info di{};
+        if (dladdr((void*)(uintptr_t)pc, &di) && di.dli_fname)
+          std::fprintf(f, "%llu %d %s 0x%llx %s\n", (unsigned long long)kv.second, (int)(kv.first >> 56), di.dli_fname,
+                       (unsigned long long)(pc - (uint64_t)(uintptr_t)di.dli_fbase), di.dli_sname ? di.dli_sname : "?");
+        else
+          std::fprintf(f, "%llu %d ? 0x%llx ?\n", (unsigned long long)kv.second, (int)(kv.first >> 56), (unsigned long long)pc);
+      }
+      std::fclose(f);
+    }
+    leave();
+    std::lock_guard<std::mutex> lk(mu());
+    nthr().store(0);
+  }
+};
 
 struct DBuf {              // device buffer, freed with its owner (atz_close deletes the context)
   void* p = nullptr;
@@ -468,6 +569,14 @@ struct Pipe {
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   bool joined[2] = {true, true};
   ChainBufs cb;
+  // pinned staging for the pipe's uploads (a pageable hipMemcpyAsync returns only once the stream has
+  // reached it, which would hold the host thread behind every kernel enqueued before it): a bump
+  // allocator that pipe_sync resets, every copy from it being complete then
+  PinBuf stage;
+  size_t stage_used = 0;
+  // match tables of the round: d_R regions handed out in order (Round::plan reserves the round's bound)
+  uint64_t r_next = 0;
+  hipEvent_t ev_built = nullptr;   // after a round's direct bucket builds (their depths: Round::plan)
   // a second stream that stays idle: it only shifts how the process's GPU_MAX_HW_QUEUES (4) hardware
   // queues are shared by the pipes' streams (two pipes then share a queue, which measured faster
   // than every pipe on its own queue: DESIGN.md s3.6)
@@ -479,11 +588,25 @@ struct Pipe {
   uint64_t diag_builds = 0;
   std::vector<std::pair<uint32_t, uint32_t>> diag_rt;   // ATZ_TIMING >= 3: every launched trial's realtime span
   std::vector<uint16_t> diag_need;
+  std::vector<uint32_t> slot;   // per stream of the current round: its index in the round's batch
   int id = 0;
   // diagnostics (ATZ_TIMING): host phase times, per trial kind x level counters; time in HIP copy calls
   // (host -> device uploads and result downloads) and in stream synchronisations
   double t_list = 0, t_chains = 0, t_trials = 0, t_apply = 0, t_copy = 0, t_sync = 0;
   uint64_t n_copy = 0, n_sync = 0;
+  // host time per phase of a round (lap), and the part of it spent waiting in copies / synchronisations
+  static constexpr int NPH = 13;
+  double ph[NPH] = {}, ph_wait[NPH] = {};
+  std::chrono::steady_clock::time_point lap_t;
+  double lap_w = 0;
+  void lap_start() { lap_t = std::chrono::steady_clock::now(); lap_w = t_copy + t_sync; }
+  void lap(int i) {
+    const auto n = std::chrono::steady_clock::now();
+    ph[i] += std::chrono::duration<double, std::milli>(n - lap_t).count();
+    ph_wait[i] += t_copy + t_sync - lap_w;
+    lap_t = n;
+    lap_w = t_copy + t_sync;
+  }
   uint64_t kind[3][10][14] = {};
   ~Pipe() {
     for (int i = 0; i < 2; i++) {
@@ -491,6 +614,7 @@ struct Pipe {
       if (ev_join[i]) hipEventDestroy(ev_join[i]);
     }
     if (ev_fork) hipEventDestroy(ev_fork);
+    if (ev_built) hipEventDestroy(ev_built);
     if (pst) { hipStreamSynchronize(pst); hipStreamDestroy(pst); }
     if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
     for (hipEvent_t e : kt.pool) hipEventDestroy(e);
@@ -613,10 +737,28 @@ static void kcollect(C* c) {
 // copy n host bytes into b (device capacity n + slack; the slack is never read from the host)
 template <class C> static void copy_timed(C*, double) {}
 template <> void copy_timed<Pipe>(Pipe* p, double ms) { p->t_copy += ms; p->n_copy++; }
+// The source of a host -> device upload: a pipe's copies go through its pinned staging (ATZ_STAGE=0: not),
+// the context's straight from the caller's memory.  (A full staging buffer falls back to the latter.)
+static bool stage_on() {
+  static const bool v = [] { const char* e = std::getenv("ATZ_STAGE"); return !e || std::atoi(e) != 0; }();
+  return v;
+}
+static constexpr size_t STAGE_BYTES = 32u << 20;
+template <class C> static const void* staged(C*, const void* h, size_t) { return h; }
+template <> const void* staged<Pipe>(Pipe* p, const void* h, size_t n) {
+  if (!stage_on() || !n) return h;
+  if (!p->stage.p && p->stage.reserve(STAGE_BYTES)) return h;
+  const size_t a = (p->stage_used + 255) & ~(size_t)255;
+  if (a + n > p->stage.n) return h;
+  std::memcpy(static_cast<uint8_t*>(p->stage.p) + a, h, n);
+  p->stage_used = a + n;
+  return static_cast<uint8_t*>(p->stage.p) + a;
+}
 // a pipe's stream synchronisation, timed (ATZ_TIMING)
 static hipError_t pipe_sync(Pipe* p) {
   const auto t = std::chrono::steady_clock::now();
   const hipError_t e = hipStreamSynchronize(p->st);
+  if (e == hipSuccess) p->stage_used = 0;   // every staged copy has run
   p->t_sync += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
   p->n_sync++;
   return e;
@@ -624,6 +766,7 @@ static hipError_t pipe_sync(Pipe* p) {
 // a pipe's copy to or from the host, timed (ATZ_TIMING)
 static hipError_t pipe_copy(Pipe* p, void* dst, const void* src, size_t n, hipMemcpyKind k) {
   const auto t = std::chrono::steady_clock::now();
+  if (k == hipMemcpyHostToDevice) src = staged(p, src, n);
   const hipError_t e = hipMemcpyAsync(dst, src, n, k, p->st);
   copy_timed(p, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count());
   return e;
@@ -632,7 +775,7 @@ template <class C>
 static int upload(C* c, DBuf& b, const void* h, size_t n, size_t slack = 4096) {
   if (int r = b.reserve(n + slack)) return r;
   const auto t = std::chrono::steady_clock::now();
-  if (n) HIPCHK(hipMemcpyAsync(b.p, h, n, hipMemcpyHostToDevice, c->st));
+  if (n) HIPCHK(hipMemcpyAsync(b.p, staged(c, h, n), n, hipMemcpyHostToDevice, c->st));
   copy_timed(c, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count());
   return 0;
 }
@@ -1634,17 +1777,28 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
   for (int k = 0; k < 3; k++) {
     const size_t n = in[k].size();
     S.perm[k].resize(n);
+    // one 64-bit key per trial, sorted descending: multi-wave bit, expected work (< 2^38), then the
+    // index complemented (ties keep the caller's order, as a stable sort would)
     std::vector<uint64_t> key(n);
+    const uint32_t mwm = mw_max_memlevel();
+    const bool packed = n < (1u << 20);
     for (size_t q = 0; q < n; q++) {
       const Trial& t = in[k][q];
-      key[q] = x->recs[t.stream].infl_len * (uint64_t)(k == 1 ? 3 : 1) * (uint64_t)(10 - t.memlevel) *
-               (uint64_t)((t.mode & 8) ? 1 : 4);   // replays skip the match walks
+      const uint64_t w = x->recs[t.stream].infl_len * (uint64_t)(k == 1 ? 3 : 1) * (uint64_t)(10 - t.memlevel) *
+                         (uint64_t)((t.mode & 8) ? 1 : 4);   // replays skip the match walks
+      const uint64_t mw = k != 0 && t.memlevel <= mwm;
+      key[q] = packed ? (mw << 63) | (std::min<uint64_t>(w, (1ull << 42) - 1) << 20) | ((1u << 20) - 1 - q) : w;
       S.perm[k][q] = (uint32_t)q;
     }
-    std::stable_sort(S.perm[k].begin(), S.perm[k].end(), [&](uint32_t a, uint32_t b) {
-      const bool ma = mw_trial(k, in[k][a].memlevel), mb = mw_trial(k, in[k][b].memlevel);
-      return ma != mb ? ma : key[a] > key[b];
-    });
+    if (packed) {
+      std::sort(key.begin(), key.end(), std::greater<uint64_t>());
+      for (size_t q = 0; q < n; q++) S.perm[k][q] = (uint32_t)((1u << 20) - 1 - (key[q] & ((1u << 20) - 1)));
+    } else {
+      std::stable_sort(S.perm[k].begin(), S.perm[k].end(), [&](uint32_t a, uint32_t b) {
+        const bool ma = mw_trial(k, in[k][a].memlevel), mb = mw_trial(k, in[k][b].memlevel);
+        return ma != mb ? ma : key[a] > key[b];
+      });
+    }
     S.tr[k].resize(n);
     for (size_t q = 0; q < n; q++) S.tr[k][q] = in[k][S.perm[k][q]];
     S.res[k].clear();
@@ -1722,12 +1876,31 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
   }
   return 0;
 }
+// ATZ_EARLY=0: every first-pass match table waits for the round's plan (Round::plan)
+static bool early_match_on() {
+  static const bool v = [] { const char* e = std::getenv("ATZ_EARLY"); return !e || std::atoi(e) != 0; }();
+  return v;
+}
+// A trial's match table in the round's d_R (c->r_next on) and its first pass: whole where the trial must
+// parse the whole stream, and for the memLevel the stream's first block names (its likely winner: no
+// rerun with the rest of the table); else a prefix.  Sets t.r_off and t.x_lim.
+static MatchJob first_match_job(atz_ctx* x, Pipe* c, int k, Trial& t) {
+  const uint64_t n = x->recs[t.stream].infl_len;
+  t.r_off = c->r_next;
+  c->r_next += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
+  t.x_lim = (t.mode & 3) || (mhint_on(x) && t.memlevel == x->recs[t.stream].mhint) ? n : match_prefix(n, t.memlevel, big_sweep(x));
+  MatchJob m{};
+  m.infl_off = x->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
+  m.p0 = 0; m.p1 = t.x_lim; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
+  return m;
+}
 // The launches of a first pass (match tables, trials); results at d_tres + bases[k] in launch order.
+// Match tables go into d_R from c->r_next on (reset by the caller: Round, run_trials); a trial whose
+// x_lim is set already has its first-pass table (launched early by Round::plan).
 static int trials_first_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, const SweepOpts& so,
                                size_t bases[3]) {
   std::vector<Trial>* tr = S.tr;
   std::vector<TrialRes>* res = S.res;
-  uint64_t r_tot = 0;
   std::vector<MatchJob> mj;
   for (int k = 0; k < 3; k++)
     for (const Trial& t : tr[k])
@@ -1740,18 +1913,13 @@ static int trials_first_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialS
     for (Trial& t : tr[k]) {
       const uint64_t n = x->recs[t.stream].infl_len;
       if ((t.mode & 24) == 8) { t.r_off = 0; t.x_lim = n; continue; }   // unchecked replays: no match table
-      t.r_off = r_tot;
-      r_tot += ((n + 63) & ~63ull) + 256;   // + the double-buffered window's over-read
-      // whole tables where the trial must parse the whole stream, and for the memLevel the stream's first
-      // block names (its likely winner: no rerun with the rest of the table)
-      t.x_lim = (t.mode & 3) || (mhint_on(x) && t.memlevel == x->recs[t.stream].mhint) ? n : match_prefix(n, t.memlevel, big_sweep(x));
-      MatchJob m{};
-      m.infl_off = x->infl_off[t.stream]; m.n = n; m.chain_off = t.chain_off; m.r_off = t.r_off;
-      m.p0 = 0; m.p1 = t.x_lim; m.level = t.clevel; m.window = t.window; m.fast = k == 1; m.memlevel = t.memlevel;
-      if (m.p1 > m.p0) mj.push_back(m);
+      if (t.x_lim) continue;   // its table's first pass is already launched (Round::plan)
+      if (MatchJob m = first_match_job(x, c, k, t); m.p1 > m.p0) mj.push_back(m);
     }
-  if (int r = c->d_R.reserve(r_tot * sizeof(uint2) + 4096)) return r;
+  if (int r = c->d_R.reserve(c->r_next * sizeof(uint2) + 4096)) return r;
+  c->lap(6);
   if (int r = launch_match(x, c, mj)) return r;
+  c->lap(7);
   const size_t tot_trials = tr[0].size() + tr[1].size() + tr[2].size();
   if (int r = c->d_trials.reserve(2 * tot_trials * sizeof(Trial) + 64)) return r;
   if (int r = c->d_tres.reserve(2 * tot_trials * sizeof(TrialRes) + 64)) return r;
@@ -1764,7 +1932,9 @@ static int trials_first_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialS
     base += tr[k].size();
   }
   S.base = base;
-  return trials_join(c);
+  const int rj = trials_join(c);
+  c->lap(8);
+  return rj;
 }
 // First pass: match-table prefixes, every trial once, results read back.  Chain tables must exist.
 static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, const SweepOpts& so) {
@@ -1777,6 +1947,7 @@ static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, 
       HIPCHK(pipe_copy(c, res[k].data(), c->d_tres.as<TrialRes>() + bases[k], tr[k].size() * sizeof(TrialRes), hipMemcpyDeviceToHost));
   HIPCHK(pipe_sync(c));
   kcollect(c);
+  c->lap(9);
   return 0;
 }
 // Reruns: the TR_NEED_R trials for which want(trial) holds get the rest of their match table and run
@@ -1842,6 +2013,7 @@ static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Tri
                       std::vector<TrialRes>* res) {
   TrialSet S;
   trials_order(x, tr, S);
+  c->r_next = 0;
   if (int r = trials_first(x, c, d_cmp, S, so)) return r;
   if (int r = trials_rerun(x, c, d_cmp, S, so, nullptr)) return r;
   trials_results(S, res);
@@ -1922,8 +2094,9 @@ static void level_dups(atz_ctx* x, std::vector<StreamState>& ss, std::vector<Tri
 // after a round: what the budget-free level-7-9 trials that ran parsed (a replay parsed its saver's
 // whole sequence)
 // (streams for which mine(stream) holds)
+template <class Mine>
 static void level_record(atz_ctx* x, std::vector<StreamState>& ss, const std::vector<Trial>& slow,
-                         const std::vector<TrialRes>& res, const std::function<bool(uint32_t)>& mine) {
+                         const std::vector<TrialRes>& res, const Mine& mine) {
   for (size_t q = 0; q < slow.size(); q++) {
     const Trial& t = slow[q];
     const TrialRes& r = res[q];
@@ -2096,10 +2269,10 @@ struct Round {
   std::vector<uint32_t> need_b;                 // per need entry: the trial's walk budget (budget-free test)
   std::vector<std::array<uint32_t, 4>> savers;  // (kind, index in tr[kind], rp_pool entry, level - 1)
   uint64_t out_tot = 0, sym_tot = 0;
+  uint64_t r_bound = 0;             // d_R entries if every table-reading trial got a table (uint2 units)
   size_t nbuild = 0;
   // streams of the batch by index a into active: held[a] = its rule walk waits for a rerun
   std::vector<uint8_t> held;
-  std::vector<uint32_t> slot_of;   // indices a, sorted by stream (is_held)
   TrialSet SA, SB;                 // A: every trial neither a duplicate nor waiting for a saver; B: the waiting ones
   std::vector<uint32_t> ia[3], ib[3];   // their indices in tr[k]
   bool waiting_trials = false;
@@ -2112,11 +2285,7 @@ struct Round {
         std::vector<uint32_t>& a_, std::vector<uint32_t>& w_)
       : x(x_), c(c_), d_file(f), ss(ss_), so(so_), active(a_), waiting(w_) {}
 
-  bool is_held(uint32_t s) const {
-    const size_t i = std::lower_bound(slot_of.begin(), slot_of.end(), s,
-                                      [&](uint32_t e, uint32_t v) { return active[e] < v; }) - slot_of.begin();
-    return held[slot_of[i]] != 0;
-  }
+  bool is_held(uint32_t s) const { return held[c->slot[s]] != 0; }
 
   // The trials of the next K list entries of every stream, within the round's scratch budget.
   void build_lists() {
@@ -2149,6 +2318,7 @@ struct Round {
         t.sym_off = sym_tot; sym_tot += sw;
         round_bytes += 8 * (x->recs[s].infl_len + 320) + t.out_cap + 4 * sw;
         if (kind) {
+          r_bound += ((x->recs[s].infl_len + 63) & ~63ull) + 256;
           need.push_back({s, m});
           need_b.push_back((uint32_t)(c_cfg_host((uint32_t)cl) >> (kind == 1 ? 0 : 2)));
         }
@@ -2159,9 +2329,8 @@ struct Round {
     mbeg.resize(active.size() + 1);
     mbeg[active.size()] = (uint32_t)mine.size();
     held.assign(active.size(), 0);
-    slot_of.resize(active.size());
-    for (size_t a = 0; a < active.size(); a++) slot_of[a] = (uint32_t)a;
-    std::sort(slot_of.begin(), slot_of.end(), [&](uint32_t p1, uint32_t p2) { return active[p1] < active[p2]; });
+    if (c->slot.size() < x->recs.size()) c->slot.resize(x->recs.size());
+    for (size_t a = 0; a < active.size(); a++) c->slot[active[a]] = (uint32_t)a;
     pend.assign(active.size(), PendDiff{});
     jpos.assign(mbeg.begin(), mbeg.end() - 1);
   }
@@ -2169,6 +2338,8 @@ struct Round {
   // Replays first (they need the pairs' bucket depths only), duplicates, the eligibility floor, then the
   // bucket tables the other trials read (stream-ordered before the match walks: no sync).
   int plan() {
+    c->r_next = 0;   // the round's match tables (early ones below, the rest in launch) never move
+    if (int r = c->d_R.reserve(r_bound * sizeof(uint2) + 4096)) return r;
     if (replay_on() && x->depth_pin.p) {
       // Replay planning reads the pairs' deepest buckets.  A trial that can only parse (its stream has no
       // saved sequence at its (level, window) to replay, nor a higher level's run to duplicate) needs its
@@ -2177,8 +2348,15 @@ struct Round {
       // will replay.  (Round 1 of a sweep has no saved sequences: no depth passes at all.)
       std::vector<std::pair<uint32_t, int>> dfirst, direct;
       std::vector<uint32_t> dfirst_b;
-      for (int k = 1; k < 3; k++)
-        for (const Trial& t : tr[k]) {
+      std::vector<std::pair<int, uint32_t>> early;   // (kind, index) of the direct pairs' trials
+      for (int k = 1; k < 3; k++) {
+        uint32_t cur = ~0u;
+        uint16_t seen[16] = {};   // the stream's levels so far in tr[k] per window (its trials are contiguous)
+        for (uint32_t q = 0; q < tr[k].size(); q++) {
+          const Trial& t = tr[k][q];
+          if (t.stream != cur) { cur = t.stream; std::memset(seen, 0, sizeof seen); }
+          const bool again = (seen[t.window & 15] >> t.clevel) & 1u;   // may wait for a saver of this round
+          seen[t.window & 15] |= (uint16_t)(1u << t.clevel);
           const StreamState& st = ss[t.stream];
           bool maybe = false;
           if (st.rp >= 0) {
@@ -2193,14 +2371,41 @@ struct Round {
             dfirst_b.push_back((uint32_t)(c_cfg_host(t.clevel) >> (k == 1 ? 0 : 2)));
           } else {
             direct.push_back({t.stream, (int)t.memlevel});
+            if (!again) early.push_back({k, q});
           }
         }
+      }
       for (auto& q : direct) nbuild += x->chain_off[q.first][q.second] == ~0ull;
       if (int r = ensure_depths(x, c, dfirst, dfirst_b)) return r;
       if (int r = ensure_chains(x, c, direct)) return r;
-      HIPCHK(pipe_sync(c));
+      c->lap(1);
+      if (early_match_on() && !early.empty()) {
+        // A direct pair's trials can become neither replays nor duplicates (no saved sequence at their
+        // level and window, no higher level's twin) unless an earlier trial of their stream in this
+        // round may save one (speculative rounds), so the others' first-pass tables need no plan: they
+        // run while the host plans the rest, once the depths (the builds) are in.
+        if (!c->ev_built) HIPCHK(hipEventCreateWithFlags(&c->ev_built, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(c->ev_built, c->st));
+        std::vector<MatchJob> mj;
+        mj.reserve(early.size());
+        for (const auto& e : early) {
+          Trial& t = tr[e.first][e.second];
+          t.chain_off = x->chain_off[t.stream][t.memlevel];
+          if (MatchJob m = first_match_job(x, c, e.first, t); m.p1 > m.p0) mj.push_back(m);
+        }
+        if (int r = launch_match(x, c, mj)) return r;
+        c->lap(6);
+        const auto t_ev = std::chrono::steady_clock::now();
+        HIPCHK(hipEventSynchronize(c->ev_built));
+        c->t_sync += ms_since(t_ev);
+        c->n_sync++;
+      } else {
+        HIPCHK(pipe_sync(c));
+      }
+      c->lap(2);
       if (dedup_on()) level_dups(x, ss, tr[2]);
       for (int k = 1; k < 3; k++) plan_replay(x, c, ss, k, tr[k], savers);
+      c->lap(3);
       need.clear();
       for (int k = 1; k < 3; k++)
         for (const Trial& t : tr[k])
@@ -2221,6 +2426,7 @@ struct Round {
         if ((t.mode & 12) && !replay_slot_ok(t)) return ATZ_E_INTERNAL;
     if (int r = c->d_out.reserve(out_tot + 4096)) return r;
     if (int r = c->d_syms.reserve(sym_tot * 4 + 4096)) return r;
+    c->lap(4);
     return 0;
   }
   bool replay_slot_ok(const Trial& t) const {
@@ -2272,6 +2478,7 @@ struct Round {
       }
       trials_order(x, ta, SA);
     }
+    c->lap(5);
     if (int r = trials_first(x, c, d_file, SA, so)) return r;
     if (!waiting_trials) {
       collect(SA, ia);
@@ -2511,15 +2718,19 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     } give{x, c, ss, active, waiting};
     Round R(x, c, d_file, ss, so, active, waiting);
     const auto tl0 = std::chrono::steady_clock::now();
+    c->lap_start();
     R.build_lists();
+    c->lap(0);
     const auto ta = std::chrono::steady_clock::now();
     if (int r = R.plan()) return r;
     const auto tb = std::chrono::steady_clock::now();
     if (int r = R.launch()) return r;
     const auto tc = std::chrono::steady_clock::now();
     if (int r = R.apply()) return r;
+    c->lap(10);
     if (int r = R.flush_diffs()) return r;
     R.release_done();
+    c->lap(11);
     const auto td = std::chrono::steady_clock::now();
     c->t_chains += std::chrono::duration<double, std::milli>(tb - ta).count();
     c->t_trials += std::chrono::duration<double, std::milli>(tc - tb).count();
@@ -2531,6 +2742,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
                    std::chrono::duration<double, std::milli>(tc - tb).count(),
                    std::chrono::duration<double, std::milli>(td - tc).count());
     R.account(rounds);
+    c->lap(12);
     c->t_apply += ms_since(tc);
     c->stats.n_trials += R.ntr; c->stats.n_trials_shortcut += R.nsc; c->stats.n_hazard += R.nhz;
     c->stats.n_trials_speculative += R.nspec;
@@ -2677,6 +2889,8 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
     p->stats = atz_stats_t{};
     p->t_list = p->t_chains = p->t_trials = p->t_apply = p->t_copy = p->t_sync = 0;
     p->n_copy = p->n_sync = 0;
+    std::memset(p->ph, 0, sizeof(p->ph));
+    std::memset(p->ph_wait, 0, sizeof(p->ph_wait));
     std::memset(p->kind, 0, sizeof(p->kind));
   }
   R.rc.assign(R.np, 0);
@@ -2684,6 +2898,7 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
   for (size_t g = 0; g < R.np; g++)
     R.th.emplace_back([c, &R, &ss, g]() {
       if (hipSetDevice(c->dev) != hipSuccess) { R.rc[g] = ATZ_E_HIP; sched_abort(c); return; }
+      HostProf::Enroll prof_enroll;
       try {   // no exception may leave a thread (guarded() covers the calling one)
         R.rc[g] = sweep_pipe(c, c->pipes[g].get(), R.d_file, ss);
       } catch (const std::bad_alloc&) {
@@ -2757,6 +2972,15 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
       Pipe* p = c->pipes[g].get();
       std::fprintf(stderr, "atz: pipe %zu: %llu copy calls %.1f ms, %llu syncs %.1f ms\n", g, (unsigned long long)p->n_copy,
                    p->t_copy, (unsigned long long)p->n_sync, p->t_sync);
+      static const char* phn[Pipe::NPH] = {"list", "tables-enq", "tables-sync", "replay-plan", "plan-rest", "order",
+                                           "match-jobs", "match-launch", "trial-launch", "results", "apply", "diffs", "account"};
+      std::string line;
+      char b[96];
+      for (int i = 0; i < Pipe::NPH; i++) {
+        std::snprintf(b, sizeof b, " %s %.1f(%.1f)", phn[i], p->ph[i], p->ph_wait[i]);
+        line += b;
+      }
+      std::fprintf(stderr, "atz: pipe %zu host phases ms (waiting):%s\n", g, line.c_str());
     }
     uint64_t nb = 0, nn = 0;
     for (size_t g = 0; g < np; g++) {
@@ -3815,6 +4039,7 @@ int atz_precompress_device(atz_ctx_t* c, const uint8_t* d_file, const uint8_t* h
     (void)hipGetLastError();
     if (!c || !d_file || !h_file || !d_atz || !atz_len) return ATZ_E_ARG;
     dev_mark_call();
+    HostProf prof;
     uint64_t al = 0;
     auto tc = std::chrono::steady_clock::now();
     if (int r = precompress_dev(c, d_file, h_file, len, &al, nullptr)) return r;
