@@ -362,6 +362,10 @@ struct StreamState {
   std::vector<uint8_t> diffval;
   uint32_t trials = 0;
   int32_t rp = -1;                // symbol-replay entries (levels 1-9) in the context's rp_pool
+  // their states at a glance (bit L: level L's entry is saved / has its saver in flight; rp_win[L]: that
+  // sequence's window), so that planning reads rp_pool only where an entry is used
+  uint16_t rp_saved = 0, rp_busy = 0;
+  uint8_t rp_win[10] = {};
   bool recomp = false;
   // levels 7-9 already run budget-free at (window, memLevel): level, longest PL a lazy read improved,
   // longest length read (cross-level duplicates, see level_dups)
@@ -2137,19 +2141,22 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
     const bool bf = replay_free(x, kind, t);
     if (!bf && !checked) continue;
     StreamState& st = ss[t.stream];
-    if (st.rp < 0) {   // the pool holds one entry per stream at most: never past its reserve
-      std::lock_guard<std::mutex> lk(x->rp_mu);
-      if (x->rp_pool.size() == x->rp_pool.capacity()) continue;
-      st.rp = (int32_t)x->rp_pool.size();
-      x->rp_pool.emplace_back();
-    }
-    RpEntry& e = x->rp_pool[st.rp][t.clevel - 1];
-    if (e.state == 2 && e.window == t.window) {
+    const uint32_t L = t.clevel;
+    const bool saved = (st.rp_saved >> L) & 1u, busy = (st.rp_busy >> L) & 1u;   // entry state 2 / 1 (else 0)
+    const bool same_w = st.rp_win[L] == t.window;
+    if (saved && same_w) {
       if (replay_mode() == 2) continue;
-      replay_from(t, e, bf);
-    } else if (e.state == 1 && e.window == t.window && replay_mode() != 2 && (bf || e.tab)) {
+      replay_from(t, x->rp_pool[st.rp][L - 1], bf);
+    } else if (busy && same_w && replay_mode() != 2 && (bf || x->rp_pool[st.rp][L - 1].tab)) {
       t.mode |= 64;   // its saver runs in this round: wait for it (second launch of the round)
-    } else if (e.state == 0 && bf) {
+    } else if (!saved && !busy && bf) {
+      if (st.rp < 0) {   // the pool holds one entry per stream at most: never past its reserve
+        std::lock_guard<std::mutex> lk(x->rp_mu);
+        if (x->rp_pool.size() == x->rp_pool.capacity()) continue;
+        st.rp = (int32_t)x->rp_pool.size();
+        x->rp_pool.emplace_back();
+      }
+      RpEntry& e = x->rp_pool[st.rp][L - 1];
       const uint64_t sb = (4 * (n + 64) + 255) & ~255ull, tb = kind == 2 ? ((8 * n + 255) & ~255ull) : 0;
       if (!e.addr) {
         e.addr = x->rp_arena.alloc(sb + tb);
@@ -2159,6 +2166,8 @@ static void plan_replay(atz_ctx* x, Pipe* c, std::vector<StreamState>& ss, int k
       e.state = 1;
       e.window = t.window;
       e.memlevel = t.memlevel;
+      st.rp_busy |= (uint16_t)(1u << L);
+      st.rp_win[L] = t.window;
       t.mode |= 4;
       t.rp_syms = e.addr;
       if (e.tab) { t.mode |= 32; t.rp_tab = e.tab; }
@@ -2359,10 +2368,7 @@ struct Round {
           seen[t.window & 15] |= (uint16_t)(1u << t.clevel);
           const StreamState& st = ss[t.stream];
           bool maybe = false;
-          if (st.rp >= 0) {
-            const RpEntry& e = x->rp_pool[st.rp][t.clevel - 1];
-            maybe = e.state == 2 && e.window == t.window;
-          }
+          if (st.rp >= 0) maybe = ((st.rp_saved >> t.clevel) & 1u) && st.rp_win[t.clevel] == t.window;
           if (!maybe && k == 2 && t.clevel >= 7)
             for (const auto& r : st.xl) maybe |= r[0] == t.window && r[1] == t.memlevel && r[2] > t.clevel;
           static const bool all_first = [] { const char* e = std::getenv("ATZ_DFIRST"); return e && std::atoi(e) == 0; }();
@@ -2445,8 +2451,12 @@ struct Round {
       if (is_held(tr[sv[0]][sv[1]].stream) != held_ones) continue;
       const TrialRes& r = trres[sv[0]][sv[1]];
       RpEntry& e = x->rp_pool[sv[2]][sv[3]];
+      StreamState& st = ss[tr[sv[0]][sv[1]].stream];
+      const uint16_t bit = (uint16_t)(1u << (sv[3] + 1));
+      st.rp_busy &= (uint16_t)~bit;
       if (r.state != TR_NEED_R && (r.saved_flags & 1u)) {
         e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags; e.reads_max = r.reads_max;
+        st.rp_saved |= bit;
       } else {
         e.state = 0;   // the slot stays for the next saving trial
       }
