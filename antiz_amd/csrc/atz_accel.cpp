@@ -567,11 +567,6 @@ struct Pipe {
   // round (a later call must not move an earlier call's tables), kept for the next rounds' reuse
   std::vector<std::unique_ptr<DBuf>> d_chains;
   size_t chains_next = 0;
-  // ATZ_KSTREAMS=1: the fast and slow trial launches of a round on streams of their own (fork after the
-  // tables, join before the results), so their tails overlap instead of adding up
-  hipStream_t kst[2] = {nullptr, nullptr};
-  hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
-  bool joined[2] = {true, true};
   ChainBufs cb;
   // pinned staging for the pipe's uploads (a pageable hipMemcpyAsync returns only once the stream has
   // reached it, which would hold the host thread behind every kernel enqueued before it): a bump
@@ -581,6 +576,7 @@ struct Pipe {
   // match tables of the round: d_R regions handed out in order (Round::plan reserves the round's bound)
   uint64_t r_next = 0;
   hipEvent_t ev_built = nullptr;   // after a round's direct bucket builds (their depths: Round::plan)
+
   // a second stream that stays idle: it only shifts how the process's GPU_MAX_HW_QUEUES (4) hardware
   // queues are shared by the pipes' streams (two pipes then share a queue, which measured faster
   // than every pipe on its own queue: DESIGN.md s3.6)
@@ -591,6 +587,8 @@ struct Pipe {
   // diagnostics (ATZ_TIMING): bucket builds, and per stream the memLevels a table-reading trial used
   uint64_t diag_builds = 0;
   std::vector<std::pair<uint32_t, uint32_t>> diag_rt;   // ATZ_TIMING >= 3: every launched trial's realtime span
+  std::vector<uint64_t> diag_path;   // ATZ_TIMING >= 3: per stream, its trials' summed realtime spans (10 ns)
+  std::vector<uint32_t> diag_ntr;    //   and their number
   std::vector<uint16_t> diag_need;
   std::vector<uint32_t> slot;   // per stream of the current round: its index in the round's batch
   int id = 0;
@@ -613,11 +611,6 @@ struct Pipe {
   }
   uint64_t kind[3][10][14] = {};
   ~Pipe() {
-    for (int i = 0; i < 2; i++) {
-      if (kst[i]) { hipStreamSynchronize(kst[i]); hipStreamDestroy(kst[i]); }
-      if (ev_join[i]) hipEventDestroy(ev_join[i]);
-    }
-    if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_built) hipEventDestroy(ev_built);
     if (pst) { hipStreamSynchronize(pst); hipStreamDestroy(pst); }
     if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
@@ -1426,7 +1419,7 @@ static int ensure_chains(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32
 // whose known lower bound already exceeds B cannot be budget-free and its depth is not computed
 // (it stays unknown, which budget_free reads as "not budget-free").
 static int ensure_depths(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32_t, int>>& need,
-                         const std::vector<uint32_t>& need_b) {
+                         const std::vector<uint32_t>& need_b, DBuf& d_jobs) {
   if (!x->depth_pin.p) return 0;
   uint32_t* dp = x->depth_pin.as<uint32_t>();
   std::vector<ChainJob> byl[10];
@@ -1458,13 +1451,13 @@ static int ensure_depths(atz_ctx* x, Pipe* c, const std::vector<std::pair<uint32
   size_t beg[11] = {};
   for (int m = 0; m < 10; m++) { beg[m] = all.size(); all.insert(all.end(), byl[m].begin(), byl[m].end()); }
   beg[10] = all.size();
-  if (int r = upload(c, c->d_djobs, all.data(), all.size() * sizeof(ChainJob))) return r;
+  if (int r = upload(c, d_jobs, all.data(), all.size() * sizeof(ChainJob))) return r;
   for (int m = 1; m < 10; m++) {
     const size_t cnt = beg[m + 1] - beg[m];
     if (!cnt) continue;
     kbeg(c, 2);
     hipLaunchKernelGGL(k_bucket_depth, dim3((uint32_t)cnt), dim3(BDEPTH_THREADS), 4u << (m + 6), c->st, INFL_BASE,
-                       c->d_djobs.as<ChainJob>() + beg[m], (uint32_t)cnt, dp);
+                       d_jobs.as<ChainJob>() + beg[m], (uint32_t)cnt, dp);
     kend(c);
     KCHECK("k_bucket_depth");
   }
@@ -1810,38 +1803,9 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
   S.base = 0;
 }
 // the trial kernels over h[0, cnt) (one kind, multi-wave ones first), at slots [base, base + cnt)
-static bool kstreams_on() {
-  static const bool v = [] { const char* e = std::getenv("ATZ_KSTREAMS"); return e && std::atoi(e) != 0; }();
-  return v;
-}
-// The stream kind k's trial launches go to (ATZ_KSTREAMS: fast and slow levels forked off the pipe's
-// stream after everything enqueued so far, i.e. their tables); trials_join puts the pipe's stream after them.
-static hipStream_t trials_fork(Pipe* c, int k) {
-  if (!kstreams_on() || k == 0) return c->st;
-  const int i = k - 1;
-  if (!c->kst[i]) {
-    if (hipStreamCreateWithFlags(&c->kst[i], hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) != hipSuccess)
-      return nullptr;
-    if (!c->ev_fork && hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-  }
-  if (hipEventRecord(c->ev_fork, c->st) != hipSuccess || hipStreamWaitEvent(c->kst[i], c->ev_fork, 0) != hipSuccess)
-    return nullptr;
-  c->joined[i] = false;
-  return c->kst[i];
-}
-static int trials_join(Pipe* c) {
-  for (int i = 0; i < 2; i++) {
-    if (c->joined[i]) continue;
-    HIPCHK(hipEventRecord(c->ev_join[i], c->kst[i]));
-    HIPCHK(hipStreamWaitEvent(c->st, c->ev_join[i], 0));
-    c->joined[i] = true;
-  }
-  return 0;
-}
 static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepOpts& so, int k, const Trial* h,
                          size_t cnt, size_t base) {
-  // the trial descriptors first (on the pipe's stream), then the launches, forked for kinds 1-2
+  // the trial descriptors first, then the launches
   for (size_t i = 0; i < cnt;) {
     const bool mw = mw_trial(k, h[i].memlevel);
     size_t j = i + 1;
@@ -1849,8 +1813,6 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
     HIPCHK(pipe_copy(c, c->d_trials.as<Trial>() + base + i, h + i, (j - i) * sizeof(Trial), hipMemcpyHostToDevice));
     i = j;
   }
-  const hipStream_t ls = trials_fork(c, k);
-  if (!ls) return ATZ_E_HIP;
   auto launch1 = [&](const Trial* hh, size_t n1, size_t b1, bool mw) -> int {
     (void)hh;
     SweepArgs A;
@@ -1860,13 +1822,13 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
     A.res = c->d_tres.as<TrialRes>() + b1; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
     A.adler = x->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)n1;
     dim3 g((uint32_t)n1), b(mw ? MW_THREADS : 64);
-    kbeg(c, 0, ls);
-    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, ls, A);
-    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw<BITMAP_BITS>, g, b, 0, ls, A);
-    else if (k == 1) hipLaunchKernelGGL(k_trial_fast<BITMAP_BITS>, g, b, 0, ls, A);
-    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, 0, ls, A);
-    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, ls, A);
-    kend(c, ls);
+    kbeg(c, 0);
+    if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
+    else if (k == 1 && mw) hipLaunchKernelGGL(k_trial_fast_mw<BITMAP_BITS>, g, b, 0, c->st, A);
+    else if (k == 1) hipLaunchKernelGGL(k_trial_fast<BITMAP_BITS>, g, b, 0, c->st, A);
+    else if (mw) hipLaunchKernelGGL(k_trial_slow_mw, g, b, 0, c->st, A);
+    else hipLaunchKernelGGL(k_trial_slow, g, b, 0, c->st, A);
+    kend(c);
     KCHECK(k == 0 ? "k_trial_stored" : k == 1 ? "k_trial_fast" : "k_trial_slow");
     return 0;
   };
@@ -1936,16 +1898,20 @@ static int trials_first_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialS
     base += tr[k].size();
   }
   S.base = base;
-  const int rj = trials_join(c);
   c->lap(8);
-  return rj;
+  return 0;
 }
 // First pass: match-table prefixes, every trial once, results read back.  Chain tables must exist.
+static int trials_first_finish(Pipe* c, TrialSet& S, const size_t bases[3]);
 static int trials_first(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, const SweepOpts& so) {
-  std::vector<Trial>* tr = S.tr;
-  std::vector<TrialRes>* res = S.res;
   size_t bases[3];
   if (int r = trials_first_launch(x, c, d_cmp, S, so, bases)) return r;
+  return trials_first_finish(c, S, bases);
+}
+// a first pass's results read back (after trials_first_launch)
+static int trials_first_finish(Pipe* c, TrialSet& S, const size_t bases[3]) {
+  std::vector<Trial>* tr = S.tr;
+  std::vector<TrialRes>* res = S.res;
   for (int k = 0; k < 3; k++)
     if (!tr[k].empty())
       HIPCHK(pipe_copy(c, res[k].data(), c->d_tres.as<TrialRes>() + bases[k], tr[k].size() * sizeof(TrialRes), hipMemcpyDeviceToHost));
@@ -1990,7 +1956,6 @@ static int trials_rerun(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, TrialSet& S, 
     rr[k].resize(again[k].size());
     base += again[k].size();
   }
-  if (int r = trials_join(c)) return r;
   for (int k = 1; k < 3; k++)
     if (!again[k].empty())
       HIPCHK(pipe_copy(c, rr[k].data(), c->d_tres.as<TrialRes>() + bases[k], again[k].size() * sizeof(TrialRes), hipMemcpyDeviceToHost));
@@ -2257,7 +2222,12 @@ static void account_trial(atz_ctx* x, Pipe* c, int k, const Trial& t, const Tria
   if (!(t.mode & 128))   // duplicates are not launched; a trial never rerun stopped at its prefix
     c->stats.k_trial_alg_bytes += r.state == TR_NEED_R ? r.parsed
                                   : x->recs[t.stream].infl_len + (r.out_len < C ? r.out_len : C);
-  if (timing_level() >= 3 && !(t.mode & 128)) c->diag_rt.push_back({r.rt0, r.rt1});
+  if (timing_level() >= 3 && !(t.mode & 128)) {
+    c->diag_rt.push_back({r.rt0, r.rt1});
+    if (c->diag_path.size() <= t.stream) { c->diag_path.resize(x->recs.size(), 0); c->diag_ntr.resize(x->recs.size(), 0); }
+    c->diag_path[t.stream] += (uint32_t)(r.rt1 - r.rt0);
+    c->diag_ntr[t.stream]++;
+  }
 }
 // One round of pipe c over its batch `active`: the next K list entries of every stream (speculatively:
 // a stream that stops at its j-th trial discards the results of the later ones), K sized so the rounds
@@ -2382,7 +2352,7 @@ struct Round {
         }
       }
       for (auto& q : direct) nbuild += x->chain_off[q.first][q.second] == ~0ull;
-      if (int r = ensure_depths(x, c, dfirst, dfirst_b)) return r;
+      if (int r = ensure_depths(x, c, dfirst, dfirst_b, c->d_djobs)) return r;
       if (int r = ensure_chains(x, c, direct)) return r;
       c->lap(1);
       if (early_match_on() && !early.empty()) {
@@ -2489,7 +2459,11 @@ struct Round {
       trials_order(x, ta, SA);
     }
     c->lap(5);
-    if (int r = trials_first(x, c, d_file, SA, so)) return r;
+    {
+      size_t bases[3];
+      if (int r = trials_first_launch(x, c, d_file, SA, so, bases)) return r;
+      if (int r = trials_first_finish(c, SA, bases)) return r;
+    }
     if (!waiting_trials) {
       collect(SA, ia);
       return 0;
@@ -2724,7 +2698,10 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     std::vector<uint32_t> waiting;
     struct Give {   // the batch goes back on every exit from the round (an error aborts the sweep anyway)
       atz_ctx* x; Pipe* c; const std::vector<StreamState>& ss; const std::vector<uint32_t>& a, &w;
-      ~Give() { forget_tmp_chains(x, c); sched_give(x, c->id, ss, a, w); }
+      ~Give() {
+        forget_tmp_chains(x, c);
+        sched_give(x, c->id, ss, a, w);
+      }
     } give{x, c, ss, active, waiting};
     Round R(x, c, d_file, ss, so, active, waiting);
     const auto tl0 = std::chrono::steady_clock::now();
@@ -2764,33 +2741,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
 
 // Phase 3 driver: streams partitioned over the context's pipes (interleaved, so every pipe gets
 // the same mix of header classes and sizes), one host thread per pipe.
-// ATZ_QMAP=1: the pipes' main streams are created before their second ones, so that (with enough hardware
-// queues) no two pipes share a queue; 0 (default): interleaved, two pipes share one
-static int qmap_mode() {
-  static const int v = [] { const char* e = std::getenv("ATZ_QMAP"); return e ? std::atoi(e) : 0; }();
-  return v;
-}
 static int ensure_pipes(atz_ctx* c, size_t np) {
-  if (qmap_mode() == 1 && c->pipes.size() < np) {   // main streams first (HIP maps streams to queues in turn)
-    std::vector<hipStream_t> mains;
-    for (size_t g = c->pipes.size(); g < np; g++) {
-      hipStream_t st;
-      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
-      mains.push_back(st);
-    }
-    for (hipStream_t st : mains) {
-      std::unique_ptr<Pipe> p(new Pipe());
-      p->id = (int)c->pipes.size();
-      p->st = st;
-      c->pipes.push_back(std::move(p));
-    }
-    for (size_t g = 0; g < c->pipes.size(); g++) {
-      Pipe* p = c->pipes[g].get();
-      if (p->pst) continue;
-      if (hipStreamCreateWithFlags(&p->pst, hipStreamNonBlocking) != hipSuccess) return ATZ_E_HIP;
-    }
-    return 0;
-  }
   while (c->pipes.size() < np) {
     std::unique_ptr<Pipe> p(new Pipe());
     p->id = (int)c->pipes.size();
@@ -3004,6 +2955,28 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
                  "%.2f GB allocated, %.2f GB served from released tables; saved sequences %.2f GB; device peak %.2f GB\n",
                  (unsigned long long)nb, (unsigned long long)nn, c->chain_arena.total / 1e9, c->chain_arena.reused / 1e9,
                  c->rp_arena.total / 1e9, g_dev.peak.load() / 1e9);
+  }
+  if (timing_level() >= 3) {   // per-stream critical path: each stream's trials run one after another
+    std::vector<uint64_t> path(n, 0), ntr(n, 0);
+    for (size_t g = 0; g < np; g++) {
+      Pipe* p = c->pipes[g].get();
+      for (size_t s2 = 0; s2 < p->diag_path.size() && s2 < n; s2++) { path[s2] += p->diag_path[s2]; ntr[s2] += p->diag_ntr[s2]; }
+      p->diag_path.clear();
+      p->diag_ntr.clear();
+    }
+    std::vector<uint32_t> ord(n);
+    for (size_t s2 = 0; s2 < n; s2++) ord[s2] = (uint32_t)s2;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return path[a] > path[b]; });
+    if (n) {
+      auto q = [&](double f) { return path[ord[std::min(n - 1, (size_t)(f * (double)n))]] / 1e5; };
+      std::fprintf(stderr, "atz: per-stream trial time (ms, summed over its trials): max %.2f p1 %.2f p5 %.2f p10 %.2f p50 %.2f\n",
+                   q(0.0), q(0.01), q(0.05), q(0.10), q(0.5));
+      for (size_t i = 0; i < n && i < 8; i++)
+        std::fprintf(stderr, "atz:   stream %u: %.2f ms over %llu trials, I=%llu C=%llu ident %llu type %d phase %u\n", ord[i],
+                     path[ord[i]] / 1e5, (unsigned long long)ntr[ord[i]], (unsigned long long)c->recs[ord[i]].infl_len,
+                     (unsigned long long)c->recs[ord[i]].comp_len, (unsigned long long)ss[ord[i]].ident, c->recs[ord[i]].type,
+                     ss[ord[i]].phase);
+    }
   }
   if (timing_level() >= 3) {   // trials running at once over the sweep (first passes only: reruns overwrite)
     std::vector<std::pair<uint32_t, int>> ev;

@@ -16,9 +16,10 @@ the ATZ1 bytes must equal the oracle's (the reference's algorithm, oracle/) for 
   ATZ_PREFIX_MIN the match-table prefix floor in positions (default 3072 where big_sweep holds, else 1024)
   ATZ_ELIG     0: every trial keeps the reference's exact rule to its end (default 1: a trial stops once
                it cannot make its stream recompressible; atz_accel.cpp elig_floor)
-  ATZ_KSTREAMS 1: a round's fast- and slow-level trial launches on streams of their own (fork / join)
-  ATZ_QMAP     1: the pipes' main streams created first (no two pipes on one hardware queue)
   ATZ_DFIRST   0: a depth pass before every bucket table (default: only where a replay may spare it)
+  ATZ_EARLY    0: every first-pass match table waits for the round's plan (default: tables of trials that
+               cannot replay are launched before it)
+  ATZ_STAGE    0: uploads straight from pageable memory (default: through a pinned staging buffer)
 """
 import hashlib
 import os
@@ -38,8 +39,8 @@ SETTINGS = [{"ATZ_REPLAY": "0"}, {"ATZ_REPLAY": "2"}, {"ATZ_REPLAY": "3"}, {"ATZ
             {"ATZ_PIPES": "8", "ATZ_TARGET": "256"}, {"ATZ_PIPES": "6", "ATZ_TARGET": "65536"},
             {"ATZ_MHINT": "1"}, {"ATZ_MHINT": "0"}, {"ATZ_PREFIX_MIN": "3072", "ATZ_MHINT": "1"},
             {"ATZ_ELIG": "0"}, {"ATZ_ELIG": "0", "ATZ_REPLAY": "0"},
-            {"ATZ_KSTREAMS": "1"}, {"ATZ_KSTREAMS": "1", "ATZ_PIPES": "6", "ATZ_TARGET": "65536"},
-            {"ATZ_QMAP": "1", "GPU_MAX_HW_QUEUES": "8"}, {"ATZ_DFIRST": "0"}]
+            {"ATZ_DFIRST": "0"}, {"ATZ_EARLY": "0"}, {"ATZ_STAGE": "0"},
+            {"ATZ_EARLY": "0", "ATZ_STAGE": "0"}, {"ATZ_PIPES": "6", "GPU_MAX_HW_QUEUES": "8", "ATZ_TARGET": "65536"}]
 
 RUN = r"""
 import hashlib, sys

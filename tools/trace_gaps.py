@@ -62,7 +62,14 @@ def main():
     for s, e, n, q in step:
         qs.setdefault(q, []).append((s, e))
     for q, iv in sorted(qs.items()):
-        print("queue %s: %d kernels, busy %.1f%%" % (q, len(iv), 100.0 * union(iv) / span))
+        # overlap: summed minus union (0: the queue's kernels never ran at once); gaps between a kernel's
+        # end and the next one's start on the same queue
+        iv.sort()
+        gaps = sorted(max(0, iv[i + 1][0] - iv[i][1]) for i in range(len(iv) - 1))
+        med = gaps[len(gaps) // 2] / 1e3 if gaps else 0.0
+        print("queue %s: %d kernels, busy %.1f%%, overlap %.2f ms, gap median %.1f us, gaps < 20 us %d" %
+              (q, len(iv), 100.0 * union(iv) / span, (sum(e - s for s, e in iv) - union(iv)) / 1e6, med,
+               sum(1 for g in gaps if g < 20000)))
     # concurrency of kernel classes over time, 2 ms bins
     nb = int(span // 2e6) + 1
     print("per 2 ms: running kernels by class (trial/match/buckets/other)")
