@@ -1916,768 +1916,805 @@ __device__ void trial_flusher(const SweepArgs& A, LDS TrialShared& s, LDS MWPart
 
 static constexpr uint32_t TR_DECIDED = 0xfffffffeu;   // parser-side: a flusher decided the trial (MWCtl::state)
 
+// One trial (a wave, or a parse wave and MW_F flushers): the stream's zlib header, the level's parse
+// over the match tables -- deflate_stored, a replay of a saved symbol sequence, deflate_fast or
+// deflate_slow -- with its blocks flushed as they fill, then the trailer and the final gates.  The
+// parse state lives in the members (registers, once everything is inlined).
 template <int KIND, typename SH>
-__device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
-  constexpr bool MW = HasMW<SH>::value;
-  const int wave = MW ? (int)(threadIdx.x >> 6) : 0;
-  LDS TrialShared& s = *(LDS TrialShared*)&shm.t;
-  LDS uint32_t* const stg = (LDS uint32_t*)shm.ring;   // emission staging (overlays the ring)
-  const uint32_t t = blockIdx.x;
-  const Trial tr = A.trials[t];
-  const StreamDev sd = A.streams[tr.stream];
-  const uint8_t* in = A.infl + sd.infl_off;
+struct TrialRun {
+  static constexpr bool MW = HasMW<SH>::value;
+  const SweepArgs& A;
+  SH& shm;
+  const int lane, wave;
+  LDS TrialShared& s;
+  LDS uint32_t* const stg;   // emission staging (overlays the ring)
+  LDS BitOut& b;
+  const uint32_t t;
+  const Trial tr;
+  const StreamDev sd;
+  const uint8_t* const in;
   // hash buckets of (stream, memLevel): sidx[npad] then bpos[npad]
-  const uint32_t npad = (sd.infl_len + 63) & ~63ull;
-  const uint32_t* sidx = KIND == 0 ? nullptr : A.chains + tr.chain_off;
-  const uint32_t* bpos = KIND == 0 ? nullptr : sidx + npad;
-  const bool full_needed = tr.mode & 1;
+  const uint32_t npad;
+  const uint32_t* const sidx;
+  const uint32_t* const bpos;
+  const bool full_needed;
+  const uint64_t lt;   // lanes below this one
   Lz z;
-  z.level = tr.clevel; z.kind = KIND;
-  z.wsize = 1u << tr.window; z.maxdist = z.wsize - LOOKMIN; z.lbs = 1u << (tr.memlevel + 6);
-  z.good = c_cfg[z.level][0]; z.lazy = c_cfg[z.level][1]; z.nice = c_cfg[z.level][2]; z.chain = c_cfg[z.level][3];
-  z.n = sd.infl_len; z.p = 0; z.lookahead = 0; z.S = 0; z.block_start = 0;
-  z.match_start = 0; z.prev_match = 0; z.match_length = 2; z.prev_length = 2; z.match_available = 0;
-  z.last_lit = 0; z.nsym = 0;
-  LDS BitOut& b = s.b;
-  if (wave == 0) {
-    b.out = (GLOBAL uint8_t*)(A.out + tr.out_off); b.cap = tr.out_cap; b.pos = 0; b.bb = 0; b.bc = 0;
-    b.orig = (const GLOBAL uint8_t*)(A.file + sd.orig_off); b.clen = sd.comp_len;
-    b.shortcut = sd.comp_len > A.o.shortcut_len ? A.o.shortcut_len : 0;
-    b.eq_all = 0; b.eq_sc = 0; b.overflow = 0;
-  }
-  // fast and slow levels: a saving trial writes its whole symbol sequence at rp_syms (block k's
-  // symbols at sbase, the count of symbols in the blocks before it); a replaying trial reads one
-  const bool saving = KIND != 0 && (tr.mode & 4);
-  bool replay = KIND != 0 && (tr.mode & 8);
-  if (KIND == 2 && replay && (tr.mode & 16)) {
-    const uint32_t tlim = tr.x_lim < sd.infl_len ? (uint32_t)tr.x_lim : (uint32_t)sd.infl_len;   // entries present
-    // replay only if this trial's table agrees with the saver's on every entry the saver's parse
-    // read (bit 0 of a saved half: that half was read): then this trial's parse reads the same
-    // entries, step by step, and takes the same path.  A read compares the length and distance
-    // (the head-valid bit only matters with a length > 2, which it implies; the literal byte is
-    // the input's)
-    const GLOBAL uint64_t* mt = (const GLOBAL uint64_t*)(A.R + tr.r_off);   // .x low, .y high
-    const GLOBAL uint64_t* st = (const GLOBAL uint64_t*)(uintptr_t)tr.rp_tab;
-    bool same = true;
-    for (uint32_t p0 = 0; p0 < tlim && same; p0 += 256) {
-      bool d = false;
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const uint32_t p = p0 + 64u * (uint32_t)u + (uint32_t)lane;
-        if (p < tlim) {
-          const uint64_t sv = st[p], df = mt[p] ^ sv;
-          d |= ((sv & 1ull) && (df & 0xffffff00ull)) || ((sv >> 32) & 1ull && (df & 0xffffff0000000000ull));
-        }
-      }
-      same = __ballot(d) == 0;
-    }
-    replay = same;
-  }
-  uint32_t* const syms = saving || replay ? (uint32_t*)(uintptr_t)tr.rp_syms : A.syms + tr.sym_off;
-  // a saving slow trial records the match-table entries its parse reads (rp_tab, cleared first)
-  const bool rec = KIND == 2 && saving && (tr.mode & 32);
-  GLOBAL uint64_t* const rtab = (GLOBAL uint64_t*)(uintptr_t)tr.rp_tab;
-  if (rec && wave == 0) {
-    for (uint32_t p = (uint32_t)lane; p < sd.infl_len; p += 64) rtab[p] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the clears land before the records
-  }
+  bool saving = false, replay = false, rec = false;
+  uint32_t* syms = nullptr;
+  GLOBAL uint64_t* rtab = nullptr;
   uint32_t sbase = 0;            // symbols in the flushed blocks
   uint32_t saved_flags = 0;
   uint32_t run_len = 0, run_imp = 0;   // slow parses: longest match length any of its reads saw, longest
                                        // prev_length a lazy read improved (per lane, reduced at the end)
-  if (wave == 0) {
-    b.cyc_tree = b.cyc_emit = b.blocks = 0;
-    b.cyc_heap = b.cyc_scan = b.cyc_send = 0;
-  }
-  const uint64_t cstart = clock64();
-  const uint32_t rtstart = (uint32_t)__builtin_amdgcn_s_memrealtime();
-  if (wave == 0) init_block(s.f, lane);
+  uint64_t cstart = 0;
+  uint32_t rtstart = 0;
   uint32_t hazard = 0;
   // Symbols and block statistics are tallied straight into HBM (syms) and LDS (lfreq / dfreq).
   uint32_t state = ~0u;
   uint64_t fallbacks = 0, cyc_fb = 0;
   uint64_t csec[4] = {0, 0, 0, 0};   // diagnostics (ATZ_STEP_CLOCKS)
-  // zlib header (Z/deflate.c:738-759)
-  if (wave == 0) {
-    uint32_t header = (8u + ((uint32_t)(tr.window - 8) << 4)) << 8;
-    uint32_t lf = z.level < 2 ? 0 : z.level < 6 ? 1 : z.level == 6 ? 2 : 3;
-    header |= lf << 6;
-    header += 31 - (header % 31);
-    put_bits(b, stg, ((header >> 8) & 0xff) | ((header & 0xff) << 8), 16, lane);   // < 32 bits: no staging
-  }
   uint32_t nblk = 0;   // multi-wave: blocks handed to the flushers
-  if constexpr (MW) {
-    LDS MWPart& mw = *(LDS MWPart*)&shm.mw;
-    if (wave == 0) {
-      if (lane < MW_F) { mw.slot[lane].seq = 0; mw.fl[lane].cyc_tree = 0; mw.fl[lane].cyc_emit = 0;
-                        mw.fl[lane].cyc_heap = 0; mw.fl[lane].cyc_scan = 0; }
-      if (lane == 0) {
-        mw.ctl.next_emit = 0; mw.ctl.stop = 0; mw.ctl.parse_done = 0; mw.ctl.nblocks = 0;
-        mw.ctl.state = ~0u; mw.ctl.hazard = 0;
-      }
-    }
-    __syncthreads();
-    if (wave != 0)
-      trial_flusher(A, s, mw, tr, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, z.level, z.lbs, full_needed,
-                    wave - 1, lane);
-  }
-  if (wave == 0) {   // (the parse; every wave of a single-wave trial)
-  // fast and slow kinds: match-table entries of the positions around the parse window in an LDS
-  // ring; window slides (fill_window at the top of an iteration when lookahead < MIN_LOOKAHEAD)
-  // are a function of the iteration position, so any lane can evaluate them.
+  // the parse (wave 0): match-table ring, the stream's geometry; deflate_fast's holes and insertion bits
   LDS uint64_t* ring = nullptr;
-  if constexpr (KIND != 0) ring = (LDS uint64_t*)shm.ring;   // position & (RING_SLOW - 1); .x low, .y high
-  const GLOBAL uint64_t* Rt = (const GLOBAL uint64_t*)(A.R + tr.r_off);
-  const uint32_t n = z.n, wsz = z.wsize, maxd = z.maxdist, xlim = (uint32_t)tr.x_lim;
-  // fill_window never slides a stream of at most wsize + MAX_DIST bytes (Z/deflate.c:1419-1451:
-  // strstart stays below it), so S is 0 throughout and the NIL-after-slide checks drop out (wave-
-  // uniform: the walks skip them with a scalar branch)
-  const bool noslide = ATZ_NOSLIDE_PATH && n <= wsz + maxd;
-  auto S_iter = [&](uint32_t S0, uint32_t q) -> uint32_t {   // S at an iteration at q >= one with S0
-    uint32_t Sx = S0;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      const bool exh = n <= Sx + 2u * wsz;
-      const bool slide = exh ? (q + LOOKMIN > n && q >= Sx + wsz + maxd) : (q > Sx + wsz + maxd);
-      if (slide) Sx += wsz;
-    }
-    return Sx;
-  };
-  // ring: chunks of 64 entries below `hi` are resident; the chunk at `hi` is in flight in pf
+  const GLOBAL uint64_t* Rt = nullptr;
+  uint32_t n = 0, wsz = 0, maxd = 0, xlim = 0;
+  bool noslide = false;
   uint32_t hi = 0;
   uint64_t pf = 0;
-  if (KIND != 0 && n && !replay) pf = Rt[lane];
+  LDS uint32_t* holes = nullptr;
+  LDS uint32_t* ins = nullptr;
+
+  __device__ __forceinline__ TrialRun(const SweepArgs& A_, SH& shm_, int lane_)
+      : A(A_), shm(shm_), lane(lane_), wave(MW ? (int)(threadIdx.x >> 6) : 0), s(*(LDS TrialShared*)&shm_.t),
+        stg((LDS uint32_t*)shm_.ring), b(s.b), t(blockIdx.x), tr(A_.trials[t]), sd(A_.streams[tr.stream]),
+        in(A_.infl + sd.infl_off), npad((uint32_t)((sd.infl_len + 63) & ~63ull)),
+        sidx(KIND == 0 ? nullptr : A_.chains + tr.chain_off), bpos(KIND == 0 ? nullptr : sidx + npad),
+        full_needed(tr.mode & 1), lt(lane_ ? (~0ull >> (64 - lane_)) : 0ull) {
+    z.level = tr.clevel; z.kind = KIND;
+    z.wsize = 1u << tr.window; z.maxdist = z.wsize - LOOKMIN; z.lbs = 1u << (tr.memlevel + 6);
+    z.good = c_cfg[z.level][0]; z.lazy = c_cfg[z.level][1]; z.nice = c_cfg[z.level][2]; z.chain = c_cfg[z.level][3];
+    z.n = sd.infl_len; z.p = 0; z.lookahead = 0; z.S = 0; z.block_start = 0;
+    z.match_start = 0; z.prev_match = 0; z.match_length = 2; z.prev_length = 2; z.match_available = 0;
+    z.last_lit = 0; z.nsym = 0;
+    if (wave == 0) {
+      b.out = (GLOBAL uint8_t*)(A.out + tr.out_off); b.cap = tr.out_cap; b.pos = 0; b.bb = 0; b.bc = 0;
+      b.orig = (const GLOBAL uint8_t*)(A.file + sd.orig_off); b.clen = sd.comp_len;
+      b.shortcut = sd.comp_len > A.o.shortcut_len ? A.o.shortcut_len : 0;
+      b.eq_all = 0; b.eq_sc = 0; b.overflow = 0;
+    }
+    // fast and slow levels: a saving trial writes its whole symbol sequence at rp_syms (block k's
+    // symbols at sbase, the count of symbols in the blocks before it); a replaying trial reads one
+    saving = KIND != 0 && (tr.mode & 4);
+    replay = KIND != 0 && (tr.mode & 8);
+    if (KIND == 2 && replay && (tr.mode & 16)) {
+      const uint32_t tlim = tr.x_lim < sd.infl_len ? (uint32_t)tr.x_lim : (uint32_t)sd.infl_len;   // entries present
+      // replay only if this trial's table agrees with the saver's on every entry the saver's parse
+      // read (bit 0 of a saved half: that half was read): then this trial's parse reads the same
+      // entries, step by step, and takes the same path.  A read compares the length and distance
+      // (the head-valid bit only matters with a length > 2, which it implies; the literal byte is
+      // the input's)
+      const GLOBAL uint64_t* mt = (const GLOBAL uint64_t*)(A.R + tr.r_off);   // .x low, .y high
+      const GLOBAL uint64_t* st = (const GLOBAL uint64_t*)(uintptr_t)tr.rp_tab;
+      bool same = true;
+      for (uint32_t p0 = 0; p0 < tlim && same; p0 += 256) {
+        bool d = false;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t p = p0 + 64u * (uint32_t)u + (uint32_t)lane;
+          if (p < tlim) {
+            const uint64_t sv = st[p], df = mt[p] ^ sv;
+            d |= ((sv & 1ull) && (df & 0xffffff00ull)) || ((sv >> 32) & 1ull && (df & 0xffffff0000000000ull));
+          }
+        }
+        same = __ballot(d) == 0;
+      }
+      replay = same;
+    }
+    syms = saving || replay ? (uint32_t*)(uintptr_t)tr.rp_syms : A.syms + tr.sym_off;
+    // a saving slow trial records the match-table entries its parse reads (rp_tab, cleared first)
+    rec = KIND == 2 && saving && (tr.mode & 32);
+    rtab = (GLOBAL uint64_t*)(uintptr_t)tr.rp_tab;
+    if (rec && wave == 0) {
+      for (uint32_t p = (uint32_t)lane; p < sd.infl_len; p += 64) rtab[p] = 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the clears land before the records
+    }
+    if (wave == 0) {
+      b.cyc_tree = b.cyc_emit = b.blocks = 0;
+      b.cyc_heap = b.cyc_scan = b.cyc_send = 0;
+    }
+    cstart = clock64();
+    rtstart = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    if (wave == 0) init_block(s.f, lane);
+    // zlib header (Z/deflate.c:738-759)
+    if (wave == 0) {
+      uint32_t header = (8u + ((uint32_t)(tr.window - 8) << 4)) << 8;
+      uint32_t lf = z.level < 2 ? 0 : z.level < 6 ? 1 : z.level == 6 ? 2 : 3;
+      header |= lf << 6;
+      header += 31 - (header % 31);
+      put_bits(b, stg, ((header >> 8) & 0xff) | ((header & 0xff) << 8), 16, lane);   // < 32 bits: no staging
+    }
+  }
+
+  static constexpr uint32_t ins_mask() { return SH::INS_BITS / 32 - 1; }
+  __device__ __forceinline__ bool ins_get(uint32_t q) const { return (ins[(q >> 5) & ins_mask()] >> (q & 31)) & 1u; }
+  // S at an iteration at q >= one with S0
+  __device__ __forceinline__ uint32_t S_iter(uint32_t S0, uint32_t q) const {
+      uint32_t Sx = S0;
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const bool exh = n <= Sx + 2u * wsz;
+        const bool slide = exh ? (q + LOOKMIN > n && q >= Sx + wsz + maxd) : (q > Sx + wsz + maxd);
+        if (slide) Sx += wsz;
+      }
+      return Sx;
+  }
   // multi-wave: hand the finished block to its flusher; false when the trial is already decided
-  auto publish = [&](int last) -> bool {
-    if constexpr (MW) {
-      LDS MWPart& mw = *(LDS MWPart*)&shm.mw;
-      const uint32_t f = nblk % (uint32_t)MW_F;
-      LDS MWSlot& sl = mw.slot[f];
-      for (;;) {
-        if (ld_acq(mw.ctl.stop)) return false;
-        if (ld_acq(sl.seq) == 0) break;
-        __builtin_amdgcn_s_sleep(1);
+  __device__ __forceinline__ bool publish(int last) {
+      if constexpr (MW) {
+        LDS MWPart& mw = *(LDS MWPart*)&shm.mw;
+        const uint32_t f = nblk % (uint32_t)MW_F;
+        LDS MWSlot& sl = mw.slot[f];
+        for (;;) {
+          if (ld_acq(mw.ctl.stop)) return false;
+          if (ld_acq(sl.seq) == 0) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        for (int i = lane; i < (NLC + 1) / 2; i += 64) sl.f.lfreq2[i] = s.f.lfreq2[i];
+        for (int i = lane; i < NDC / 2; i += 64) sl.f.dfreq2[i] = s.f.dfreq2[i];
+        if (lane == 0) {
+          sl.block_start = (int64_t)z.block_start; sl.p = z.p; sl.S = z.S;
+          sl.last_lit = z.last_lit; sl.sbase = sbase; sl.last = (uint32_t)last;
+        }
+        st_rel(sl.seq, nblk + 1, lane);   // after the wave's symbol stores and the slot writes
+        nblk++;
+        init_block(s.f, lane);
+        sbase += z.last_lit;
+        z.last_lit = 0;
+        z.block_start = z.p;
       }
-      for (int i = lane; i < (NLC + 1) / 2; i += 64) sl.f.lfreq2[i] = s.f.lfreq2[i];
-      for (int i = lane; i < NDC / 2; i += 64) sl.f.dfreq2[i] = s.f.dfreq2[i];
-      if (lane == 0) {
-        sl.block_start = (int64_t)z.block_start; sl.p = z.p; sl.S = z.S;
-        sl.last_lit = z.last_lit; sl.sbase = sbase; sl.last = (uint32_t)last;
-      }
-      st_rel(sl.seq, nblk + 1, lane);   // after the wave's symbol stores and the slot writes
-      nblk++;
-      init_block(s.f, lane);
+      return true;
+  }
+  __device__ __forceinline__ void FLUSH(int last) {
+      hazard |= uni(flush_block(s, *(LDS TreeScratch*)shm.ring, b, (const GLOBAL uint32_t*)syms + ((saving || replay) ? sbase : 0u),
+                                (const GLOBAL uint8_t*)in, (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last,
+                                A.o, tr.best_ident, full_needed, lane));
       sbase += z.last_lit;
       z.last_lit = 0;
       z.block_start = z.p;
-    }
-    return true;
-  };
-  auto FLUSH = [&](int last) {
-    hazard |= uni(flush_block(s, *(LDS TreeScratch*)shm.ring, b, (const GLOBAL uint32_t*)syms + ((saving || replay) ? sbase : 0u),
-                              (const GLOBAL uint8_t*)in, (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last,
-                              A.o, tr.best_ident, full_needed, lane));
-    sbase += z.last_lit;
-    z.last_lit = 0;
-    z.block_start = z.p;
-    if (KIND != 0 && !replay) {   // the tree scratch overlaid the ring: reload its resident chunks
-      for (uint32_t c0 = hi >= RING_SLOW ? hi - RING_SLOW : 0u; c0 < hi; c0 += 64) {
-        const uint32_t pos = c0 + (uint32_t)lane;
-        if (pos < n) ring[pos & (RING_SLOW - 1)] = Rt[pos];
+      if (KIND != 0 && !replay) {   // the tree scratch overlaid the ring: reload its resident chunks
+        for (uint32_t c0 = hi >= RING_SLOW ? hi - RING_SLOW : 0u; c0 < hi; c0 += 64) {
+          const uint32_t pos = c0 + (uint32_t)lane;
+          if (pos < n) ring[pos & (RING_SLOW - 1)] = Rt[pos];
+        }
       }
-    }
-  };
+  }
   // a block is full: flush it (single wave) or hand it over (multi-wave); returns the early-exit state
-  auto FLUSH0 = [&]() -> uint32_t {
-    if constexpr (MW) {
-      return publish(0) ? ~0u : TR_DECIDED;
-    } else {
-      FLUSH(0);
-      return uni(early_exit(b, A.o, tr.best_ident, full_needed));
+  __device__ __forceinline__ uint32_t FLUSH0() {
+      if constexpr (MW) {
+        return publish(0) ? ~0u : TR_DECIDED;
+      } else {
+        FLUSH(0);
+        return uni(early_exit(b, A.o, tr.best_ident, full_needed));
+      }
+  }
+
+  __device__ __forceinline__ void parse_setup() {
+    // fast and slow kinds: match-table entries of the positions around the parse window in an LDS
+    // ring; window slides (fill_window at the top of an iteration when lookahead < MIN_LOOKAHEAD)
+    // are a function of the iteration position, so any lane can evaluate them.
+    if constexpr (KIND != 0) ring = (LDS uint64_t*)shm.ring;   // position & (RING_SLOW - 1); .x low, .y high
+    Rt = (const GLOBAL uint64_t*)(A.R + tr.r_off);
+    n = z.n; wsz = z.wsize; maxd = z.maxdist; xlim = (uint32_t)tr.x_lim;
+    // fill_window never slides a stream of at most wsize + MAX_DIST bytes (Z/deflate.c:1419-1451:
+    // strstart stays below it), so S is 0 throughout and the NIL-after-slide checks drop out (wave-
+    // uniform: the walks skip them with a scalar branch)
+    noslide = ATZ_NOSLIDE_PATH && n <= wsz + maxd;
+    // ring: chunks of 64 entries below `hi` are resident; the chunk at `hi` is in flight in pf
+    if (KIND != 0 && n && !replay) pf = Rt[lane];
+  }
+
+  // deflate_stored (Z/deflate.c:1564-1619)
+  __device__ __forceinline__ void parse_stored() {
+  uint64_t max_block = 0xffff;
+  if (max_block > 4ull * z.lbs - 5) max_block = 4ull * z.lbs - 5;
+  for (;;) {
+    if (z.lookahead <= 1) { fill(z); if (z.lookahead == 0) break; }
+    z.p += z.lookahead;
+    z.lookahead = 0;
+    const uint32_t max_start = z.block_start + (uint32_t)max_block;
+    if (z.p == 0 || z.p >= max_start) {
+      z.lookahead = z.p - max_start;
+      z.p = max_start;
+      state = FLUSH0();
+      if (state != ~0u) break;
+    }
+    if (z.p - z.block_start >= z.maxdist) {
+      state = FLUSH0();
+      if (state != ~0u) break;
+    }
+  }
+  }
+
+  __device__ __forceinline__ void parse_replay() {
+  // Symbol replay.  The sequence saved by a trial of this stream at the same (level, window) and
+  // another memLevel is this trial's own: the host proved that no chain walk of either memLevel
+  // reaches its budget (every bucket holds at most B + 1 positions, B = max_chain for deflate_fast,
+  // whose prev_length never reaches good_match, and max_chain / 4 for deflate_slow), so each walk
+  // examines the same-trigram positions in the same order (other hashes in a chain never match:
+  // their first two bytes differ) and returns the same match; deflate_fast's insertions follow the
+  // match lengths, and neither parse depends on lit_bufsize.  Only the blocks differ: the symbols
+  // are tallied into this memLevel's blocks of lit_bufsize - 1, each flushed at the position after
+  // its last symbol (deflate_slow tallies a literal at iteration pos + 1, a match when strstart
+  // reaches its end; deflate_fast flushes after strstart moved past the symbol); deflate_slow's
+  // end-of-input pending literal is tallied without a flush check (Z/deflate.c:1842-1846).
+  // A replay checked against a table prefix (x_lim < n) stops where the parse would read past it.
+  const GLOBAL uint32_t* sv = (const GLOBAL uint32_t*)syms;
+  const uint32_t nsv = tr.rp_nsym;
+  const bool endlit = (tr.rp_flags & 2u) != 0;
+  saved_flags |= 4;
+  uint32_t k = 0, pos = 0;
+  while (k < nsv) {
+    const uint32_t cnt = nsv - k < 64u ? nsv - k : 64u;
+    const bool valid = (uint32_t)lane < cnt;
+    const uint32_t v = valid ? sv[k + (uint32_t)lane] : 0u;
+    const uint32_t len = valid ? ((v >> 8) ? (v & 0xffu) + 3u : 1u) : 0u;
+    const uint32_t incl = wave_incl_scan(len);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (xlim < n && pos + tot + 2u > xlim) { state = TR_NEED_R; z.p = pos; break; }
+    uint32_t base = 0;
+    while (base < cnt) {
+      const uint32_t room = z.lbs - 1u - z.last_lit;
+      const uint32_t seg_end = cnt - base < room ? cnt : base + room;
+      if ((uint32_t)lane >= base && (uint32_t)lane < seg_end) {
+        if (v >> 8) {
+          const uint32_t lc = 257u + len_code(v & 0xffu), dc = dist_code((v >> 8) - 1u);
+          __hip_atomic_fetch_add(&s.f.lfreq2[lc >> 1], 1u << (16 * (lc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&s.f.dfreq2[dc >> 1], 1u << (16 * (dc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          __hip_atomic_fetch_add(&s.f.lfreq2[v >> 1], 1u << (16 * (v & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      z.last_lit += seg_end - base;
+      z.nsym += seg_end - base;
+      if (z.last_lit == z.lbs - 1u && !(endlit && k + seg_end == nsv)) {
+        z.p = pos + (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)seg_end - 1);
+        state = FLUSH0();
+        if (state != ~0u) break;
+      }
+      base = seg_end;
+    }
+    if (state != ~0u) break;
+    pos += tot;
+    k += cnt;
+  }
+  if (state == ~0u) {
+    z.p = n;
+    z.S = 0;
+  }
+  }
+
+  // deflate_fast: whether the table's step at path node x may differ from deflate_fast's own walk
+  __device__ __forceinline__ bool fast_node_bad(bool onp, uint32_t x, uint32_t ex, uint32_t ey, uint32_t Sx, uint32_t sxl) {
+  bool bad = false;
+  if (onp && x + 3u <= n) {
+    const uint32_t hl = holes[(ey >> 1) & (HOLE_SLOTS - 1)];
+    bool exact = hl == 0 || hl - 1u < x - (ey >> 16);
+    if (!exact && !((ey >> 12) & 1u)) {
+      // Skipped nodes only shrink the visited set -- except at the MAX_DIST edge: deflate_fast
+      // walks its hash head at distance MAX_DIST (Z/deflate.c:1660) but later chain nodes only
+      // above it (Z/deflate.c:1227), so when holes above it made a hole the table's head, the
+      // node at exactly x - MAX_DIST can be examined by deflate_fast and not by the table walk.
+      // Such a node is resolved by the exact walk below.
+      const uint32_t q0 = x - maxd;
+      const uint32_t hb = tr.memlevel + 7u, hs = (hb + 2u) / 3u, hm = (1u << hb) - 1u;
+      const bool edge = x > maxd && q0 > Sx &&
+                        ((((uint32_t)in[q0] << (2u * hs)) ^ ((uint32_t)in[q0 + 1] << hs) ^ in[q0 + 2]) & hm) ==
+                        ((((uint32_t)in[x] << (2u * hs)) ^ ((uint32_t)in[x + 1] << hs) ^ in[x + 2]) & hm);
+      if (edge) exact = false;
+      else if ((ex >> 23) <= 2) exact = true;
+      else {
+        const uint32_t wpos = x - ((ex >> 8) & 0x7fffu);
+        exact = wpos > Sx && ins_get(wpos);
+      }
+    } else if (!exact && ATZ_VISITED_CHECK && z.chain <= ATZ_VISITED_MAX) {
+      // the walk spent its budget and a hole shares the slot: the entry is still exact when
+      // every node the walk visited (the bucket entries below x down to the lowest visited
+      // one, at most `chain` of them) was inserted -- deflate_fast's chain then starts with
+      // the same nodes and spends the same budget on them
+      const uint32_t lo = x - (ey >> 16);
+      const int32_t si = (int32_t)sxl;
+      bool ok = true, stop = false;
+      for (int32_t k = si - 1; ok && !stop && k > si - 1 - (int32_t)z.chain; k -= 4) {
+        uint32_t e4[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) e4[u] = k - u >= 0 ? bpos[k - u] : BUCKET_FIRST;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (!ok || stop || k - u <= si - 1 - (int32_t)z.chain) break;
+          const uint32_t pos = e4[u] & ~BUCKET_FIRST;
+          if (k - u < 0 || pos < lo) { stop = true; break; }
+          ok = pos > Sx && ins_get(pos);
+          if (e4[u] & BUCKET_FIRST) stop = true;
+        }
+      }
+      exact = ok;
+    }
+    bad = !exact;
+  }
+    return bad;
+  }
+
+  // deflate_fast's longest_match at f over the INSERTED same-hash positions (Z/deflate.c:1148-1289):
+  // 64 bucket entries per step, lanes test insertion and compare bytes in parallel; the walk order is
+  // the lane order.  ml / ms: the match (0: none).
+  __device__ __forceinline__ void fast_exact_walk(uint32_t f, uint32_t Sf, uint32_t la, uint32_t sxl, int fln,
+                                                  uint32_t& ml, uint32_t& ms) {
+    const uint32_t si = uni((uint32_t)__builtin_amdgcn_readlane((int)sxl, fln));
+    bool done = false;
+    bool head_done = false, hv = false, won = false;
+    uint32_t examined = 0, best = 2, win = 0;
+    const uint32_t limit = f > maxd ? f - maxd : 0u;   // later nodes only while > limit
+    const uint32_t cap = n - f < 258u ? n - f : 258u;
+    const uint32_t nicec = z.nice < la ? z.nice : la;   // <= cap
+    // lane l reads bucket entry top - l; the first chunk starts at f's own entry (lane 0), whose
+    // first-of-bucket flag says whether f has a chain at all
+    int32_t top = (int32_t)si;
+    int skip = 1;
+    while (!done) {
+      const int32_t k = top - lane;
+      const uint32_t e = k >= 0 ? bpos[k] : BUCKET_FIRST;
+      if (skip && (uni((uint32_t)__builtin_amdgcn_readlane((int)e, 0)) & BUCKET_FIRST)) break;   // first of its bucket: no chain
+      const uint64_t fm = __ballot((e & BUCKET_FIRST) != 0 && lane >= skip);
+      const int flane = fm ? __ffsll((unsigned long long)fm) - 1 : 64;   // bucket's first entry: last node
+      const uint32_t qc = e & ~BUCKET_FIRST;
+      const bool insd = lane >= skip && lane <= flane && k >= 0 && ins_get(qc);
+      const uint64_t im = __ballot(insd);
+      int head_lane = -1, from = 0;
+      if (!head_done) {
+        if (!im) {   // no inserted node in this chunk yet
+          if (flane < 64) break;
+          top -= 64;
+          skip = 0;
+          continue;
+        }
+        head_lane = __ffsll((unsigned long long)im) - 1;
+        const uint32_t hh = (uint32_t)__builtin_amdgcn_readlane((int)qc, head_lane);
+        head_done = true;
+        hv = hh > Sf && f - hh <= maxd;   // zlib calls longest_match only then
+        if (!hv) break;
+        from = head_lane;
+      }
+      // the walk stops at the first inserted node <= limit (the head is always examined)
+      const uint64_t sm = __ballot(insd && lane >= from && lane != head_lane && qc <= limit);
+      const int slane = sm ? __ffsll((unsigned long long)sm) - 1 : 64;
+      bool cand = insd && lane >= from && lane < slane;
+      const uint32_t room = z.chain - examined;
+      cand = cand && (uint32_t)__popcll(__ballot(cand) & lt) < room;
+      const uint64_t cm = __ballot(cand);
+      examined += (uint32_t)__popcll(cm);
+      // match lengths capped at nice (16 bytes per round trip); the first candidate reaching
+      // nice ends the walk, so capped lengths decide the winner
+      uint32_t len = 0;
+      bool go = cand;
+      while (__ballot(go)) {
+        if (go) {
+          // 16 bytes per round trip: 5 aligned dword loads per side (stream bases are 256-byte aligned)
+          const uint32_t run = match16((const GLOBAL uint32_t*)in, qc + len, f + len, nullptr, 0);
+          const uint32_t left = nicec - len;
+          len += run < left ? run : left;
+          go = run == 16 && len < nicec;
+        }
+      }
+      const uint64_t nm = __ballot(cand && len >= nicec);
+      if (nm) {
+        const int wl = __ffsll((unsigned long long)nm) - 1;
+        win = (uint32_t)__builtin_amdgcn_readlane((int)qc, wl);
+        best = uni(common_len(in, win, f, nicec, cap, lane));   // full length of the winner
+        won = true;
+        break;
+      }
+      uint32_t mx = cand ? len : 0u;
+      for (int d = 32; d >= 1; d >>= 1) { const uint32_t o2 = __shfl_xor(mx, d, 64); mx = mx > o2 ? mx : o2; }
+      mx = uni(mx);
+      if (mx > best) {
+        const uint64_t xm = __ballot(cand && len == mx);
+        win = (uint32_t)__builtin_amdgcn_readlane((int)qc, __ffsll((unsigned long long)xm) - 1);
+        best = mx;
+        won = true;
+      }
+      done = examined >= z.chain || slane < 64 || flane < 64;
+      top -= 64;
+      skip = 0;
+    }
+    if (hv && won) {
+      ml = best <= la ? best : la;
+      ms = win;
+    }
+  }
+
+  __device__ __forceinline__ void parse_fast() {
+  // deflate_fast (Z/deflate.c:1628-1722), lane-parallel.  Every deflate_fast iteration starts in
+  // the same state, so a window takes the match table's step at each of its 64 positions in
+  // lanes, the scalar unit follows the parse path through them, and the path's insertion state
+  // and symbols are written lane-parallel.  A table entry is the walk over ALL same-hash
+  // positions; deflate_fast walks the INSERTED ones (interiors of matches longer than
+  // max_insert_length are skipped: "holes"), so every path node is checked: the entry is exact
+  // unless a hole with its hash slot lies in the walked range [lowest visited node, p) AND it
+  // can matter -- skipped nodes only shrink the visited set, so a walk that ended by nice_match
+  // or by the end of the chain keeps its winner W if W itself was inserted (and with no winner
+  // the step emits a literal either way); only a walk that spent its budget with nodes left can
+  // see new nodes (bit 12).  The first node that fails the check is walked exactly over the
+  // inserted positions and the window ends there.  holes[] keeps per slot the latest hole; the
+  // window's own holes are entered before the check, so a hole behind the node only makes the
+  // check conservative (slot collisions likewise).
+  holes = (LDS uint32_t*)shm.holes;
+  ins = (LDS uint32_t*)shm.ins;   // insertion bits, position mod SH::INS_BITS
+  for (int i = lane; i < (int)HOLE_SLOTS; i += 64) holes[i] = 0;
+  // insertion bits and holes of the positions [lo, hi) covered by path nodes; cover(p) gives the
+  // node y <= p covering p and its match length (0: literal).  cover runs with all lanes active
+  // (it may shuffle: a lane outside EXEC would read as 0).
+  auto span_set = [&](uint32_t lo, uint32_t hi2, auto cover) {
+    for (uint32_t c0 = lo & ~63u; c0 < hi2; c0 += 64) {
+      const uint32_t p = c0 + (uint32_t)lane;
+      const bool insp = p >= lo && p < hi2;
+      bool insd = false, hole = false;
+      uint32_t y, Ly;
+      cover(p, y, Ly);
+      if (insp) {
+        if (p == y) insd = p + 3u <= n;
+        else if (Ly <= z.lazy && y + Ly + 3u <= n) insd = true;
+        else hole = p + 3u <= n;
+      }
+      const uint64_t bits = __ballot(insd), sm = __ballot(insp);
+      if (lane < 2) {
+        const uint32_t sh = 32u * (uint32_t)lane;
+        const uint32_t m = (uint32_t)(sm >> sh), bv = (uint32_t)(bits >> sh);
+        if (m) {
+          LDS uint32_t& w = ins[((c0 + sh) >> 5) & ins_mask()];
+          w = (w & ~m) | (bv & m);
+        }
+      }
+      if (hole) {
+        const uint32_t slot = ((uint32_t)(ring[p & (RING_SLOW - 1)] >> 32) >> 1) & (HOLE_SLOTS - 1);
+        __hip_atomic_fetch_max(&holes[slot], p + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
   };
-  if constexpr (KIND == 0) {
-    // deflate_stored (Z/deflate.c:1564-1619)
-    uint64_t max_block = 0xffff;
-    if (max_block > 4ull * z.lbs - 5) max_block = 4ull * z.lbs - 5;
+  // one symbol, tallied by the scalar unit; returns true when the block is full
+  auto tally1 = [&](uint32_t v) -> bool {
+    if (lane == 0) {
+      syms[(saving || MW ? sbase : 0u) + z.last_lit] = v;
+      if (v >> 8) {
+        __hip_atomic_fetch_add(&s.f.lfreq2[(257u + len_code(v & 0xffu)) >> 1], 1u << (16 * ((257u + len_code(v & 0xffu)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&s.f.dfreq2[(dist_code((v >> 8) - 1u)) >> 1], 1u << (16 * ((dist_code((v >> 8) - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    z.last_lit++;
+    z.nsym++;
+    return z.last_lit == z.lbs - 1u;
+  };
+  uint32_t q = 0, Sb = 0;
+  bool need = false;
+  while (q < n) {
+    const uint32_t wb = q, bal = wb & ~63u;
+    uint64_t t0 = STEP_CLOCK();
+    while (hi < bal + RING_SLOW) {
+      ring[(hi + lane) & (RING_SLOW - 1)] = pf;
+      hi += 64;
+      if (hi < n) pf = Rt[hi + lane];
+    }
+    Sb = S_iter(Sb, wb);
+    if (ATZ_STEP_CLOCKS) { (void)ring[wb & (RING_SLOW - 1)]; __builtin_amdgcn_s_waitcnt(0); }
+    uint64_t t1 = STEP_CLOCK(); csec[0] += t1 - t0; t0 = t1;
+    // ---- the table's step at x = wb + lane: wt 0 none (x >= n), 1 literal, 2 match, 3 needs R >= x_lim
+    const uint32_t x = wb + lane;
+    // x's bucket index, loaded now and read only by the node checks and the exact walks below (its
+    // latency hides behind the window's own work instead of opening a walk)
+    const uint32_t sxl = x < n ? sidx[x] : 0u;
+    uint32_t wt = 0, L = 0, D = 0, ex = 0, ey = 0, Sx = Sb;
+    if (x < n) {
+      if (x >= xlim) wt = 3;
+      else {
+        const uint64_t e64 = ring[x & (RING_SLOW - 1)];
+        ex = (uint32_t)e64; ey = (uint32_t)(e64 >> 32);
+        if (!noslide) Sx = S_iter(Sb, x);
+        bool hv = x + 3u <= n && (ey & 1u);
+        if (!noslide && hv && Sx != 0 && x - Sx <= maxd) {   // hash_head == S is NIL after a slide
+          const uint32_t si = sidx[x];
+          hv = (bpos[si] & BUCKET_FIRST) || (bpos[si - 1] & ~BUCKET_FIRST) != Sx;
+        }
+        const uint32_t len = ex >> 23;
+        if (hv && len > 2) { wt = 2; L = len; D = (ex >> 8) & 0x7fffu; }
+        else wt = 1;
+      }
+    }
+    // ---- follow the parse path through the window
+    const uint64_t Am = __ballot(wt == 1), Nm = __ballot(wt == 3);
+    t1 = STEP_CLOCK(); csec[1] += t1 - t0; t0 = t1;
+    const uint32_t rel = wt == 1 ? run_end_rel(Am, lane) : wt == 2 ? (uint32_t)lane + L : 0xffffu;
+    const WinPath wp = follow_path(rel, Nm, n - wb < 64 ? n - wb : 64u);
+    bool onp;
+    uint32_t mab_unused;
+    path_lane(wp, Am, 0, lane, onp, mab_unused);
+    const uint64_t P = __ballot(onp);
+    need = wp.need;
+    const uint32_t qn = wb + wp.end;
+    const uint32_t last = P ? wb + 63u - (uint32_t)__builtin_clzll(P) : wb;
+    // ---- insertion state of the path, then the check of its nodes
+    t1 = STEP_CLOCK(); csec[2] += t1 - t0; t0 = t1;
+    if (qn > wb)
+      span_set(wb, qn, [&](uint32_t p, uint32_t& y, uint32_t& Ly) {
+        const uint32_t i = p - wb;   // huge for p < wb (such lanes are outside the span)
+        uint32_t yl = last - wb;
+        if (i < 64) yl = 63u - (uint32_t)__builtin_clzll(P & (~0ull >> (63 - i)));
+        y = wb + yl;
+        Ly = (uint32_t)__shfl((int)L, (int)yl, 64);
+      });
+#if ATZ_STEP_SPLIT
+    t1 = STEP_CLOCK(); csec[0] += t1 - t0; t0 = t1;   // (diagnostics: span_set counted with refill)
+#endif
+    const bool bad = fast_node_bad(onp, x, ex, ey, Sx, sxl);
+    // Bad nodes are resolved one at a time by an exact walk.  When the walk's length equals the
+    // table's (or both give a literal), the parse path is unchanged: the node keeps its place on
+    // the path (with the walk's distance) and the window goes on to its next bad node.  Only a
+    // different length ends the window there.
+    uint64_t badm = __ballot(bad);
+    uint64_t donem = 0;   // path nodes tallied so far
+    uint32_t Dx = D;      // this lane's match distance (an exact walk may replace the table's)
+    bool restart = false;
+    uint32_t qnext = qn;
     for (;;) {
-      if (z.lookahead <= 1) { fill(z); if (z.lookahead == 0) break; }
-      z.p += z.lookahead;
-      z.lookahead = 0;
-      const uint32_t max_start = z.block_start + (uint32_t)max_block;
-      if (z.p == 0 || z.p >= max_start) {
-        z.lookahead = z.p - max_start;
-        z.p = max_start;
-        state = FLUSH0();
-        if (state != ~0u) break;
+      // ---- tally the committed nodes' symbols lane-parallel, in position order
+      const uint64_t Pc = (badm ? P & ((1ull << __builtin_ctzll(badm)) - 1ull) : P) & ~donem;
+      {
+        const bool mine = (Pc >> lane) & 1ull;
+        const uint32_t o = (uint32_t)__popcll(Pc & lt);
+        const uint32_t T = (uint32_t)__popcll(Pc);
+        z.nsym += T;
+        uint32_t base = 0;
+        while (base < T) {
+          const uint32_t room = z.lbs - 1u - z.last_lit;
+          const uint32_t seg_end = T - base < room ? T : base + room;
+          if (mine && o >= base && o < seg_end) {
+            uint32_t v;
+            if (wt == 2) {
+              v = (Dx << 8) | (L - 3u);
+              __hip_atomic_fetch_add(&s.f.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_fetch_add(&s.f.dfreq2[(dist_code(Dx - 1u)) >> 1], 1u << (16 * ((dist_code(Dx - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+              v = ex & 0xffu;
+              __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            syms[(saving || MW ? sbase : 0u) + z.last_lit + (o - base)] = v;
+          }
+          z.last_lit += seg_end - base;
+          if (z.last_lit == z.lbs - 1u) {   // flush after the node tallied last: strstart past its step
+            const uint64_t om = __ballot(mine && o == seg_end - 1u);
+            const int ol = (int)__builtin_ctzll(om);
+            const uint32_t fx = (uint32_t)__builtin_amdgcn_readlane((int)x, ol);
+            const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)L, ol);
+            z.p = fx + (fl ? fl : 1u);
+            z.S = S_iter(Sb, fx);
+            state = FLUSH0();
+            if (state != ~0u) break;
+          }
+          base = seg_end;
+        }
       }
-      if (z.p - z.block_start >= z.maxdist) {
-        state = FLUSH0();
-        if (state != ~0u) break;
+      donem |= Pc;
+      if (state != ~0u || !badm) break;
+      // ---- the first node that may differ: deflate_fast's longest_match over the INSERTED
+      // same-hash positions (Z/deflate.c:1148-1289): 64 bucket entries per step, lanes test
+      // insertion and compare bytes in parallel; the walk order is the lane order.
+      fallbacks++;
+      const uint64_t cf0 = STEP_CLOCK();
+      const int fln = __builtin_ctzll(badm);
+      const uint32_t f = wb + (uint32_t)fln;
+      const uint32_t Sf = S_iter(Sb, f);
+      const uint32_t la = n - f < LOOKMIN ? n - f : LOOKMIN;   // lookahead (>= 258 stands for more)
+      uint32_t ml = 0, ms = 0;
+      fast_exact_walk(f, Sf, la, sxl, fln, ml, ms);
+      cyc_fb += STEP_CLOCK() - cf0;
+      const uint32_t twt = uni((uint32_t)__builtin_amdgcn_readlane((int)wt, fln));
+      const uint32_t tL = uni((uint32_t)__builtin_amdgcn_readlane((int)L, fln));
+      if (ml >= 3 ? (twt == 2 && tL == ml) : twt == 1) {   // same step: the path stands
+        if (ml >= 3 && lane == fln) Dx = f - ms;
+        badm &= badm - 1ull;
+        continue;
       }
+      // the path changes at f: its exact step, then a new window after it
+      fallbacks += 1ull << 32;   // diagnostics: walks that changed the path (high half)
+      const uint32_t step = ml >= 3 ? ml : 1u;
+      span_set(f, f + step, [&](uint32_t p, uint32_t& y, uint32_t& Ly) { y = f; Ly = ml >= 3 ? ml : 0u; });
+      const bool full = tally1(ml >= 3 ? (((f - ms) << 8) | (ml - 3u)) : (uint32_t)in[f]);
+      if (full) {
+        z.p = f + step;
+        z.S = Sf;
+        state = FLUSH0();
+      }
+      qnext = f + step;
+      restart = true;
+      break;
     }
-  } else if (replay) {
-    // Symbol replay.  The sequence saved by a trial of this stream at the same (level, window) and
-    // another memLevel is this trial's own: the host proved that no chain walk of either memLevel
-    // reaches its budget (every bucket holds at most B + 1 positions, B = max_chain for deflate_fast,
-    // whose prev_length never reaches good_match, and max_chain / 4 for deflate_slow), so each walk
-    // examines the same-trigram positions in the same order (other hashes in a chain never match:
-    // their first two bytes differ) and returns the same match; deflate_fast's insertions follow the
-    // match lengths, and neither parse depends on lit_bufsize.  Only the blocks differ: the symbols
-    // are tallied into this memLevel's blocks of lit_bufsize - 1, each flushed at the position after
-    // its last symbol (deflate_slow tallies a literal at iteration pos + 1, a match when strstart
-    // reaches its end; deflate_fast flushes after strstart moved past the symbol); deflate_slow's
-    // end-of-input pending literal is tallied without a flush check (Z/deflate.c:1842-1846).
-    // A replay checked against a table prefix (x_lim < n) stops where the parse would read past it.
-    const GLOBAL uint32_t* sv = (const GLOBAL uint32_t*)syms;
-    const uint32_t nsv = tr.rp_nsym;
-    const bool endlit = (tr.rp_flags & 2u) != 0;
-    saved_flags |= 4;
-    uint32_t k = 0, pos = 0;
-    while (k < nsv) {
-      const uint32_t cnt = nsv - k < 64u ? nsv - k : 64u;
-      const bool valid = (uint32_t)lane < cnt;
-      const uint32_t v = valid ? sv[k + (uint32_t)lane] : 0u;
-      const uint32_t len = valid ? ((v >> 8) ? (v & 0xffu) + 3u : 1u) : 0u;
-      const uint32_t incl = wave_incl_scan(len);
-      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-      if (xlim < n && pos + tot + 2u > xlim) { state = TR_NEED_R; z.p = pos; break; }
-      uint32_t base = 0;
-      while (base < cnt) {
-        const uint32_t room = z.lbs - 1u - z.last_lit;
-        const uint32_t seg_end = cnt - base < room ? cnt : base + room;
-        if ((uint32_t)lane >= base && (uint32_t)lane < seg_end) {
-          if (v >> 8) {
-            const uint32_t lc = 257u + len_code(v & 0xffu), dc = dist_code((v >> 8) - 1u);
-            __hip_atomic_fetch_add(&s.f.lfreq2[lc >> 1], 1u << (16 * (lc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&s.f.dfreq2[dc >> 1], 1u << (16 * (dc & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            __hip_atomic_fetch_add(&s.f.lfreq2[v >> 1], 1u << (16 * (v & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    t1 = STEP_CLOCK(); csec[3] += t1 - t0;
+    if (state != ~0u) break;
+    if (!restart && need) { state = TR_NEED_R; z.p = qn; break; }
+    q = qnext;
+  }
+  if (state == ~0u) {
+    z.p = n;
+    z.S = S_iter(Sb, n);
+  }
+  }
+
+  __device__ __forceinline__ void parse_slow() {
+  // deflate_slow (Z/deflate.c:1730-1853), lane-parallel.
+  // After an emitted match (and at the start) deflate_slow's state is canonical: prev_length 2,
+  // no pending literal; after a literal with no match pending it is prev_length 2 with a pending
+  // literal.  So the iterations from a position x up to the next canonical state -- "the walk
+  // from x": either no match at x (next state at x + 1), or a lazy chain of c improving matches
+  // that emits literals x .. m-1 and then the match at m = x + c (next state at m + length) --
+  // depend on x alone.  A window computes the walks from its 64 positions in lanes, the scalar
+  // unit follows the parse path through them (one hop per match or literal run), and the path's
+  // symbols are tallied lane-parallel in position order, which is deflate_slow's tally order.
+  // Window slides are a function of the iteration position (fill_window runs at the top of the
+  // iteration when lookahead < MIN_LOOKAHEAD), so each lane evaluates them itself.
+  uint32_t q = 0, ma = 0, Sb = 0, prevb = 0;   // canonical position, pending literal, S there, byte q-1
+  bool need = false;
+  while (q < n) {
+    const uint32_t wb = q, bal = wb & ~63u;
+    uint64_t t0 = STEP_CLOCK();
+    while (hi < bal + RING_SLOW) {
+      ring[(hi + lane) & (RING_SLOW - 1)] = pf;
+      hi += 64;
+      if (hi < n) pf = Rt[hi + lane];
+    }
+    Sb = S_iter(Sb, wb);
+    if (ATZ_STEP_CLOCKS) { (void)ring[wb & (RING_SLOW - 1)]; __builtin_amdgcn_s_waitcnt(0); }
+    uint64_t t1 = STEP_CLOCK(); csec[0] += t1 - t0; t0 = t1;
+    // ---- the walk from x = wb + lane: wt 0 none (x >= n), 1 no match, 2 match, 3 needs R >= x_lim
+    const uint32_t x = wb + lane;
+    uint32_t wt = 0, nxt = 0, c = 0, L = 0, D = 0;
+    uint32_t rd_last = 0, rd_ey = ~0u;   // rec: last entry the walk read, first quarter-budget read
+    uint32_t w_len = 0, w_imp = 0;       // longest length the walk read; longest PL a lazy read improved
+    if (x < n) {
+      uint32_t qq = x, PL = 2, PD = 0;
+      for (;;) {
+        if (qq >= xlim) { wt = 3; break; }
+        if (rec && (PL == 2 || PL < z.lazy)) {
+          rd_last = qq;
+          if (PL != 2 && PL >= z.good && rd_ey == ~0u) rd_ey = qq;
+        }
+        const uint64_t e64 = ring[qq & (RING_SLOW - 1)];
+        const uint32_t ex = (uint32_t)e64, ey = (uint32_t)(e64 >> 32);
+        bool hv = qq + 3u <= n && (ey & 1u);
+        if (!noslide && hv) {   // hash_head == S is NIL after a slide (only right after one)
+          const uint32_t Sq = S_iter(Sb, qq);
+          if (Sq != 0 && qq - Sq <= maxd) {
+            const uint32_t si = sidx[qq];
+            hv = (bpos[si] & BUCKET_FIRST) || (bpos[si - 1] & ~BUCKET_FIRST) != Sq;
           }
         }
-        z.last_lit += seg_end - base;
-        z.nsym += seg_end - base;
-        if (z.last_lit == z.lbs - 1u && !(endlit && k + seg_end == nsv)) {
-          z.p = pos + (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)seg_end - 1);
-          state = FLUSH0();
-          if (state != ~0u) break;
+        if (PL == 2) {   // first iteration of the walk (qq == x)
+          const uint32_t len = ex >> 23, dist = (ex >> 8) & 0x7fffu;
+          if (hv && len > w_len) w_len = len;
+          uint32_t ML = hv && len > 2 ? len : 2u;
+          if (ML == 3 && dist > 4096) ML = 2;   // TOO_FAR
+          if (ML == 2) { wt = 1; nxt = x + 1; break; }
+          PL = ML; PD = dist; qq++;
+          continue;
         }
-        base = seg_end;
+        if (PL < z.lazy && hv) {
+          const uint32_t ev = PL >= z.good ? ey : ex;
+          const uint32_t len = ev >> 23;
+          if (len > w_len) w_len = len;
+          if (len > PL) { if (PL > w_imp) w_imp = PL; PL = len; PD = (ev >> 8) & 0x7fffu; c++; qq++; continue; }
+        }
+        wt = 2; L = PL; D = PD; nxt = qq - 1 + PL;
+        break;
       }
-      if (state != ~0u) break;
-      pos += tot;
-      k += cnt;
     }
-    if (state == ~0u) {
-      z.p = n;
-      z.S = 0;
+    // ---- follow the parse path through the window
+    const uint64_t Am = __ballot(wt == 1), Nm = __ballot(wt == 3);
+    t1 = STEP_CLOCK(); csec[1] += t1 - t0; t0 = t1;
+    const uint32_t rel = wt == 1 ? run_end_rel(Am, lane) : wt == 2 ? nxt - wb : 0xffffu;
+    const WinPath wp = follow_path(rel, Nm, n - wb < 64 ? n - wb : 64u);
+    bool onp;
+    uint32_t mab;
+    path_lane(wp, Am, ma, lane, onp, mab);
+    need = wp.need;
+    const uint32_t qn = wb + wp.end;
+    if (onp && (wt == 1 || wt == 2)) {   // the parse's own walks (diagnostics for level equivalence)
+      run_len = w_len > run_len ? w_len : run_len;
+      run_imp = w_imp > run_imp ? w_imp : run_imp;
     }
-  } else if constexpr (KIND == 1) {
-    // deflate_fast (Z/deflate.c:1628-1722), lane-parallel.  Every deflate_fast iteration starts in
-    // the same state, so a window takes the match table's step at each of its 64 positions in
-    // lanes, the scalar unit follows the parse path through them, and the path's insertion state
-    // and symbols are written lane-parallel.  A table entry is the walk over ALL same-hash
-    // positions; deflate_fast walks the INSERTED ones (interiors of matches longer than
-    // max_insert_length are skipped: "holes"), so every path node is checked: the entry is exact
-    // unless a hole with its hash slot lies in the walked range [lowest visited node, p) AND it
-    // can matter -- skipped nodes only shrink the visited set, so a walk that ended by nice_match
-    // or by the end of the chain keeps its winner W if W itself was inserted (and with no winner
-    // the step emits a literal either way); only a walk that spent its budget with nodes left can
-    // see new nodes (bit 12).  The first node that fails the check is walked exactly over the
-    // inserted positions and the window ends there.  holes[] keeps per slot the latest hole; the
-    // window's own holes are entered before the check, so a hole behind the node only makes the
-    // check conservative (slot collisions likewise).
-    LDS uint32_t* holes = (LDS uint32_t*)shm.holes;
-    LDS uint32_t* ins = (LDS uint32_t*)shm.ins;   // insertion bits, position mod SH::INS_BITS
-    constexpr uint32_t INS_MASK = SH::INS_BITS / 32 - 1;
-    for (int i = lane; i < (int)HOLE_SLOTS; i += 64) holes[i] = 0;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    auto ins_get = [&](uint32_t q) -> bool { return (ins[(q >> 5) & INS_MASK] >> (q & 31)) & 1u; };
-    // insertion bits and holes of the positions [lo, hi) covered by path nodes; cover(p) gives the
-    // node y <= p covering p and its match length (0: literal).  cover runs with all lanes active
-    // (it may shuffle: a lane outside EXEC would read as 0).
-    auto span_set = [&](uint32_t lo, uint32_t hi2, auto cover) {
-      for (uint32_t c0 = lo & ~63u; c0 < hi2; c0 += 64) {
-        const uint32_t p = c0 + (uint32_t)lane;
-        const bool insp = p >= lo && p < hi2;
-        bool insd = false, hole = false;
-        uint32_t y, Ly;
-        cover(p, y, Ly);
-        if (insp) {
-          if (p == y) insd = p + 3u <= n;
-          else if (Ly <= z.lazy && y + Ly + 3u <= n) insd = true;
-          else hole = p + 3u <= n;
-        }
-        const uint64_t bits = __ballot(insd), sm = __ballot(insp);
-        if (lane < 2) {
-          const uint32_t sh = 32u * (uint32_t)lane;
-          const uint32_t m = (uint32_t)(sm >> sh), bv = (uint32_t)(bits >> sh);
-          if (m) {
-            LDS uint32_t& w = ins[((c0 + sh) >> 5) & INS_MASK];
-            w = (w & ~m) | (bv & m);
-          }
-        }
-        if (hole) {
-          const uint32_t slot = ((uint32_t)(ring[p & (RING_SLOW - 1)] >> 32) >> 1) & (HOLE_SLOTS - 1);
-          __hip_atomic_fetch_max(&holes[slot], p + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+    if (rec && onp && (wt == 1 || wt == 2))   // the walk's reads: x full-budget, then by PL
+      for (uint32_t i = x; i <= rd_last; i++) {
+        const uint64_t e64 = ring[i & (RING_SLOW - 1)];
+        rtab[i] = (i == x || i < rd_ey) ? ((e64 & 0xffffff00ull) | 1ull) : ((e64 & 0xffffff0000000000ull) | (1ull << 32));
       }
-    };
-    // one symbol, tallied by the scalar unit; returns true when the block is full
-    auto tally1 = [&](uint32_t v) -> bool {
-      if (lane == 0) {
-        syms[(saving || MW ? sbase : 0u) + z.last_lit] = v;
-        if (v >> 8) {
-          __hip_atomic_fetch_add(&s.f.lfreq2[(257u + len_code(v & 0xffu)) >> 1], 1u << (16 * ((257u + len_code(v & 0xffu)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          __hip_atomic_fetch_add(&s.f.dfreq2[(dist_code((v >> 8) - 1u)) >> 1], 1u << (16 * ((dist_code((v >> 8) - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // pending literal at qn: after a run yes, after a match no
+    const uint32_t man = wp.H ? (uint32_t)((Am >> (63 - __builtin_clzll(wp.H))) & 1ull) : ma;
+    // ---- tally the path's symbols: node x emits [literal x-1 if pending], literals x..m-1, match
+    t1 = STEP_CLOCK(); csec[2] += t1 - t0; t0 = t1;
+    const uint32_t cnt = onp ? mab + (wt == 2 ? c + 1u : 0u) : 0u;
+    const uint64_t ltm = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t T;
+    const uint32_t o = wave_excl_sum(cnt, ltm, T);
+    z.nsym += T;
+    uint32_t base = 0;
+    while (base < T) {
+      const uint32_t room = z.lbs - 1u - z.last_lit;
+      const uint32_t seg_end = T - base < room ? T : base + room;
+      const uint32_t klo = o > base ? 0u : base - o;
+      const uint32_t khi = o + cnt < seg_end ? cnt : (seg_end > o ? seg_end - o : 0u);
+      for (uint32_t k = klo; k < khi; k++) {
+        const uint32_t j = k - mab;   // k == 0 with mab: literal x-1
+        uint32_t v;
+        if (mab && k == 0) v = lane == 0 ? prevb : (uint32_t)ring[(x - 1) & (RING_SLOW - 1)] & 0xffu;
+        else if (j < c) v = (uint32_t)ring[(x + j) & (RING_SLOW - 1)] & 0xffu;
+        else v = 0x80000000u | (D << 8) | (L - 3u);
+        if (v & 0x80000000u) {
+          v &= 0x7fffffffu;
+          __hip_atomic_fetch_add(&s.f.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&s.f.dfreq2[(dist_code(D - 1u)) >> 1], 1u << (16 * ((dist_code(D - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else {
           __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        syms[(saving || MW ? sbase : 0u) + z.last_lit + (o + k - base)] = v;
+      }
+      z.last_lit += seg_end - base;
+      if (z.last_lit == z.lbs - 1u) {
+        // flush after symbol seg_end - 1: strstart = its iteration + 1 for a literal (the
+        // literal of y is tallied at iteration y + 1), match end for a match (tallied at m + 1)
+        const uint32_t g = seg_end - 1u;
+        const bool own = cnt && o <= g && g < o + cnt;
+        uint32_t fp = 0, fit = 0;
+        if (own) {
+          const uint32_t k = g - o, j = k - mab;
+          if (mab && k == 0) { fp = x; fit = x; }
+          else if (j < c) { fp = x + j + 1u; fit = fp; }
+          else { fp = x + c + L; fit = x + c + 1u; }
+        }
+        const uint64_t om = __ballot(own);
+        const int ol = (int)__builtin_ctzll(om);
+        z.p = (uint32_t)__builtin_amdgcn_readlane((int)fp, ol);
+        z.S = S_iter(Sb, (uint32_t)__builtin_amdgcn_readlane((int)fit, ol));
+        state = FLUSH0();
+        if (state != ~0u) break;
+      }
+      base = seg_end;
+    }
+    t1 = STEP_CLOCK(); csec[3] += t1 - t0;
+    if (state != ~0u) break;
+    if (need) { state = TR_NEED_R; z.p = qn; break; }
+    prevb = qn > 0 ? (uint32_t)ring[(qn - 1u) & (RING_SLOW - 1)] & 0xffu : 0u;   // read when man: qn - 1 < wb + 64
+    q = qn;
+    ma = man;
+  }
+  if (state == ~0u) {
+    // end of input: the pending literal goes into the final block without a flush check
+    if (ma) {
+      const uint32_t v = prevb;
+      saved_flags |= 2;
+      if (lane == 0) {
+        syms[(saving || MW ? sbase : 0u) + z.last_lit] = v;
+        __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       z.last_lit++;
       z.nsym++;
-      return z.last_lit == z.lbs - 1u;
-    };
-    uint32_t q = 0, Sb = 0;
-    bool need = false;
-    while (q < n) {
-      const uint32_t wb = q, bal = wb & ~63u;
-      uint64_t t0 = STEP_CLOCK();
-      while (hi < bal + RING_SLOW) {
-        ring[(hi + lane) & (RING_SLOW - 1)] = pf;
-        hi += 64;
-        if (hi < n) pf = Rt[hi + lane];
-      }
-      Sb = S_iter(Sb, wb);
-      if (ATZ_STEP_CLOCKS) { (void)ring[wb & (RING_SLOW - 1)]; __builtin_amdgcn_s_waitcnt(0); }
-      uint64_t t1 = STEP_CLOCK(); csec[0] += t1 - t0; t0 = t1;
-      // ---- the table's step at x = wb + lane: wt 0 none (x >= n), 1 literal, 2 match, 3 needs R >= x_lim
-      const uint32_t x = wb + lane;
-      // x's bucket index, loaded now and read only by the node checks and the exact walks below (its
-      // latency hides behind the window's own work instead of opening a walk)
-      const uint32_t sxl = x < n ? sidx[x] : 0u;
-      uint32_t wt = 0, L = 0, D = 0, ex = 0, ey = 0, Sx = Sb;
-      if (x < n) {
-        if (x >= xlim) wt = 3;
-        else {
-          const uint64_t e64 = ring[x & (RING_SLOW - 1)];
-          ex = (uint32_t)e64; ey = (uint32_t)(e64 >> 32);
-          if (!noslide) Sx = S_iter(Sb, x);
-          bool hv = x + 3u <= n && (ey & 1u);
-          if (!noslide && hv && Sx != 0 && x - Sx <= maxd) {   // hash_head == S is NIL after a slide
-            const uint32_t si = sidx[x];
-            hv = (bpos[si] & BUCKET_FIRST) || (bpos[si - 1] & ~BUCKET_FIRST) != Sx;
-          }
-          const uint32_t len = ex >> 23;
-          if (hv && len > 2) { wt = 2; L = len; D = (ex >> 8) & 0x7fffu; }
-          else wt = 1;
-        }
-      }
-      // ---- follow the parse path through the window
-      const uint64_t Am = __ballot(wt == 1), Nm = __ballot(wt == 3);
-      t1 = STEP_CLOCK(); csec[1] += t1 - t0; t0 = t1;
-      const uint32_t rel = wt == 1 ? run_end_rel(Am, lane) : wt == 2 ? (uint32_t)lane + L : 0xffffu;
-      const WinPath wp = follow_path(rel, Nm, n - wb < 64 ? n - wb : 64u);
-      bool onp;
-      uint32_t mab_unused;
-      path_lane(wp, Am, 0, lane, onp, mab_unused);
-      const uint64_t P = __ballot(onp);
-      need = wp.need;
-      const uint32_t qn = wb + wp.end;
-      const uint32_t last = P ? wb + 63u - (uint32_t)__builtin_clzll(P) : wb;
-      // ---- insertion state of the path, then the check of its nodes
-      t1 = STEP_CLOCK(); csec[2] += t1 - t0; t0 = t1;
-      if (qn > wb)
-        span_set(wb, qn, [&](uint32_t p, uint32_t& y, uint32_t& Ly) {
-          const uint32_t i = p - wb;   // huge for p < wb (such lanes are outside the span)
-          uint32_t yl = last - wb;
-          if (i < 64) yl = 63u - (uint32_t)__builtin_clzll(P & (~0ull >> (63 - i)));
-          y = wb + yl;
-          Ly = (uint32_t)__shfl((int)L, (int)yl, 64);
-        });
-#if ATZ_STEP_SPLIT
-      t1 = STEP_CLOCK(); csec[0] += t1 - t0; t0 = t1;   // (diagnostics: span_set counted with refill)
-#endif
-      bool bad = false;
-      if (onp && x + 3u <= n) {
-        const uint32_t hl = holes[(ey >> 1) & (HOLE_SLOTS - 1)];
-        bool exact = hl == 0 || hl - 1u < x - (ey >> 16);
-        if (!exact && !((ey >> 12) & 1u)) {
-          // Skipped nodes only shrink the visited set -- except at the MAX_DIST edge: deflate_fast
-          // walks its hash head at distance MAX_DIST (Z/deflate.c:1660) but later chain nodes only
-          // above it (Z/deflate.c:1227), so when holes above it made a hole the table's head, the
-          // node at exactly x - MAX_DIST can be examined by deflate_fast and not by the table walk.
-          // Such a node is resolved by the exact walk below.
-          const uint32_t q0 = x - maxd;
-          const uint32_t hb = tr.memlevel + 7u, hs = (hb + 2u) / 3u, hm = (1u << hb) - 1u;
-          const bool edge = x > maxd && q0 > Sx &&
-                            ((((uint32_t)in[q0] << (2u * hs)) ^ ((uint32_t)in[q0 + 1] << hs) ^ in[q0 + 2]) & hm) ==
-                            ((((uint32_t)in[x] << (2u * hs)) ^ ((uint32_t)in[x + 1] << hs) ^ in[x + 2]) & hm);
-          if (edge) exact = false;
-          else if ((ex >> 23) <= 2) exact = true;
-          else {
-            const uint32_t wpos = x - ((ex >> 8) & 0x7fffu);
-            exact = wpos > Sx && ins_get(wpos);
-          }
-        } else if (!exact && ATZ_VISITED_CHECK && z.chain <= ATZ_VISITED_MAX) {
-          // the walk spent its budget and a hole shares the slot: the entry is still exact when
-          // every node the walk visited (the bucket entries below x down to the lowest visited
-          // one, at most `chain` of them) was inserted -- deflate_fast's chain then starts with
-          // the same nodes and spends the same budget on them
-          const uint32_t lo = x - (ey >> 16);
-          const int32_t si = (int32_t)sxl;
-          bool ok = true, stop = false;
-          for (int32_t k = si - 1; ok && !stop && k > si - 1 - (int32_t)z.chain; k -= 4) {
-            uint32_t e4[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) e4[u] = k - u >= 0 ? bpos[k - u] : BUCKET_FIRST;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-              if (!ok || stop || k - u <= si - 1 - (int32_t)z.chain) break;
-              const uint32_t pos = e4[u] & ~BUCKET_FIRST;
-              if (k - u < 0 || pos < lo) { stop = true; break; }
-              ok = pos > Sx && ins_get(pos);
-              if (e4[u] & BUCKET_FIRST) stop = true;
-            }
-          }
-          exact = ok;
-        }
-        bad = !exact;
-      }
-      // Bad nodes are resolved one at a time by an exact walk.  When the walk's length equals the
-      // table's (or both give a literal), the parse path is unchanged: the node keeps its place on
-      // the path (with the walk's distance) and the window goes on to its next bad node.  Only a
-      // different length ends the window there.
-      uint64_t badm = __ballot(bad);
-      uint64_t donem = 0;   // path nodes tallied so far
-      uint32_t Dx = D;      // this lane's match distance (an exact walk may replace the table's)
-      bool restart = false;
-      uint32_t qnext = qn;
-      for (;;) {
-        // ---- tally the committed nodes' symbols lane-parallel, in position order
-        const uint64_t Pc = (badm ? P & ((1ull << __builtin_ctzll(badm)) - 1ull) : P) & ~donem;
-        {
-          const bool mine = (Pc >> lane) & 1ull;
-          const uint32_t o = (uint32_t)__popcll(Pc & lt);
-          const uint32_t T = (uint32_t)__popcll(Pc);
-          z.nsym += T;
-          uint32_t base = 0;
-          while (base < T) {
-            const uint32_t room = z.lbs - 1u - z.last_lit;
-            const uint32_t seg_end = T - base < room ? T : base + room;
-            if (mine && o >= base && o < seg_end) {
-              uint32_t v;
-              if (wt == 2) {
-                v = (Dx << 8) | (L - 3u);
-                __hip_atomic_fetch_add(&s.f.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(&s.f.dfreq2[(dist_code(Dx - 1u)) >> 1], 1u << (16 * ((dist_code(Dx - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              } else {
-                v = ex & 0xffu;
-                __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              }
-              syms[(saving || MW ? sbase : 0u) + z.last_lit + (o - base)] = v;
-            }
-            z.last_lit += seg_end - base;
-            if (z.last_lit == z.lbs - 1u) {   // flush after the node tallied last: strstart past its step
-              const uint64_t om = __ballot(mine && o == seg_end - 1u);
-              const int ol = (int)__builtin_ctzll(om);
-              const uint32_t fx = (uint32_t)__builtin_amdgcn_readlane((int)x, ol);
-              const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)L, ol);
-              z.p = fx + (fl ? fl : 1u);
-              z.S = S_iter(Sb, fx);
-              state = FLUSH0();
-              if (state != ~0u) break;
-            }
-            base = seg_end;
-          }
-        }
-        donem |= Pc;
-        if (state != ~0u || !badm) break;
-        // ---- the first node that may differ: deflate_fast's longest_match over the INSERTED
-        // same-hash positions (Z/deflate.c:1148-1289): 64 bucket entries per step, lanes test
-        // insertion and compare bytes in parallel; the walk order is the lane order.
-        fallbacks++;
-        const uint64_t cf0 = STEP_CLOCK();
-        const int fln = __builtin_ctzll(badm);
-        const uint32_t f = wb + (uint32_t)fln;
-        const uint32_t Sf = S_iter(Sb, f);
-        const uint32_t la = n - f < LOOKMIN ? n - f : LOOKMIN;   // lookahead (>= 258 stands for more)
-        uint32_t ml = 0, ms = 0;
-        {
-          const uint32_t si = uni((uint32_t)__builtin_amdgcn_readlane((int)sxl, fln));
-          bool done = false;
-          bool head_done = false, hv = false, won = false;
-          uint32_t examined = 0, best = 2, win = 0;
-          const uint32_t limit = f > maxd ? f - maxd : 0u;   // later nodes only while > limit
-          const uint32_t cap = n - f < 258u ? n - f : 258u;
-          const uint32_t nicec = z.nice < la ? z.nice : la;   // <= cap
-          // lane l reads bucket entry top - l; the first chunk starts at f's own entry (lane 0), whose
-          // first-of-bucket flag says whether f has a chain at all
-          int32_t top = (int32_t)si;
-          int skip = 1;
-          while (!done) {
-            const int32_t k = top - lane;
-            const uint32_t e = k >= 0 ? bpos[k] : BUCKET_FIRST;
-            if (skip && (uni((uint32_t)__builtin_amdgcn_readlane((int)e, 0)) & BUCKET_FIRST)) break;   // first of its bucket: no chain
-            const uint64_t fm = __ballot((e & BUCKET_FIRST) != 0 && lane >= skip);
-            const int flane = fm ? __ffsll((unsigned long long)fm) - 1 : 64;   // bucket's first entry: last node
-            const uint32_t qc = e & ~BUCKET_FIRST;
-            const bool insd = lane >= skip && lane <= flane && k >= 0 && ins_get(qc);
-            const uint64_t im = __ballot(insd);
-            int head_lane = -1, from = 0;
-            if (!head_done) {
-              if (!im) {   // no inserted node in this chunk yet
-                if (flane < 64) break;
-                top -= 64;
-                skip = 0;
-                continue;
-              }
-              head_lane = __ffsll((unsigned long long)im) - 1;
-              const uint32_t hh = (uint32_t)__builtin_amdgcn_readlane((int)qc, head_lane);
-              head_done = true;
-              hv = hh > Sf && f - hh <= maxd;   // zlib calls longest_match only then
-              if (!hv) break;
-              from = head_lane;
-            }
-            // the walk stops at the first inserted node <= limit (the head is always examined)
-            const uint64_t sm = __ballot(insd && lane >= from && lane != head_lane && qc <= limit);
-            const int slane = sm ? __ffsll((unsigned long long)sm) - 1 : 64;
-            bool cand = insd && lane >= from && lane < slane;
-            const uint32_t room = z.chain - examined;
-            cand = cand && (uint32_t)__popcll(__ballot(cand) & lt) < room;
-            const uint64_t cm = __ballot(cand);
-            examined += (uint32_t)__popcll(cm);
-            // match lengths capped at nice (16 bytes per round trip); the first candidate reaching
-            // nice ends the walk, so capped lengths decide the winner
-            uint32_t len = 0;
-            bool go = cand;
-            while (__ballot(go)) {
-              if (go) {
-                // 16 bytes per round trip: 5 aligned dword loads per side (stream bases are 256-byte aligned)
-                const uint32_t run = match16((const GLOBAL uint32_t*)in, qc + len, f + len, nullptr, 0);
-                const uint32_t left = nicec - len;
-                len += run < left ? run : left;
-                go = run == 16 && len < nicec;
-              }
-            }
-            const uint64_t nm = __ballot(cand && len >= nicec);
-            if (nm) {
-              const int wl = __ffsll((unsigned long long)nm) - 1;
-              win = (uint32_t)__builtin_amdgcn_readlane((int)qc, wl);
-              best = uni(common_len(in, win, f, nicec, cap, lane));   // full length of the winner
-              won = true;
-              break;
-            }
-            uint32_t mx = cand ? len : 0u;
-            for (int d = 32; d >= 1; d >>= 1) { const uint32_t o2 = __shfl_xor(mx, d, 64); mx = mx > o2 ? mx : o2; }
-            mx = uni(mx);
-            if (mx > best) {
-              const uint64_t xm = __ballot(cand && len == mx);
-              win = (uint32_t)__builtin_amdgcn_readlane((int)qc, __ffsll((unsigned long long)xm) - 1);
-              best = mx;
-              won = true;
-            }
-            done = examined >= z.chain || slane < 64 || flane < 64;
-            top -= 64;
-            skip = 0;
-          }
-          if (hv && won) {
-            ml = best <= la ? best : la;
-            ms = win;
-          }
-        }
-        cyc_fb += STEP_CLOCK() - cf0;
-        const uint32_t twt = uni((uint32_t)__builtin_amdgcn_readlane((int)wt, fln));
-        const uint32_t tL = uni((uint32_t)__builtin_amdgcn_readlane((int)L, fln));
-        if (ml >= 3 ? (twt == 2 && tL == ml) : twt == 1) {   // same step: the path stands
-          if (ml >= 3 && lane == fln) Dx = f - ms;
-          badm &= badm - 1ull;
-          continue;
-        }
-        // the path changes at f: its exact step, then a new window after it
-        fallbacks += 1ull << 32;   // diagnostics: walks that changed the path (high half)
-        const uint32_t step = ml >= 3 ? ml : 1u;
-        span_set(f, f + step, [&](uint32_t p, uint32_t& y, uint32_t& Ly) { y = f; Ly = ml >= 3 ? ml : 0u; });
-        const bool full = tally1(ml >= 3 ? (((f - ms) << 8) | (ml - 3u)) : (uint32_t)in[f]);
-        if (full) {
-          z.p = f + step;
-          z.S = Sf;
-          state = FLUSH0();
-        }
-        qnext = f + step;
-        restart = true;
-        break;
-      }
-      t1 = STEP_CLOCK(); csec[3] += t1 - t0;
-      if (state != ~0u) break;
-      if (!restart && need) { state = TR_NEED_R; z.p = qn; break; }
-      q = qnext;
     }
-    if (state == ~0u) {
-      z.p = n;
-      z.S = S_iter(Sb, n);
-    }
-  } else {
-    // deflate_slow (Z/deflate.c:1730-1853), lane-parallel.
-    // After an emitted match (and at the start) deflate_slow's state is canonical: prev_length 2,
-    // no pending literal; after a literal with no match pending it is prev_length 2 with a pending
-    // literal.  So the iterations from a position x up to the next canonical state -- "the walk
-    // from x": either no match at x (next state at x + 1), or a lazy chain of c improving matches
-    // that emits literals x .. m-1 and then the match at m = x + c (next state at m + length) --
-    // depend on x alone.  A window computes the walks from its 64 positions in lanes, the scalar
-    // unit follows the parse path through them (one hop per match or literal run), and the path's
-    // symbols are tallied lane-parallel in position order, which is deflate_slow's tally order.
-    // Window slides are a function of the iteration position (fill_window runs at the top of the
-    // iteration when lookahead < MIN_LOOKAHEAD), so each lane evaluates them itself.
-    uint32_t q = 0, ma = 0, Sb = 0, prevb = 0;   // canonical position, pending literal, S there, byte q-1
-    bool need = false;
-    while (q < n) {
-      const uint32_t wb = q, bal = wb & ~63u;
-      uint64_t t0 = STEP_CLOCK();
-      while (hi < bal + RING_SLOW) {
-        ring[(hi + lane) & (RING_SLOW - 1)] = pf;
-        hi += 64;
-        if (hi < n) pf = Rt[hi + lane];
-      }
-      Sb = S_iter(Sb, wb);
-      if (ATZ_STEP_CLOCKS) { (void)ring[wb & (RING_SLOW - 1)]; __builtin_amdgcn_s_waitcnt(0); }
-      uint64_t t1 = STEP_CLOCK(); csec[0] += t1 - t0; t0 = t1;
-      // ---- the walk from x = wb + lane: wt 0 none (x >= n), 1 no match, 2 match, 3 needs R >= x_lim
-      const uint32_t x = wb + lane;
-      uint32_t wt = 0, nxt = 0, c = 0, L = 0, D = 0;
-      uint32_t rd_last = 0, rd_ey = ~0u;   // rec: last entry the walk read, first quarter-budget read
-      uint32_t w_len = 0, w_imp = 0;       // longest length the walk read; longest PL a lazy read improved
-      if (x < n) {
-        uint32_t qq = x, PL = 2, PD = 0;
-        for (;;) {
-          if (qq >= xlim) { wt = 3; break; }
-          if (rec && (PL == 2 || PL < z.lazy)) {
-            rd_last = qq;
-            if (PL != 2 && PL >= z.good && rd_ey == ~0u) rd_ey = qq;
-          }
-          const uint64_t e64 = ring[qq & (RING_SLOW - 1)];
-          const uint32_t ex = (uint32_t)e64, ey = (uint32_t)(e64 >> 32);
-          bool hv = qq + 3u <= n && (ey & 1u);
-          if (!noslide && hv) {   // hash_head == S is NIL after a slide (only right after one)
-            const uint32_t Sq = S_iter(Sb, qq);
-            if (Sq != 0 && qq - Sq <= maxd) {
-              const uint32_t si = sidx[qq];
-              hv = (bpos[si] & BUCKET_FIRST) || (bpos[si - 1] & ~BUCKET_FIRST) != Sq;
-            }
-          }
-          if (PL == 2) {   // first iteration of the walk (qq == x)
-            const uint32_t len = ex >> 23, dist = (ex >> 8) & 0x7fffu;
-            if (hv && len > w_len) w_len = len;
-            uint32_t ML = hv && len > 2 ? len : 2u;
-            if (ML == 3 && dist > 4096) ML = 2;   // TOO_FAR
-            if (ML == 2) { wt = 1; nxt = x + 1; break; }
-            PL = ML; PD = dist; qq++;
-            continue;
-          }
-          if (PL < z.lazy && hv) {
-            const uint32_t ev = PL >= z.good ? ey : ex;
-            const uint32_t len = ev >> 23;
-            if (len > w_len) w_len = len;
-            if (len > PL) { if (PL > w_imp) w_imp = PL; PL = len; PD = (ev >> 8) & 0x7fffu; c++; qq++; continue; }
-          }
-          wt = 2; L = PL; D = PD; nxt = qq - 1 + PL;
-          break;
-        }
-      }
-      // ---- follow the parse path through the window
-      const uint64_t Am = __ballot(wt == 1), Nm = __ballot(wt == 3);
-      t1 = STEP_CLOCK(); csec[1] += t1 - t0; t0 = t1;
-      const uint32_t rel = wt == 1 ? run_end_rel(Am, lane) : wt == 2 ? nxt - wb : 0xffffu;
-      const WinPath wp = follow_path(rel, Nm, n - wb < 64 ? n - wb : 64u);
-      bool onp;
-      uint32_t mab;
-      path_lane(wp, Am, ma, lane, onp, mab);
-      need = wp.need;
-      const uint32_t qn = wb + wp.end;
-      if (onp && (wt == 1 || wt == 2)) {   // the parse's own walks (diagnostics for level equivalence)
-        run_len = w_len > run_len ? w_len : run_len;
-        run_imp = w_imp > run_imp ? w_imp : run_imp;
-      }
-      if (rec && onp && (wt == 1 || wt == 2))   // the walk's reads: x full-budget, then by PL
-        for (uint32_t i = x; i <= rd_last; i++) {
-          const uint64_t e64 = ring[i & (RING_SLOW - 1)];
-          rtab[i] = (i == x || i < rd_ey) ? ((e64 & 0xffffff00ull) | 1ull) : ((e64 & 0xffffff0000000000ull) | (1ull << 32));
-        }
-      // pending literal at qn: after a run yes, after a match no
-      const uint32_t man = wp.H ? (uint32_t)((Am >> (63 - __builtin_clzll(wp.H))) & 1ull) : ma;
-      // ---- tally the path's symbols: node x emits [literal x-1 if pending], literals x..m-1, match
-      t1 = STEP_CLOCK(); csec[2] += t1 - t0; t0 = t1;
-      const uint32_t cnt = onp ? mab + (wt == 2 ? c + 1u : 0u) : 0u;
-      const uint64_t ltm = lane ? (~0ull >> (64 - lane)) : 0ull;
-      uint32_t T;
-      const uint32_t o = wave_excl_sum(cnt, ltm, T);
-      z.nsym += T;
-      uint32_t base = 0;
-      while (base < T) {
-        const uint32_t room = z.lbs - 1u - z.last_lit;
-        const uint32_t seg_end = T - base < room ? T : base + room;
-        const uint32_t klo = o > base ? 0u : base - o;
-        const uint32_t khi = o + cnt < seg_end ? cnt : (seg_end > o ? seg_end - o : 0u);
-        for (uint32_t k = klo; k < khi; k++) {
-          const uint32_t j = k - mab;   // k == 0 with mab: literal x-1
-          uint32_t v;
-          if (mab && k == 0) v = lane == 0 ? prevb : (uint32_t)ring[(x - 1) & (RING_SLOW - 1)] & 0xffu;
-          else if (j < c) v = (uint32_t)ring[(x + j) & (RING_SLOW - 1)] & 0xffu;
-          else v = 0x80000000u | (D << 8) | (L - 3u);
-          if (v & 0x80000000u) {
-            v &= 0x7fffffffu;
-            __hip_atomic_fetch_add(&s.f.lfreq2[(257u + len_code(L - 3u)) >> 1], 1u << (16 * ((257u + len_code(L - 3u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&s.f.dfreq2[(dist_code(D - 1u)) >> 1], 1u << (16 * ((dist_code(D - 1u)) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          syms[(saving || MW ? sbase : 0u) + z.last_lit + (o + k - base)] = v;
-        }
-        z.last_lit += seg_end - base;
-        if (z.last_lit == z.lbs - 1u) {
-          // flush after symbol seg_end - 1: strstart = its iteration + 1 for a literal (the
-          // literal of y is tallied at iteration y + 1), match end for a match (tallied at m + 1)
-          const uint32_t g = seg_end - 1u;
-          const bool own = cnt && o <= g && g < o + cnt;
-          uint32_t fp = 0, fit = 0;
-          if (own) {
-            const uint32_t k = g - o, j = k - mab;
-            if (mab && k == 0) { fp = x; fit = x; }
-            else if (j < c) { fp = x + j + 1u; fit = fp; }
-            else { fp = x + c + L; fit = x + c + 1u; }
-          }
-          const uint64_t om = __ballot(own);
-          const int ol = (int)__builtin_ctzll(om);
-          z.p = (uint32_t)__builtin_amdgcn_readlane((int)fp, ol);
-          z.S = S_iter(Sb, (uint32_t)__builtin_amdgcn_readlane((int)fit, ol));
-          state = FLUSH0();
-          if (state != ~0u) break;
-        }
-        base = seg_end;
-      }
-      t1 = STEP_CLOCK(); csec[3] += t1 - t0;
-      if (state != ~0u) break;
-      if (need) { state = TR_NEED_R; z.p = qn; break; }
-      prevb = qn > 0 ? (uint32_t)ring[(qn - 1u) & (RING_SLOW - 1)] & 0xffu : 0u;   // read when man: qn - 1 < wb + 64
-      q = qn;
-      ma = man;
-    }
-    if (state == ~0u) {
-      // end of input: the pending literal goes into the final block without a flush check
-      if (ma) {
-        const uint32_t v = prevb;
-        saved_flags |= 2;
-        if (lane == 0) {
-          syms[(saving || MW ? sbase : 0u) + z.last_lit] = v;
-          __hip_atomic_fetch_add(&s.f.lfreq2[(v) >> 1], 1u << (16 * ((v) & 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        z.last_lit++;
-        z.nsym++;
-      }
-      z.p = n;
-      z.S = S_iter(Sb, n);
-    }
+    z.p = n;
+    z.S = S_iter(Sb, n);
   }
+  }
+
+  // the final block, the trailer and the final gates (main.cpp:632-681); multi-wave: the last block's
+  // hand-over
+  __device__ __forceinline__ void end_parse() {
   if (MW && state == ~0u) {
     saved_flags |= 1;   // every symbol tallied: a saving trial's sequence is complete
     if (!publish(1)) state = TR_DECIDED;   // the final gates run on the last block's flusher
@@ -2708,7 +2745,10 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     st_rel(ctl.parse_done, 1u, lane);
     if (state == TR_NEED_R) st_rel(ctl.stop, 1u, lane);
   }
-  }   // wave 0
+  }
+
+  // the flushers' outcome (multi-wave) and the trial's result
+  __device__ __forceinline__ void finish() {
   if constexpr (MW) {
     __syncthreads();   // every flusher has stopped
     if (wave != 0) return;
@@ -2758,6 +2798,40 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     r.rt1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
     A.res[t] = r;
   }
+  }
+
+  __device__ __forceinline__ void run() {
+    if constexpr (MW) {
+      LDS MWPart& mw = *(LDS MWPart*)&shm.mw;
+      if (wave == 0) {
+        if (lane < MW_F) { mw.slot[lane].seq = 0; mw.fl[lane].cyc_tree = 0; mw.fl[lane].cyc_emit = 0;
+                          mw.fl[lane].cyc_heap = 0; mw.fl[lane].cyc_scan = 0; }
+        if (lane == 0) {
+          mw.ctl.next_emit = 0; mw.ctl.stop = 0; mw.ctl.parse_done = 0; mw.ctl.nblocks = 0;
+          mw.ctl.state = ~0u; mw.ctl.hazard = 0;
+        }
+      }
+      __syncthreads();
+      if (wave != 0)
+        trial_flusher(A, s, mw, tr, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, z.level, z.lbs, full_needed,
+                      wave - 1, lane);
+    }
+    if (wave == 0) {   // the parse; every wave of a single-wave trial
+      parse_setup();
+      if constexpr (KIND == 0) parse_stored();
+      else if (replay) parse_replay();
+      else if constexpr (KIND == 1) parse_fast();
+      else parse_slow();
+      end_parse();
+    }
+    finish();
+  }
+};
+
+template <int KIND, typename SH>
+__device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
+  TrialRun<KIND, SH> run(A, shm, lane);
+  run.run();
 }
 
 #ifndef TRIAL_SLOW_WAVES
