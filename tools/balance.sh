@@ -12,7 +12,7 @@ export ATZ_BENCH_BACKEND=gloo ATZ_BENCH_CACHE=/tmp/atz_bench_cache
 export ATZ_TARGET=${ATZ_TARGET:-4096}
 port=29611
 for wl in ${WLS:-c4 c4c3}; do
-  for hint in 1 0; do
+  for hint in ${HINTS:-1 0}; do
     port=$((port + 1))
     echo "== $wl hint=$hint $(date +%T)"
     ATZ_SPLIT_HINT=$hint timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $W \

@@ -12,7 +12,10 @@ case $P in
   b) bash tools/measure.sh $T sq pmc || exit $?
      bash tools/shares.sh ${T}_sh || exit 20
      timeout -k 10 400 python3 bench.py --workload c5 --steps 3 --warmup 1 --no-recon --no-h2h > $O/c5.json 2> $O/c5.err || exit 21 ;;
-  c) bash tools/ceiling.sh ${T}_ceil || exit 30
-     WLS="c4 c4c3" bash tools/balance.sh ${T}_bal 8 || exit 31 ;;
+  c) for n in 12500 25000; do   # one rank's share at N = 8 / 4, as bench.py runs it there (8 hardware queues)
+       GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python3 bench.py --streams $n --steps 3 --warmup 1 --no-cpu --no-recon --no-h2h > $O/q8_s$n.json 2> $O/q8_s$n.err || exit 29
+     done
+     bash tools/ceiling.sh ${T}_ceil || exit 30
+     WLS="c4 c4c3" HINTS=1 bash tools/balance.sh ${T}_bal 8 || exit 31 ;;
 esac
 echo done
