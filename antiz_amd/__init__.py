@@ -44,7 +44,8 @@ class Stats(C.Structure):
                                    "trial_cyc_total", "trial_cyc_tree", "trial_cyc_emit", "trial_blocks",
                                    "trial_cyc_heap", "trial_cyc_fallback", "trial_symbols",
                                    "n_trials_speculative", "n_reinflated", "n_inflate_retries", "n_trials_replayed", "n_replay_checked",
-                                   "n_trials_duplicate", "n_fast_restarts", "dev_bytes_peak", "dev_bytes_held")]
+                                   "n_trials_duplicate", "n_fast_restarts", "dev_bytes_peak", "dev_bytes_held",
+                                   "n_trials_skipped")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -563,6 +563,14 @@ struct Pipe {
   KTimer kt;
   atz_stats_t stats{};
   DBuf d_trials, d_tres, d_out, d_syms, d_R, d_mjobs, d_diffjobs, d_diffpos, d_diffval, d_diffcnt, d_djobs;
+  // speculative rounds: per stream, the lowest place in the round of a trial that stops it
+  // (SweepArgs::stopj); stopj_cur is the round's (null: no flag)
+  DBuf d_stopj;
+  uint32_t* stopj_cur = nullptr;
+  // and the idents of its TR_FULL trials (SweepArgs::rbest, rbK places per stream; null: none)
+  DBuf d_rbest;
+  uint64_t* rbest_cur = nullptr;
+  uint32_t rbK = 0;
   // round-local bucket tables (the context's cache is full): one buffer per ensure_chains call of the
   // round (a later call must not move an earlier call's tables), kept for the next rounds' reuse
   std::vector<std::unique_ptr<DBuf>> d_chains;
@@ -1770,12 +1778,24 @@ static uint64_t sym_words(int kind, uint32_t memlevel, uint64_t n) {   // symbol
 // A launch lasts as long as its slowest wave, so the trials go in longest-expected-first order
 // (classic LPT): low memLevels mean many blocks (one tree build each), fast levels mean hole
 // fallbacks, and the work grows with the stream.  Multi-wave trials lead each kind (a launch of their own).
+// ATZ_STOPFLAG=0: speculative rounds without the stop flag (SweepArgs::stopj): every trial of a round
+// runs to its own end
+static bool stopflag_on() {
+  static const bool v = [] { const char* e = std::getenv("ATZ_STOPFLAG"); return !e || std::atoi(e) != 0; }();
+  return v;
+}
+// ATZ_RBEST=0: a speculative trial's "cannot beat" bound stays its round-start ident (SweepArgs::rbest)
+static bool rbest_on() {
+  static const bool v = [] { const char* e = std::getenv("ATZ_RBEST"); return !e || std::atoi(e) != 0; }();
+  return v;
+}
 static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
   for (int k = 0; k < 3; k++) {
     const size_t n = in[k].size();
     S.perm[k].resize(n);
-    // one 64-bit key per trial, sorted descending: multi-wave bit, expected work (< 2^38), then the
-    // index complemented (ties keep the caller's order, as a stable sort would)
+    // one 64-bit key per trial, sorted descending: multi-wave bit, the place in the round (stop flag),
+    // expected work (< 2^38), then the index complemented (ties keep the caller's order, as a stable
+    // sort would)
     std::vector<uint64_t> key(n);
     const uint32_t mwm = mw_max_memlevel();
     const bool packed = n < (1u << 20);
@@ -1784,7 +1804,10 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
       const uint64_t w = x->recs[t.stream].infl_len * (uint64_t)(k == 1 ? 3 : 1) * (uint64_t)(10 - t.memlevel) *
                          (uint64_t)((t.mode & 8) ? 1 : 4);   // replays skip the match walks
       const uint64_t mw = k != 0 && t.memlevel <= mwm;
-      key[q] = packed ? (mw << 63) | (std::min<uint64_t>(w, (1ull << 42) - 1) << 20) | ((1u << 20) - 1 - q) : w;
+      // with the stop flag or round bests, a stream's earlier trials of the round first: what they find
+      // ends or bounds the later ones
+      const uint64_t jr = stopflag_on() || rbest_on() ? 15 - std::min<uint32_t>(t.spec_j, 15) : 0;
+      key[q] = packed ? (mw << 63) | (jr << 59) | (std::min<uint64_t>(w, (1ull << 39) - 1) << 20) | ((1u << 20) - 1 - q) : w;
       S.perm[k][q] = (uint32_t)q;
     }
     if (packed) {
@@ -1821,6 +1844,7 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
     A.streams = x->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + b1;
     A.res = c->d_tres.as<TrialRes>() + b1; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
     A.adler = x->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)n1;
+    A.stopj = c->stopj_cur; A.rbest = c->rbest_cur; A.rbK = c->rbK;
     dim3 g((uint32_t)n1), b(mw ? MW_THREADS : 64);
     kbeg(c, 0);
     if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
@@ -2070,7 +2094,9 @@ static void level_record(atz_ctx* x, std::vector<StreamState>& ss, const std::ve
     const Trial& t = slow[q];
     const TrialRes& r = res[q];
     if (!mine(t.stream)) continue;
-    if (t.clevel < 7 || t.clevel > 9 || (t.mode & 128) || r.state == TR_NEED_R || r.state == TR_OVERFLOW) continue;
+    if (t.clevel < 7 || t.clevel > 9 || (t.mode & 128) || r.state == TR_NEED_R || r.state == TR_OVERFLOW ||
+        r.state == TR_SKIPPED)
+      continue;
     if (!budget_free(x, 2, t)) continue;
     StreamState& st = ss[t.stream];
     bool have = false;
@@ -2210,6 +2236,7 @@ static void account_trial(atz_ctx* x, Pipe* c, int k, const Trial& t, const Tria
   c->stats.trial_parsed_bytes += r.parsed;
   c->stats.n_fast_fallbacks += r.fallbacks & 0xffffffffull;
   c->stats.n_fast_restarts += r.fallbacks >> 32;
+  c->stats.n_trials_skipped += r.state == TR_SKIPPED;
   c->stats.trial_cyc_total += r.cyc_total; c->stats.trial_cyc_tree += r.cyc_tree;
   c->stats.trial_cyc_emit += r.cyc_emit; c->stats.trial_blocks += r.blocks;
   c->stats.trial_cyc_heap += r.cyc_heap; c->stats.trial_cyc_fallback += r.cyc_fallback;
@@ -2220,7 +2247,7 @@ static void account_trial(atz_ctx* x, Pipe* c, int k, const Trial& t, const Tria
   for (int i = 0; i < 4; i++) gk[10 + i] += r.cyc_sec[i];
   // trial input read + compare read (bytes emitted and compared against the original)
   if (!(t.mode & 128))   // duplicates are not launched; a trial never rerun stopped at its prefix
-    c->stats.k_trial_alg_bytes += r.state == TR_NEED_R ? r.parsed
+    c->stats.k_trial_alg_bytes += r.state == TR_NEED_R || r.state == TR_SKIPPED ? r.parsed
                                   : x->recs[t.stream].infl_len + (r.out_len < C ? r.out_len : C);
   if (timing_level() >= 3 && !(t.mode & 128)) {
     c->diag_rt.push_back({r.rt0, r.rt1});
@@ -2290,6 +2317,7 @@ struct Round {
         Trial t{};
         t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
         t.best_ident = st.ident;
+        t.spec_j = j; t.spec_a = (uint32_t)a;
         t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
         const int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
@@ -2319,6 +2347,20 @@ struct Round {
   int plan() {
     c->r_next = 0;   // the round's match tables (early ones below, the rest in launch) never move
     if (int r = c->d_R.reserve(r_bound * sizeof(uint2) + 4096)) return r;
+    c->stopj_cur = nullptr;
+    if (K > 1 && stopflag_on()) {   // ~0 per stream: no stop found yet (stream-ordered before the trials)
+      if (int r = c->d_stopj.reserve(x->recs.size() * sizeof(uint32_t) + 64)) return r;
+      HIPCHK(hipMemsetAsync(c->d_stopj.p, 0xff, x->recs.size() * sizeof(uint32_t), c->st));
+      c->stopj_cur = c->d_stopj.as<uint32_t>();
+    }
+    c->rbest_cur = nullptr;
+    if (K > 1 && rbest_on()) {   // 0: no ident yet
+      const size_t nb = active.size() * (size_t)K * sizeof(uint64_t);
+      if (int r = c->d_rbest.reserve(nb + 64)) return r;
+      HIPCHK(hipMemsetAsync(c->d_rbest.p, 0, nb, c->st));
+      c->rbest_cur = c->d_rbest.as<uint64_t>();
+      c->rbK = K;
+    }
     if (replay_on() && x->depth_pin.p) {
       // Replay planning reads the pairs' deepest buckets.  A trial that can only parse (its stream has no
       // saved sequence at its (level, window) to replay, nor a higher level's run to duplicate) needs its
@@ -2510,6 +2552,7 @@ struct Round {
         held[a] = 1;
         return 0;
       }
+      if (r.state == TR_SKIPPED) return ATZ_E_INTERNAL;   // only trials past the stream's stop end so
       st.trials++;
       ntr++;
       if (r.state == TR_SHORTCUT) nsc++;
@@ -2699,6 +2742,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     struct Give {   // the batch goes back on every exit from the round (an error aborts the sweep anyway)
       atz_ctx* x; Pipe* c; const std::vector<StreamState>& ss; const std::vector<uint32_t>& a, &w;
       ~Give() {
+        c->stopj_cur = nullptr; c->rbest_cur = nullptr;
         forget_tmp_chains(x, c);
         sched_give(x, c->id, ss, a, w);
       }
@@ -2922,7 +2966,7 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
     t.trial_cyc_total += q.trial_cyc_total; t.trial_cyc_tree += q.trial_cyc_tree; t.trial_cyc_emit += q.trial_cyc_emit;
     t.trial_blocks += q.trial_blocks; t.trial_cyc_heap += q.trial_cyc_heap; t.trial_cyc_fallback += q.trial_cyc_fallback;
     t.trial_symbols += q.trial_symbols; t.n_trials_replayed += q.n_trials_replayed; t.n_replay_checked += q.n_replay_checked;
-    t.n_trials_duplicate += q.n_trials_duplicate;
+    t.n_trials_duplicate += q.n_trials_duplicate; t.n_trials_skipped += q.n_trials_skipped;
     tch = std::max(tch, p->t_chains); ttr = std::max(ttr, p->t_trials); tap = std::max(tap, p->t_apply);
     for (int k = 0; k < 3; k++) for (int l = 0; l < 10; l++) for (int i = 0; i < 14; i++) kind[k][l][i] += p->kind[k][l][i];
   }

@@ -63,6 +63,10 @@ struct Trial {
   uint64_t rp_syms;     // absolute device address (u32 symbols)
   uint64_t rp_tab;      // absolute device address (uint2 match-table entries)
   uint32_t rp_nsym, rp_flags;
+  // speculative rounds: the trial's place among its stream's trials of the round (0: the first); a trial
+  // whose stream an earlier one of the round has already stopped ends at once (SweepArgs::stopj); the
+  // stream's slot in the round (SweepArgs::rbest)
+  uint32_t spec_j, spec_a;
 };
 
 // ---- match tables (k_match) ----------------------------------------------------------------
@@ -115,6 +119,7 @@ enum : uint32_t {
   TR_CANT_BEAT = 3,   // stopped: cannot exceed best_ident (result irrelevant to the sweep)
   TR_OVERFLOW = 4,    // output capacity exceeded (host treats as reference abort)
   TR_NEED_R = 5,      // parse reached x_lim: extend the match table and run the trial again
+  TR_SKIPPED = 6,     // an earlier trial of its stream in the round stops the stream: never walked
 };
 
 struct SweepOpts {

@@ -993,6 +993,14 @@ struct SweepArgs {
   const StreamDev* streams;
   const Trial* trials;
   TrialRes* res;
+  // speculative rounds: per stream, the lowest Trial::spec_j of the round whose result stops the stream
+  // (reference's rule, main.cpp:685-700; ~0: none yet), or null
+  uint32_t* stopj;
+  // speculative rounds: the idents of the round's TR_FULL trials, rbest[spec_a * rbK + spec_j] (0: none
+  // yet), or null.  A trial's result matters only if it beats every earlier trial of its stream, so
+  // those idents raise its "cannot beat" bound (the stream's rule walks them first, main.cpp:685-700).
+  uint64_t* rbest;
+  uint32_t rbK;
   uint8_t* out;                 // per-trial output scratch (Trial::out_off)
   uint32_t* syms;               // symbol buffers (Trial::sym_off)
   const uint32_t* adler;        // per-stream Adler-32 of the inflated data
@@ -1847,6 +1855,24 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t cnt, uint64_t lt, uin
 }
 
 // One flusher wave of a multi-wave trial: blocks f, f + MW_F, f + 2 MW_F, ... (see MWSlot).
+// Speculative rounds (SweepArgs::stopj).  A trial whose result stops its stream -- full output, its ident
+// within mismatch_tol of C and above the best it started from -- records its place in the round; the
+// stream's rule walk stops there or earlier (any earlier trial reaching C - tol also stops it), so its
+// later trials of the round are never walked and may end at once.  (Relaxed device-scope atomics: a
+// trial that misses a fresh value only runs to its end, as without the flag.)
+__device__ __forceinline__ bool spec_stopped(const SweepArgs& A, const Trial& tr) {
+  if (!A.stopj || !tr.spec_j) return false;
+  return uni(__hip_atomic_load(A.stopj + tr.stream, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < tr.spec_j;
+}
+__device__ __forceinline__ void spec_stop(const SweepArgs& A, const Trial& tr, uint32_t state, uint64_t ident,
+                                          uint64_t clen, int lane) {
+  if (A.rbest && state == TR_FULL && lane == 0)
+    __hip_atomic_store(A.rbest + (uint64_t)tr.spec_a * A.rbK + tr.spec_j, ident, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!A.stopj || state != TR_FULL || ident <= tr.best_ident) return;
+  if (ident != clen && ident + A.o.mismatch_tol < clen) return;
+  if (lane == 0) __hip_atomic_fetch_min(A.stopj + tr.stream, tr.spec_j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ void trial_flusher(const SweepArgs& A, LDS TrialShared& s, LDS MWPart& mw, const Trial& tr,
                               const GLOBAL uint32_t* syms, const GLOBAL uint8_t* in, uint32_t level, uint32_t lbs,
                               bool full_needed, int f, int lane) {
@@ -1905,6 +1931,7 @@ __device__ void trial_flusher(const SweepArgs& A, LDS TrialShared& s, LDS MWPart
       st = uni(early_exit(b, A.o, tr.best_ident, full_needed));
     }
     if (lane == 0) { me.cyc_tree += c1 - c0; me.cyc_emit += clock64() - c2; }
+    if (last) spec_stop(A, tr, st, uni(b.eq_all), uni(b.clen), lane);
     if (st != ~0u) {
       if (lane == 0) ctl.state = st;
       st_rel(ctl.stop, 1u, lane);
@@ -1931,6 +1958,7 @@ struct TrialRun {
   LDS BitOut& b;
   const uint32_t t;
   const Trial tr;
+  uint64_t best;   // the "cannot beat" bound: tr.best_ident, raised by the round's earlier trials (SweepArgs::rbest)
   const StreamDev sd;
   const uint8_t* const in;
   // hash buckets of (stream, memLevel): sidx[npad] then bpos[npad]
@@ -1967,7 +1995,7 @@ struct TrialRun {
 
   __device__ __forceinline__ TrialRun(const SweepArgs& A_, SH& shm_, int lane_)
       : A(A_), shm(shm_), lane(lane_), wave(MW ? (int)(threadIdx.x >> 6) : 0), s(*(LDS TrialShared*)&shm_.t),
-        stg((LDS uint32_t*)shm_.ring), b(s.b), t(blockIdx.x), tr(A_.trials[t]), sd(A_.streams[tr.stream]),
+        stg((LDS uint32_t*)shm_.ring), b(s.b), t(blockIdx.x), tr(A_.trials[t]), best(tr.best_ident), sd(A_.streams[tr.stream]),
         in(A_.infl + sd.infl_off), npad((uint32_t)((sd.infl_len + 63) & ~63ull)),
         sidx(KIND == 0 ? nullptr : A_.chains + tr.chain_off), bpos(KIND == 0 ? nullptr : sidx + npad),
         full_needed(tr.mode & 1), lt(lane_ ? (~0ull >> (64 - lane_)) : 0ull) {
@@ -2075,10 +2103,24 @@ struct TrialRun {
       }
       return true;
   }
+  // the round's earlier trials of the stream that ended with full output: their best ident
+  __device__ __forceinline__ void refresh_best() {
+      if (!A.rbest || !tr.spec_j) return;
+      uint64_t v = (uint32_t)lane < tr.spec_j
+                       ? __hip_atomic_load(A.rbest + (uint64_t)tr.spec_a * A.rbK + (uint32_t)lane, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                       : 0ull;
+      for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t o = __shfl_xor(v, d, 64);
+        v = v > o ? v : o;
+      }
+      v = uni(v);
+      if (v > best) best = v;
+  }
   __device__ __forceinline__ void FLUSH(int last) {
       hazard |= uni(flush_block(s, *(LDS TreeScratch*)shm.ring, b, (const GLOBAL uint32_t*)syms + ((saving || replay) ? sbase : 0u),
                                 (const GLOBAL uint8_t*)in, (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last,
-                                A.o, tr.best_ident, full_needed, lane));
+                                A.o, best, full_needed, lane));
       sbase += z.last_lit;
       z.last_lit = 0;
       z.block_start = z.p;
@@ -2094,8 +2136,10 @@ struct TrialRun {
       if constexpr (MW) {
         return publish(0) ? ~0u : TR_DECIDED;
       } else {
+        refresh_best();
         FLUSH(0);
-        return uni(early_exit(b, A.o, tr.best_ident, full_needed));
+        const uint32_t e = uni(early_exit(b, A.o, best, full_needed));
+        return e == ~0u && spec_stopped(A, tr) ? TR_SKIPPED : e;
       }
   }
 
@@ -2738,6 +2782,7 @@ struct TrialRun {
       else if (ad2 > A.o.sizediff_tresh) state = TR_SIZEDIFF;
       else state = TR_FULL;
     }
+    spec_stop(A, tr, state, uni(b.eq_all), uni(b.clen), lane);
   }
   if constexpr (MW) {   // no more blocks: flushers waiting past the last one stop; TR_NEED_R abandons the rest
     LDS MWCtl& ctl = (*(LDS MWPart*)&shm.mw).ctl;
@@ -2810,13 +2855,20 @@ struct TrialRun {
           mw.ctl.next_emit = 0; mw.ctl.stop = 0; mw.ctl.parse_done = 0; mw.ctl.nblocks = 0;
           mw.ctl.state = ~0u; mw.ctl.hazard = 0;
         }
+        if (spec_stopped(A, tr)) {   // decided before any flusher starts
+          state = TR_SKIPPED;
+          if (lane == 0) { mw.ctl.state = TR_SKIPPED; mw.ctl.stop = 1; }
+        }
       }
       __syncthreads();
       if (wave != 0)
         trial_flusher(A, s, mw, tr, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, z.level, z.lbs, full_needed,
                       wave - 1, lane);
     }
-    if (wave == 0) {   // the parse; every wave of a single-wave trial
+    if constexpr (!MW) if (spec_stopped(A, tr)) state = TR_SKIPPED;
+    if (wave == 0 && state == TR_SKIPPED) {
+      end_parse();
+    } else if (wave == 0) {   // the parse; every wave of a single-wave trial
       parse_setup();
       if constexpr (KIND == 0) parse_stored();
       else if (replay) parse_replay();

@@ -87,6 +87,7 @@ typedef struct {
     /* device memory the library held in this process (every context's buffers): the peak during the call,
        and what stays allocated after it (kept for the next call's reuse) */
     uint64_t dev_bytes_peak, dev_bytes_held;
+    uint64_t n_trials_skipped;                           /* speculative trials ended by an earlier trial's stop */
 } atz_stats_t;
 
 enum {

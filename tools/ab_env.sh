@@ -14,6 +14,6 @@ for ((i=1;i<=R;i++)); do
     k=$((k+1))
     [ "$E" = "-" ] && E=""
     env $E timeout -k 10 240 python3 bench.py --streams ${AB_STREAMS:-100000} --steps 3 --warmup 1 --no-cpu --no-recon --no-h2h > gpurun_out/$TAG/v$k.$i.json 2> gpurun_out/$TAG/v$k.$i.err || exit 1
-    echo "v$k.$i [$E] $(python3 -c "import json;d=json.load(open('gpurun_out/$TAG/v$k.$i.json'));print(d['value'],d['ms_per_step'],(d.get('atz_parity') or {}).get('identical_to_reference'),{x:d['detail'].get(x) for x in ('k_trial_ms','k_match_ms','k_chains_ms','k_inflate_ms','n_trials','n_trials_replayed','n_replay_checked','n_trials_duplicate')})")"
+    echo "v$k.$i [$E] $(python3 -c "import json;d=json.load(open('gpurun_out/$TAG/v$k.$i.json'));print(d['value'],d['ms_per_step'],(d.get('atz_parity') or {}).get('identical_to_reference'),{x:d['detail'].get(x) for x in ('k_trial_ms','k_match_ms','k_chains_ms','k_inflate_ms','n_trials','n_trials_replayed','n_replay_checked','n_trials_duplicate','n_trials_speculative','n_trials_skipped')})")"
   done
 done
