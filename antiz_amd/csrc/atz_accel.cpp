@@ -567,6 +567,7 @@ struct Pipe {
   // (SweepArgs::stopj); stopj_cur is the round's (null: no flag)
   DBuf d_stopj;
   uint32_t* stopj_cur = nullptr;
+  uint32_t mw_cap = 2;   // multi-wave trials up to this memLevel (mw_cap_for, set per round)
   // and the idents of its TR_FULL trials (SweepArgs::rbest, rbK places per stream; null: none)
   DBuf d_rbest;
   uint64_t* rbest_cur = nullptr;
@@ -689,6 +690,7 @@ struct atz_ctx {
   std::vector<std::unique_ptr<Pipe>> pipes;
   std::vector<std::unique_ptr<DBuf>> slabs;   // inflated records, one allocation per scan piece
   size_t pipes_running = 1;
+  size_t sweep_nmax = 0;   // the sweep's bound on its streams (sweep_begin)
   std::atomic<bool> sweep_abort{false};   // the pipes stop at their next round (a withdrawn speculative scan)
   // precompress_dev's large per-call state, kept so its capacity survives the calls
   std::shared_ptr<struct ScanState> scan_keep;
@@ -1766,13 +1768,16 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
 // 484-498)
 // (k_trial_{fast,slow}_mw: one parse wave, MW_F flusher waves; k_deflate.hip MWSlot).  Their symbols
 // stay in HBM for the whole stream (the flushers read each block at its own offset).
-static uint32_t mw_max_memlevel() {   // ATZ_MW=m: multi-wave up to memLevel m (0: none; tests/test_gpu_knobs.py)
-  static const int v = [] { const char* e = std::getenv("ATZ_MW"); return (int)(e ? std::max(0, std::min(9, std::atoi(e))) : 2); }();
-  return (uint32_t)v;
+// Multi-wave trials up to memLevel Pipe::mw_cap: 2, or 4 in a sweep of at most 16 000 streams (one
+// rank's share at 8 GPUs), whose rounds wait for their slowest trials: a multi-wave trial ends sooner,
+// at more cost.  ATZ_MW=m forces m (0: none; tests/test_gpu_knobs.py).
+static uint32_t mw_cap_for(size_t n_streams) {
+  static const int v = [] { const char* e = std::getenv("ATZ_MW"); return (int)(e ? std::max(0, std::min(9, std::atoi(e))) : -1); }();
+  return v >= 0 ? (uint32_t)v : n_streams <= 16000 ? 4u : 2u;
 }
-static bool mw_trial(int kind, uint32_t memlevel) { return kind != 0 && memlevel <= mw_max_memlevel(); }
-static uint64_t sym_words(int kind, uint32_t memlevel, uint64_t n) {   // symbol buffer of a trial (u32 units)
-  return (mw_trial(kind, memlevel) ? n + 64 : 0) + (1ull << (memlevel + 6)) + 64;
+static bool mw_trial(const Pipe* c, int kind, uint32_t memlevel) { return kind != 0 && memlevel <= c->mw_cap; }
+static uint64_t sym_words(const Pipe* c, int kind, uint32_t memlevel, uint64_t n) {   // symbol buffer of a trial (u32 units)
+  return (mw_trial(c, kind, memlevel) ? n + 64 : 0) + (1ull << (memlevel + 6)) + 64;
 }
 
 // A launch lasts as long as its slowest wave, so the trials go in longest-expected-first order
@@ -1789,7 +1794,7 @@ static bool rbest_on() {
   static const bool v = [] { const char* e = std::getenv("ATZ_RBEST"); return !e || std::atoi(e) != 0; }();
   return v;
 }
-static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
+static void trials_order(atz_ctx* x, const Pipe* c, std::vector<Trial>* in, TrialSet& S) {
   for (int k = 0; k < 3; k++) {
     const size_t n = in[k].size();
     S.perm[k].resize(n);
@@ -1797,7 +1802,7 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
     // expected work (< 2^38), then the index complemented (ties keep the caller's order, as a stable
     // sort would)
     std::vector<uint64_t> key(n);
-    const uint32_t mwm = mw_max_memlevel();
+    const uint32_t mwm = c->mw_cap;
     const bool packed = n < (1u << 20);
     for (size_t q = 0; q < n; q++) {
       const Trial& t = in[k][q];
@@ -1815,7 +1820,7 @@ static void trials_order(atz_ctx* x, std::vector<Trial>* in, TrialSet& S) {
       for (size_t q = 0; q < n; q++) S.perm[k][q] = (uint32_t)((1u << 20) - 1 - (key[q] & ((1u << 20) - 1)));
     } else {
       std::stable_sort(S.perm[k].begin(), S.perm[k].end(), [&](uint32_t a, uint32_t b) {
-        const bool ma = mw_trial(k, in[k][a].memlevel), mb = mw_trial(k, in[k][b].memlevel);
+        const bool ma = mw_trial(c, k, in[k][a].memlevel), mb = mw_trial(c, k, in[k][b].memlevel);
         return ma != mb ? ma : key[a] > key[b];
       });
     }
@@ -1830,9 +1835,9 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
                          size_t cnt, size_t base) {
   // the trial descriptors first, then the launches
   for (size_t i = 0; i < cnt;) {
-    const bool mw = mw_trial(k, h[i].memlevel);
+    const bool mw = mw_trial(c, k, h[i].memlevel);
     size_t j = i + 1;
-    while (j < cnt && mw_trial(k, h[j].memlevel) == mw) j++;
+    while (j < cnt && mw_trial(c, k, h[j].memlevel) == mw) j++;
     HIPCHK(pipe_copy(c, c->d_trials.as<Trial>() + base + i, h + i, (j - i) * sizeof(Trial), hipMemcpyHostToDevice));
     i = j;
   }
@@ -1858,9 +1863,9 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
   };
   size_t i = 0;
   while (i < cnt) {   // runs of equal multi-wave-ness: trials_order made them contiguous
-    const bool mw = mw_trial(k, h[i].memlevel);
+    const bool mw = mw_trial(c, k, h[i].memlevel);
     size_t j = i + 1;
-    while (j < cnt && mw_trial(k, h[j].memlevel) == mw) j++;
+    while (j < cnt && mw_trial(c, k, h[j].memlevel) == mw) j++;
     if (int r = launch1(h + i, j - i, base + i, mw)) return r;
     i = j;
   }
@@ -2005,7 +2010,7 @@ static void trials_results(const TrialSet& S, std::vector<TrialRes>* res) {
 static int run_trials(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, std::vector<Trial>* tr, const SweepOpts& so,
                       std::vector<TrialRes>* res) {
   TrialSet S;
-  trials_order(x, tr, S);
+  trials_order(x, c, tr, S);
   c->r_next = 0;
   if (int r = trials_first(x, c, d_cmp, S, so)) return r;
   if (int r = trials_rerun(x, c, d_cmp, S, so, nullptr)) return r;
@@ -2296,6 +2301,7 @@ struct Round {
   // The trials of the next K list entries of every stream, within the round's scratch budget.
   void build_lists() {
     K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, round_target(x) / active.size()));
+    c->mw_cap = mw_cap_for(x->sweep_nmax);
     mbeg.assign(active.size() + 1, 0);
     mine.reserve(active.size() * K);
     uint64_t round_bytes = 0;
@@ -2321,7 +2327,7 @@ struct Round {
         t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
         const int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
-        const uint64_t sw = sym_words(kind, (uint32_t)m, x->recs[s].infl_len);
+        const uint64_t sw = sym_words(c, kind, (uint32_t)m, x->recs[s].infl_len);
         t.sym_off = sym_tot; sym_tot += sw;
         round_bytes += 8 * (x->recs[s].infl_len + 320) + t.out_cap + 4 * sw;
         if (kind) {
@@ -2498,7 +2504,7 @@ struct Round {
           ia[k].push_back(q);
         }
       }
-      trials_order(x, ta, SA);
+      trials_order(x, c, ta, SA);
     }
     c->lap(5);
     {
@@ -2527,7 +2533,7 @@ struct Round {
         t3[k].push_back(t);
         ib[k].push_back(q);
       }
-    trials_order(x, t3, SB);
+    trials_order(x, c, t3, SB);
     if (int r = trials_first(x, c, d_file, SB, so)) return r;
     collect(SB, ib);
     return 0;
@@ -2878,6 +2884,7 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
   if (int r = c->d_streams.reserve(n_max * sizeof(StreamDev) + 4096)) return r;
   R.np = std::max<size_t>(1, std::min(sweep_pipes(n_max), (n_max + 255) / 256));
   c->pipes_running = R.np;
+  c->sweep_nmax = n_max;
   if (int r = ensure_pipes(c, R.np)) return r;
   {
     auto& Q = c->sched;
@@ -3356,6 +3363,7 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
   if (int r = ensure_pipes(c, 1)) return r;
   HIPCHK(hipStreamSynchronize(c->st));   // tables (context stream) before the pipe's kernels
   Pipe* p = c->pipes[0].get();
+  p->mw_cap = mw_cap_for(~(size_t)0);   // the large-sweep cap (or ATZ_MW)
   if (int r = c->d_tmp.reserve(4096)) return r;   // zero-length "file" for the compare side
   const uint64_t budget = ROUND_BUDGET_BYTES;
   for (size_t s0 = 0; s0 < n;) {
@@ -3364,7 +3372,7 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
     uint64_t bytes = 0;
     while (s1 < n && (s1 == s0 || bytes <= budget)) {
       const int m = (int)(params[s1] & 0xff);
-      bytes += 9 * len[s1] + 4 * sym_words(1, (uint32_t)m, len[s1]) + 4096;
+      bytes += 9 * len[s1] + 4 * sym_words(p, 1, (uint32_t)m, len[s1]) + 4096;
       s1++;
     }
     c->chain_off.assign(n, {});
@@ -3386,7 +3394,7 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
       t.best_ident = 0; t.out_off = out_tot; t.out_cap = bound(len[s], w, m) + 64;
       out_tot += (t.out_cap + 255) & ~255ull;
       const int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
-      t.sym_off = sym_tot; sym_tot += sym_words(kind, (uint32_t)m, len[s]);
+      t.sym_off = sym_tot; sym_tot += sym_words(p, kind, (uint32_t)m, len[s]);
       if (kind) t.chain_off = c->chain_off[s][m];
       tr[kind].push_back(t);
       idx[kind].push_back((uint32_t)s);

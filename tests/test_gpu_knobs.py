@@ -10,7 +10,8 @@ the ATZ1 bytes must equal the oracle's (the reference's algorithm, oracle/) for 
   ATZ_TARGET   trials per round and pipe (speculation depth; default 8192 for a sweep of at most 32 000
                streams, else 4096)
   ATZ_SPEC_CONT 0: the scan waits for the first chunk-boundary continuations (default 1: speculative)
-  ATZ_MW       multi-wave trials up to this memLevel (default 2; 0: every trial on one wave)
+  ATZ_MW       multi-wave trials up to this memLevel (default 2, 4 in sweeps of at most 16 000 streams;
+               0: every trial on one wave)
   ATZ_MHINT    0 / 1: whole match tables for the first block's memLevel off / on (default: above 16 000
                streams, or on six or more pipes: atz_accel.cpp big_sweep)
   ATZ_PREFIX_MIN the match-table prefix floor in positions (default 3072 where big_sweep holds, else 1024)
@@ -38,7 +39,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SETTINGS = [{"ATZ_REPLAY": "0"}, {"ATZ_REPLAY": "2"}, {"ATZ_REPLAY": "3"}, {"ATZ_DEDUP": "0"},
             {"ATZ_PIPES": "1"}, {"ATZ_PIPES": "5"}, {"GPU_MAX_HW_QUEUES": "8"}, {"ATZ_TARGET": "256"}, {"ATZ_TARGET": "65536"},
-            {"ATZ_SPEC_CONT": "0"}, {"ATZ_MW": "0"}, {"ATZ_MW": "9"}, {"ATZ_REPLAY": "0", "ATZ_DEDUP": "0", "ATZ_PIPES": "2", "ATZ_SPEC_CONT": "0"},
+            {"ATZ_SPEC_CONT": "0"}, {"ATZ_MW": "0"}, {"ATZ_MW": "2"}, {"ATZ_MW": "9"}, {"ATZ_REPLAY": "0", "ATZ_DEDUP": "0", "ATZ_PIPES": "2", "ATZ_SPEC_CONT": "0"},
             {"ATZ_PIPES": "8", "ATZ_TARGET": "256"}, {"ATZ_PIPES": "6", "ATZ_TARGET": "65536"},
             {"ATZ_MHINT": "1"}, {"ATZ_MHINT": "0"}, {"ATZ_PREFIX_MIN": "3072", "ATZ_MHINT": "1"},
             {"ATZ_ELIG": "0"}, {"ATZ_ELIG": "0", "ATZ_REPLAY": "0"},
