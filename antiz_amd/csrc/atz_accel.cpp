@@ -1768,9 +1768,10 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
 // 484-498)
 // (k_trial_{fast,slow}_mw: one parse wave, MW_F flusher waves; k_deflate.hip MWSlot).  Their symbols
 // stay in HBM for the whole stream (the flushers read each block at its own offset).
-// Multi-wave trials up to memLevel Pipe::mw_cap: 2, or 4 in a sweep of at most 16 000 streams (one
-// rank's share at 8 GPUs), whose rounds wait for their slowest trials: a multi-wave trial ends sooner,
-// at more cost.  ATZ_MW=m forces m (0: none; tests/test_gpu_knobs.py).
+// Multi-wave trials up to memLevel Pipe::mw_cap: 2, or 4 for a round of a sweep with at most 16 000
+// streams left (about: the pipe's batch times the pipes) -- one rank's share at 8 GPUs, the late rounds
+// of a full file -- whose rounds wait for their slowest trials: a multi-wave trial ends sooner, at more
+// cost.  ATZ_MW=m forces m (0: none; tests/test_gpu_knobs.py).
 static uint32_t mw_cap_for(size_t n_streams) {
   static const int v = [] { const char* e = std::getenv("ATZ_MW"); return (int)(e ? std::max(0, std::min(9, std::atoi(e))) : -1); }();
   return v >= 0 ? (uint32_t)v : n_streams <= 16000 ? 4u : 2u;
@@ -2301,7 +2302,7 @@ struct Round {
   // The trials of the next K list entries of every stream, within the round's scratch budget.
   void build_lists() {
     K = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, round_target(x) / active.size()));
-    c->mw_cap = mw_cap_for(x->sweep_nmax);
+    c->mw_cap = mw_cap_for(std::min(x->sweep_nmax, active.size() * x->pipes_running));
     mbeg.assign(active.size() + 1, 0);
     mine.reserve(active.size() * K);
     uint64_t round_bytes = 0;

@@ -10,7 +10,7 @@ the ATZ1 bytes must equal the oracle's (the reference's algorithm, oracle/) for 
   ATZ_TARGET   trials per round and pipe (speculation depth; default 8192 for a sweep of at most 32 000
                streams, else 4096)
   ATZ_SPEC_CONT 0: the scan waits for the first chunk-boundary continuations (default 1: speculative)
-  ATZ_MW       multi-wave trials up to this memLevel (default 2, 4 in sweeps of at most 16 000 streams;
+  ATZ_MW       multi-wave trials up to this memLevel (default 2, 4 in rounds with at most 16 000 streams left;
                0: every trial on one wave)
   ATZ_MHINT    0 / 1: whole match tables for the first block's memLevel off / on (default: above 16 000
                streams, or on six or more pipes: atz_accel.cpp big_sweep)
