@@ -935,7 +935,10 @@ static_assert(STAGE_WORDS * 4 <= RING_SLOW * sizeof(uint64_t), "emission staging
 // side by side and emit them strictly in block order, each block appending to the one bit output
 // and comparing it with the original.  A flusher that decides the trial (the early-exit gates, or
 // the final gates after the last block) raises `stop`; the parser checks it at every hand-over.
-static constexpr int MW_F = 3;   // flusher waves per multi-wave trial
+#ifndef ATZ_MW_F
+#define ATZ_MW_F 3
+#endif
+static constexpr int MW_F = ATZ_MW_F;   // flusher waves per multi-wave trial
 struct MWSlot {                  // a finished block waiting for its flusher
   BlockFreq f;
   int64_t block_start;
