@@ -568,10 +568,6 @@ struct Pipe {
   DBuf d_stopj;
   uint32_t* stopj_cur = nullptr;
   uint32_t mw_cap = 2;   // multi-wave trials up to this memLevel (mw_cap_for, set per round)
-  // and the idents of its TR_FULL trials (SweepArgs::rbest, rbK places per stream; null: none)
-  DBuf d_rbest;
-  uint64_t* rbest_cur = nullptr;
-  uint32_t rbK = 0;
   // round-local bucket tables (the context's cache is full): one buffer per ensure_chains call of the
   // round (a later call must not move an earlier call's tables), kept for the next rounds' reuse
   std::vector<std::unique_ptr<DBuf>> d_chains;
@@ -1790,11 +1786,6 @@ static bool stopflag_on() {
   static const bool v = [] { const char* e = std::getenv("ATZ_STOPFLAG"); return !e || std::atoi(e) != 0; }();
   return v;
 }
-// ATZ_RBEST=0: a speculative trial's "cannot beat" bound stays its round-start ident (SweepArgs::rbest)
-static bool rbest_on() {
-  static const bool v = [] { const char* e = std::getenv("ATZ_RBEST"); return !e || std::atoi(e) != 0; }();
-  return v;
-}
 static void trials_order(atz_ctx* x, const Pipe* c, std::vector<Trial>* in, TrialSet& S) {
   for (int k = 0; k < 3; k++) {
     const size_t n = in[k].size();
@@ -1810,9 +1801,9 @@ static void trials_order(atz_ctx* x, const Pipe* c, std::vector<Trial>* in, Tria
       const uint64_t w = x->recs[t.stream].infl_len * (uint64_t)(k == 1 ? 3 : 1) * (uint64_t)(10 - t.memlevel) *
                          (uint64_t)((t.mode & 8) ? 1 : 4);   // replays skip the match walks
       const uint64_t mw = k != 0 && t.memlevel <= mwm;
-      // with the stop flag or round bests, a stream's earlier trials of the round first: what they find
-      // ends or bounds the later ones
-      const uint64_t jr = stopflag_on() || rbest_on() ? 15 - std::min<uint32_t>(t.spec_j, 15) : 0;
+      // with the stop flag, a stream's earlier trials of the round first: a stop they find ends the later
+      // ones
+      const uint64_t jr = stopflag_on() ? 15 - std::min<uint32_t>(t.spec_j, 15) : 0;
       key[q] = packed ? (mw << 63) | (jr << 59) | (std::min<uint64_t>(w, (1ull << 39) - 1) << 20) | ((1u << 20) - 1 - q) : w;
       S.perm[k][q] = (uint32_t)q;
     }
@@ -1850,7 +1841,7 @@ static int trials_launch(atz_ctx* x, Pipe* c, const uint8_t* d_cmp, const SweepO
     A.streams = x->d_streams.as<StreamDev>(); A.trials = c->d_trials.as<Trial>() + b1;
     A.res = c->d_tres.as<TrialRes>() + b1; A.out = c->d_out.as<uint8_t>(); A.syms = c->d_syms.as<uint32_t>();
     A.adler = x->d_adler.as<uint32_t>(); A.o = so; A.ntrials = (uint32_t)n1;
-    A.stopj = c->stopj_cur; A.rbest = c->rbest_cur; A.rbK = c->rbK;
+    A.stopj = c->stopj_cur;
     dim3 g((uint32_t)n1), b(mw ? MW_THREADS : 64);
     kbeg(c, 0);
     if (k == 0) hipLaunchKernelGGL(k_trial_stored, g, b, 0, c->st, A);
@@ -2324,7 +2315,7 @@ struct Round {
         Trial t{};
         t.stream = s; t.clevel = (uint8_t)cl; t.window = (uint8_t)w; t.memlevel = (uint8_t)m; t.mode = 0;
         t.best_ident = st.ident;
-        t.spec_j = j; t.spec_a = (uint32_t)a;
+        t.spec_j = j;
         t.out_off = out_tot; t.out_cap = bound(x->recs[s].infl_len, w, m) + 64;
         out_tot += (t.out_cap + 255) & ~255ull;
         const int kind = cl == 0 ? 0 : cl <= 3 ? 1 : 2;
@@ -2359,14 +2350,6 @@ struct Round {
       if (int r = c->d_stopj.reserve(x->recs.size() * sizeof(uint32_t) + 64)) return r;
       HIPCHK(hipMemsetAsync(c->d_stopj.p, 0xff, x->recs.size() * sizeof(uint32_t), c->st));
       c->stopj_cur = c->d_stopj.as<uint32_t>();
-    }
-    c->rbest_cur = nullptr;
-    if (K > 1 && rbest_on()) {   // 0: no ident yet
-      const size_t nb = active.size() * (size_t)K * sizeof(uint64_t);
-      if (int r = c->d_rbest.reserve(nb + 64)) return r;
-      HIPCHK(hipMemsetAsync(c->d_rbest.p, 0, nb, c->st));
-      c->rbest_cur = c->d_rbest.as<uint64_t>();
-      c->rbK = K;
     }
     if (replay_on() && x->depth_pin.p) {
       // Replay planning reads the pairs' deepest buckets.  A trial that can only parse (its stream has no
@@ -2749,7 +2732,7 @@ static int sweep_pipe(atz_ctx* x, Pipe* c, const uint8_t* d_file, std::vector<St
     struct Give {   // the batch goes back on every exit from the round (an error aborts the sweep anyway)
       atz_ctx* x; Pipe* c; const std::vector<StreamState>& ss; const std::vector<uint32_t>& a, &w;
       ~Give() {
-        c->stopj_cur = nullptr; c->rbest_cur = nullptr;
+        c->stopj_cur = nullptr;
         forget_tmp_chains(x, c);
         sched_give(x, c->id, ss, a, w);
       }

@@ -64,9 +64,8 @@ struct Trial {
   uint64_t rp_tab;      // absolute device address (uint2 match-table entries)
   uint32_t rp_nsym, rp_flags;
   // speculative rounds: the trial's place among its stream's trials of the round (0: the first); a trial
-  // whose stream an earlier one of the round has already stopped ends at once (SweepArgs::stopj); the
-  // stream's slot in the round (SweepArgs::rbest)
-  uint32_t spec_j, spec_a;
+  // whose stream an earlier one of the round has already stopped ends at once (SweepArgs::stopj)
+  uint32_t spec_j, pad2_;
 };
 
 // ---- match tables (k_match) ----------------------------------------------------------------

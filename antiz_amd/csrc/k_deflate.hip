@@ -902,6 +902,8 @@ struct TrialShared {
   BitOut b;              // output / compare state of the trial (in LDS: the flush helpers take it by LDS reference)
   BlockFreq f;           // the block being parsed
   TreeCodes k;
+  uint64_t stop_at;      // speculative rounds: the stream's stop word (SweepArgs::stopj), 0: none
+  uint32_t stop_j, pad_; // the trial's place in the round
   // the bit-packing staging words (STAGE_WORDS) live in the match-table ring's LDS: they are only
   // used while a block is emitted, when the parse is paused (like TreeScratch during build_tree)
 };
@@ -999,11 +1001,6 @@ struct SweepArgs {
   // speculative rounds: per stream, the lowest Trial::spec_j of the round whose result stops the stream
   // (reference's rule, main.cpp:685-700; ~0: none yet), or null
   uint32_t* stopj;
-  // speculative rounds: the idents of the round's TR_FULL trials, rbest[spec_a * rbK + spec_j] (0: none
-  // yet), or null.  A trial's result matters only if it beats every earlier trial of its stream, so
-  // those idents raise its "cannot beat" bound (the stream's rule walks them first, main.cpp:685-700).
-  uint64_t* rbest;
-  uint32_t rbK;
   uint8_t* out;                 // per-trial output scratch (Trial::out_off)
   uint32_t* syms;               // symbol buffers (Trial::sym_off)
   const uint32_t* adler;        // per-stream Adler-32 of the inflated data
@@ -1863,17 +1860,26 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t cnt, uint64_t lt, uin
 // stream's rule walk stops there or earlier (any earlier trial reaching C - tol also stops it), so its
 // later trials of the round are never walked and may end at once.  (Relaxed device-scope atomics: a
 // trial that misses a fresh value only runs to its end, as without the flag.)
-__device__ __forceinline__ bool spec_stopped(const SweepArgs& A, const Trial& tr) {
-  if (!A.stopj || !tr.spec_j) return false;
-  return uni(__hip_atomic_load(A.stopj + tr.stream, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < tr.spec_j;
+// The stream's word and the trial's place sit in LDS (TrialShared::stop_at / stop_j, set at the trial's
+// start), so the parse loop keeps no registers for them.
+__device__ __forceinline__ void spec_init(LDS TrialShared& s, const SweepArgs& A, const Trial& tr, int lane) {
+  if (lane == 0) {
+    s.stop_at = A.stopj ? (uint64_t)(uintptr_t)(A.stopj + tr.stream) : 0ull;
+    s.stop_j = tr.spec_j;
+  }
 }
-__device__ __forceinline__ void spec_stop(const SweepArgs& A, const Trial& tr, uint32_t state, uint64_t ident,
-                                          uint64_t clen, int lane) {
-  if (A.rbest && state == TR_FULL && lane == 0)
-    __hip_atomic_store(A.rbest + (uint64_t)tr.spec_a * A.rbK + tr.spec_j, ident, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (!A.stopj || state != TR_FULL || ident <= tr.best_ident) return;
+__device__ __forceinline__ bool spec_stopped(const LDS TrialShared& s) {
+  const uint64_t a = uni(s.stop_at);
+  const uint32_t j = uni(s.stop_j);
+  if (!a || !j) return false;
+  return uni(__hip_atomic_load((const uint32_t*)(uintptr_t)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < j;
+}
+__device__ __forceinline__ void spec_stop(const LDS TrialShared& s, const SweepArgs& A, uint64_t best_ident, uint32_t state,
+                                          uint64_t ident, uint64_t clen, int lane) {
+  const uint64_t a = uni(s.stop_at);
+  if (!a || state != TR_FULL || ident <= best_ident) return;
   if (ident != clen && ident + A.o.mismatch_tol < clen) return;
-  if (lane == 0) __hip_atomic_fetch_min(A.stopj + tr.stream, tr.spec_j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) __hip_atomic_fetch_min((uint32_t*)(uintptr_t)a, uni(s.stop_j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ void trial_flusher(const SweepArgs& A, LDS TrialShared& s, LDS MWPart& mw, const Trial& tr,
@@ -1934,7 +1940,7 @@ __device__ void trial_flusher(const SweepArgs& A, LDS TrialShared& s, LDS MWPart
       st = uni(early_exit(b, A.o, tr.best_ident, full_needed));
     }
     if (lane == 0) { me.cyc_tree += c1 - c0; me.cyc_emit += clock64() - c2; }
-    if (last) spec_stop(A, tr, st, uni(b.eq_all), uni(b.clen), lane);
+    if (last) spec_stop(s, A, tr.best_ident, st, uni(b.eq_all), uni(b.clen), lane);
     if (st != ~0u) {
       if (lane == 0) ctl.state = st;
       st_rel(ctl.stop, 1u, lane);
@@ -1961,7 +1967,6 @@ struct TrialRun {
   LDS BitOut& b;
   const uint32_t t;
   const Trial tr;
-  uint64_t best;   // the "cannot beat" bound: tr.best_ident, raised by the round's earlier trials (SweepArgs::rbest)
   const StreamDev sd;
   const uint8_t* const in;
   // hash buckets of (stream, memLevel): sidx[npad] then bpos[npad]
@@ -1998,7 +2003,7 @@ struct TrialRun {
 
   __device__ __forceinline__ TrialRun(const SweepArgs& A_, SH& shm_, int lane_)
       : A(A_), shm(shm_), lane(lane_), wave(MW ? (int)(threadIdx.x >> 6) : 0), s(*(LDS TrialShared*)&shm_.t),
-        stg((LDS uint32_t*)shm_.ring), b(s.b), t(blockIdx.x), tr(A_.trials[t]), best(tr.best_ident), sd(A_.streams[tr.stream]),
+        stg((LDS uint32_t*)shm_.ring), b(s.b), t(blockIdx.x), tr(A_.trials[t]), sd(A_.streams[tr.stream]),
         in(A_.infl + sd.infl_off), npad((uint32_t)((sd.infl_len + 63) & ~63ull)),
         sidx(KIND == 0 ? nullptr : A_.chains + tr.chain_off), bpos(KIND == 0 ? nullptr : sidx + npad),
         full_needed(tr.mode & 1), lt(lane_ ? (~0ull >> (64 - lane_)) : 0ull) {
@@ -2106,24 +2111,10 @@ struct TrialRun {
       }
       return true;
   }
-  // the round's earlier trials of the stream that ended with full output: their best ident
-  __device__ __forceinline__ void refresh_best() {
-      if (!A.rbest || !tr.spec_j) return;
-      uint64_t v = (uint32_t)lane < tr.spec_j
-                       ? __hip_atomic_load(A.rbest + (uint64_t)tr.spec_a * A.rbK + (uint32_t)lane, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)
-                       : 0ull;
-      for (int d = 32; d >= 1; d >>= 1) {
-        const uint64_t o = __shfl_xor(v, d, 64);
-        v = v > o ? v : o;
-      }
-      v = uni(v);
-      if (v > best) best = v;
-  }
   __device__ __forceinline__ void FLUSH(int last) {
       hazard |= uni(flush_block(s, *(LDS TreeScratch*)shm.ring, b, (const GLOBAL uint32_t*)syms + ((saving || replay) ? sbase : 0u),
                                 (const GLOBAL uint8_t*)in, (int64_t)z.block_start, z.p, z.S, z.last_lit, z.level, z.lbs, last,
-                                A.o, best, full_needed, lane));
+                                A.o, tr.best_ident, full_needed, lane));
       sbase += z.last_lit;
       z.last_lit = 0;
       z.block_start = z.p;
@@ -2139,10 +2130,9 @@ struct TrialRun {
       if constexpr (MW) {
         return publish(0) ? ~0u : TR_DECIDED;
       } else {
-        refresh_best();
         FLUSH(0);
-        const uint32_t e = uni(early_exit(b, A.o, best, full_needed));
-        return e == ~0u && spec_stopped(A, tr) ? TR_SKIPPED : e;
+        const uint32_t e = uni(early_exit(b, A.o, tr.best_ident, full_needed));
+        return e == ~0u && spec_stopped(s) ? TR_SKIPPED : e;
       }
   }
 
@@ -2785,7 +2775,7 @@ struct TrialRun {
       else if (ad2 > A.o.sizediff_tresh) state = TR_SIZEDIFF;
       else state = TR_FULL;
     }
-    spec_stop(A, tr, state, uni(b.eq_all), uni(b.clen), lane);
+    spec_stop(s, A, tr.best_ident, state, uni(b.eq_all), uni(b.clen), lane);
   }
   if constexpr (MW) {   // no more blocks: flushers waiting past the last one stop; TR_NEED_R abandons the rest
     LDS MWCtl& ctl = (*(LDS MWPart*)&shm.mw).ctl;
@@ -2858,20 +2848,18 @@ struct TrialRun {
           mw.ctl.next_emit = 0; mw.ctl.stop = 0; mw.ctl.parse_done = 0; mw.ctl.nblocks = 0;
           mw.ctl.state = ~0u; mw.ctl.hazard = 0;
         }
-        if (spec_stopped(A, tr)) {   // decided before any flusher starts
-          state = TR_SKIPPED;
-          if (lane == 0) { mw.ctl.state = TR_SKIPPED; mw.ctl.stop = 1; }
-        }
+        spec_init(s, A, tr, lane);
+        // decided before any flusher starts: the parse stops at its first hand-over (a separate
+        // no-parse path would cost the kernel 25 VGPRs)
+        if (spec_stopped(s) && lane == 0) { mw.ctl.state = TR_SKIPPED; mw.ctl.stop = 1; }
       }
       __syncthreads();
       if (wave != 0)
         trial_flusher(A, s, mw, tr, (const GLOBAL uint32_t*)syms, (const GLOBAL uint8_t*)in, z.level, z.lbs, full_needed,
                       wave - 1, lane);
     }
-    if constexpr (!MW) if (spec_stopped(A, tr)) state = TR_SKIPPED;
-    if (wave == 0 && state == TR_SKIPPED) {
-      end_parse();
-    } else if (wave == 0) {   // the parse; every wave of a single-wave trial
+    if constexpr (!MW) spec_init(s, A, tr, lane);   // (checked at each block flush: FLUSH0)
+    if (wave == 0) {   // the parse; every wave of a single-wave trial
       parse_setup();
       if constexpr (KIND == 0) parse_stored();
       else if (replay) parse_replay();

@@ -22,8 +22,6 @@ the ATZ1 bytes must equal the oracle's (the reference's algorithm, oracle/) for 
                cannot replay are launched before it)
   ATZ_STAGE    0: uploads straight from pageable memory (default: through a pinned staging buffer)
   ATZ_STOPFLAG 0: speculative trials run to their own end (default: a stream's stop ends its later trials)
-  ATZ_RBEST    0: a speculative trial's "cannot beat" bound stays its round-start ident (default: raised by
-               the idents of its stream's earlier trials of the round)
 """
 import hashlib
 import os
@@ -44,8 +42,7 @@ SETTINGS = [{"ATZ_REPLAY": "0"}, {"ATZ_REPLAY": "2"}, {"ATZ_REPLAY": "3"}, {"ATZ
             {"ATZ_MHINT": "1"}, {"ATZ_MHINT": "0"}, {"ATZ_PREFIX_MIN": "3072", "ATZ_MHINT": "1"},
             {"ATZ_ELIG": "0"}, {"ATZ_ELIG": "0", "ATZ_REPLAY": "0"},
             {"ATZ_DFIRST": "0"}, {"ATZ_EARLY": "0"}, {"ATZ_STAGE": "0"},
-            {"ATZ_EARLY": "0", "ATZ_STAGE": "0"}, {"ATZ_STOPFLAG": "0"}, {"ATZ_RBEST": "0"},
-            {"ATZ_RBEST": "0", "ATZ_STOPFLAG": "0"}, {"ATZ_TARGET": "16384"},
+            {"ATZ_EARLY": "0", "ATZ_STAGE": "0"}, {"ATZ_STOPFLAG": "0"}, {"ATZ_TARGET": "16384"},
             {"ATZ_PIPES": "6", "GPU_MAX_HW_QUEUES": "8", "ATZ_TARGET": "65536"}]
 
 RUN = r"""
