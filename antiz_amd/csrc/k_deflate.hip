@@ -2873,6 +2873,21 @@ struct TrialRun {
 
 template <int KIND, typename SH>
 __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
+  if constexpr (!HasMW<SH>::value) {
+    // a single-wave trial whose stream an earlier trial of the round has stopped ends before any set-up
+    // (kept out of TrialRun: a path there costs the parse registers; multi-wave ones decide on wave 0)
+    const Trial& tr = A.trials[blockIdx.x];
+    const uint32_t j = uni(tr.spec_j);
+    if (A.stopj && j &&
+        uni(__hip_atomic_load(A.stopj + uni(tr.stream), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < j) {
+      if (lane == 0) {
+        TrialRes r = {};
+        r.state = TR_SKIPPED;
+        A.res[blockIdx.x] = r;
+      }
+      return;
+    }
+  }
   TrialRun<KIND, SH> run(A, shm, lane);
   run.run();
 }
