@@ -1759,9 +1759,9 @@ static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
   return 0;
 }
 
-// Trials with small blocks (memLevel <= 2: lit_bufsize <= 256 symbols) run on the multi-wave kernels
-// (C4, same box, 2 runs each: 1302-1363 vs 1250-1264 MB/s without; the 12 500-stream file 574-593 vs
-// 484-498)
+// Trials with small blocks (memLevel <= 2: lit_bufsize <= 256 symbols; <= 4 in small rounds, below) run
+// on the multi-wave kernels (round 3, C4, same box, 2 runs each: 1302-1363 vs 1250-1264 MB/s without;
+// the 12 500-stream file 574-593 vs 484-498)
 // (k_trial_{fast,slow}_mw: one parse wave, MW_F flusher waves; k_deflate.hip MWSlot).  Their symbols
 // stay in HBM for the whole stream (the flushers read each block at its own offset).
 // Multi-wave trials up to memLevel Pipe::mw_cap: 2, or 4 for a round of a sweep with at most 16 000

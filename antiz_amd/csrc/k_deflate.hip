@@ -928,7 +928,7 @@ static_assert(sizeof(TreeScratch) <= RING_SLOW * sizeof(uint64_t), "tree scratch
 static_assert(offsetof(BitOut, cyc_scan) == offsetof(BitOut, cyc_heap) + 8, "block_trees' cyc[0], cyc[1]");
 static_assert(STAGE_WORDS * 4 <= RING_SLOW * sizeof(uint64_t), "emission staging overlays the ring");
 
-// Multi-wave trials (small blocks: memLevel <= MW_MAX_MEMLEVEL, host side).  A block of lit_bufsize
+// Multi-wave trials (small blocks: memLevel <= Pipe::mw_cap, host side).  A block of lit_bufsize
 // = 2^(memLevel + 6) symbols is flushed every ~128-256 positions, and the flush -- three Huffman trees
 // with zlib's serial heap, then the block's bits -- costs more than parsing it, so such a trial is
 // bound by its flushes (a stream's 90 block trees at memLevel 1 took most of a tail round).  Wave 0
