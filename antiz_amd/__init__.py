@@ -60,7 +60,11 @@ _lib = None
 
 
 class AtzError(RuntimeError):
-    pass
+    """A libatz_accel call failed; `code` is its negative ATZ_E_* value (include/atz_accel.h), 0 if none."""
+
+    def __init__(self, msg, code=0):
+        super().__init__(msg)
+        self.code = code
 
 
 def lib():
@@ -108,7 +112,7 @@ def lib():
 
 def _check(rc):
     if rc != 0:
-        raise AtzError("atz error %d: %s" % (rc, lib().atz_strerror(rc).decode()))
+        raise AtzError("atz error %d: %s" % (rc, lib().atz_strerror(rc).decode()), rc)
 
 
 class Context:

@@ -2456,7 +2456,8 @@ struct Round {
       StreamState& st = ss[tr[sv[0]][sv[1]].stream];
       const uint16_t bit = (uint16_t)(1u << (sv[3] + 1));
       st.rp_busy &= (uint16_t)~bit;
-      if (r.state != TR_NEED_R && (r.saved_flags & 1u)) {
+      // a skipped trial never reached its stream's walk: its sequence is not relied on even if complete
+      if (r.state != TR_NEED_R && r.state != TR_SKIPPED && (r.saved_flags & 1u)) {
         e.state = 2; e.nsym = r.saved_syms; e.flags = r.saved_flags; e.reads_max = r.reads_max;
         st.rp_saved |= bit;
       } else {

@@ -2753,8 +2753,10 @@ struct TrialRun {
   // hand-over
   __device__ __forceinline__ void end_parse() {
   if (MW && state == ~0u) {
-    saved_flags |= 1;   // every symbol tallied: a saving trial's sequence is complete
-    if (!publish(1)) state = TR_DECIDED;   // the final gates run on the last block's flusher
+    // the final gates run on the last block's flusher; a refused hand-over (the trial was decided or
+    // skipped first) leaves the last block's symbols out of sbase, so the sequence is not complete
+    if (publish(1)) saved_flags |= 1;   // every symbol tallied: a saving trial's sequence is complete
+    else state = TR_DECIDED;
   } else if (state == ~0u) {
     saved_flags |= 1;   // every symbol tallied: a saving trial's sequence is complete
     FLUSH(1);

@@ -192,7 +192,37 @@ def gen_c4c3(seed=4, n_streams=100000, c3_bytes=100 * 1000 * 1000, workers=None)
     return gen_c4(seed, n_streams, workers=workers) + gen_c3(seed=3, total=c3_bytes, workers=workers)
 
 
-CONFIGS = {"c1": gen_c1, "c2": gen_c2, "c3": gen_c3, "c4": gen_c4, "c5": gen_c5, "c4c3": gen_c4c3}
+def _relevel(s, flevel):
+    """The same zlib stream with its header's FLEVEL field set to `flevel` (FCHECK recomputed): it still
+    inflates, but no trial can reproduce its second byte, so its best ident is at most C - 1."""
+    cmf = s[0]
+    flg = (flevel << 6) | (s[1] & 0x20)
+    flg |= (31 - (cmf * 256 + flg) % 31) % 31
+    return s[:1] + bytes([flg]) + s[2:]
+
+
+def gen_near(seed=71, n_streams=600):
+    """Small streams (mostly one deflate block) at c U{1..9}, m U{1..9}, w U{10..15}; half of them with
+    their header's FLEVEL moved to another class, so their best trial misses the original by exactly one
+    byte (ident = C - 1).  The mismatch-tolerance stop (main.cpp:700) and the brute-window phase
+    (main.cpp:590) then decide them: the threshold-grid fixtures (tests/golden/threshold_grid.json)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n_streams):
+        c = int(rng.integers(1, 10))
+        m = int(rng.integers(1, 10))
+        w = int(rng.integers(10, 16))
+        s = zstream(text(rng, int(rng.integers(300, 4097))), c, w, m)
+        if rng.random() < 0.5:
+            fl = (s[1] >> 6) & 3
+            s = _relevel(s, (fl + 1 + int(rng.integers(0, 3))) % 4)
+        out.append(rng.integers(0, 256, size=int(rng.integers(0, 33)), dtype=np.uint8).tobytes())
+        out.append(s)
+    return b"".join(out)
+
+
+CONFIGS = {"c1": gen_c1, "c2": gen_c2, "c3": gen_c3, "c4": gen_c4, "c5": gen_c5, "c4c3": gen_c4c3,
+           "near": gen_near}
 
 
 def cached(name, cache_dir, **kw):

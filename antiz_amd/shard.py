@@ -8,6 +8,9 @@ over the C ABI's atz_shard_* calls (include/atz_accel.h).  The data path has two
   2. gather of the ATZ1 pieces (descriptors + inflated payloads of each rank's recompressed streams,
      main.cpp:805-831) to rank 0, one point-to-point transfer per rank, received in place at its
      offset in rank 0's output buffer; rank 0 then writes the header and the residue (main.cpp:764-801).
+Failures follow the reference's abort (main.cpp:450-452, 663-665) on every rank: each library step is
+followed by an all-gather of the ranks' status codes before the next data collective, so a rank whose
+step raised makes every rank raise the same AtzError instead of leaving its peers blocked in a collective.
 The ATZ1 bytes equal the one-GPU result.  precompress_sharded keeps the ATZ1 in rank 0's HBM (the
 metric's device-resident output); precompress_sharded_to_file is the host path (the CLI's output file):
 each rank copies its own piece device -> host into the file at its offset (payloads go to
@@ -17,6 +20,8 @@ import os
 
 import torch
 import torch.distributed as dist
+
+from . import AtzError
 
 HEADER = 28   # "ATZ\x01" + file length + original length + stream count (main.cpp:770-776)
 
@@ -52,6 +57,36 @@ def allgather_ints(vals, group=None):
     return [[int(x) for x in u.cpu().tolist()] for u in ts]
 
 
+def _status(err):
+    """A rank's status for the exchange: 0 ok, -ATZ_E_* for a library error, 1000 for anything else."""
+    if err is None:
+        return 0
+    code = getattr(err, "code", 0)
+    return -code if code < 0 else 1000
+
+
+def agree(step, fn, group=None):
+    """Run this rank's part of `step` (fn()), then exchange every rank's status (one small all-gather)
+    before any data collective: if any rank failed, every rank raises AtzError naming the failed ranks
+    and their codes (main.cpp:450-452 aborts the process; here the whole job stops, no rank is left
+    waiting in a collective for a peer that is gone)."""
+    err, val = None, None
+    try:
+        val = fn()
+    except Exception as e:   # noqa: BLE001 -- any failure must reach the other ranks before we raise
+        err = e
+    codes = [c[0] for c in allgather_ints([_status(err)], group)]
+    bad = [(q, c) for q, c in enumerate(codes) if c]
+    if bad:
+        msg = "%s failed on rank(s) %s" % (step, ", ".join("%d (%s)" % (q, "atz error %d" % -c if c != 1000 else "exception")
+                                                           for q, c in bad))
+        code = -bad[0][1] if bad[0][1] != 1000 else 0
+        if err is not None:
+            raise AtzError("%s: %s" % (msg, err), getattr(err, "code", 0)) from err
+        raise AtzError(msg, code)
+    return val
+
+
 def gather_pieces(ctx, piece_lens, out, out_device="cuda", group=None):
     """Rank r's piece lands at out[HEADER + sum(piece_lens[:r])] on rank 0 (out: rank 0's output buffer;
     pieces are staged through the host when the backend is gloo).  Zero-length pieces are not sent."""
@@ -60,9 +95,17 @@ def gather_pieces(ctx, piece_lens, out, out_device="cuda", group=None):
     offs = [HEADER]
     for L in piece_lens[:-1]:
         offs.append(offs[-1] + L)
-    if rank == 0:
-        if piece_lens[0]:
+    piece = None
+
+    def local():
+        nonlocal piece
+        if rank == 0 and piece_lens[0]:
             ctx.shard_piece(out.data_ptr() + offs[0])
+        elif rank != 0 and piece_lens[rank]:
+            piece = torch.empty(piece_lens[rank], dtype=torch.uint8, device=out_device)
+            ctx.shard_piece(piece.data_ptr())
+    agree("shard_piece", local, group)
+    if rank == 0:
         ops, stage = [], []
         for q in range(1, world):
             if not piece_lens[q]:
@@ -78,8 +121,6 @@ def gather_pieces(ctx, piece_lens, out, out_device="cuda", group=None):
         for q, buf in stage:
             out[offs[q]:offs[q] + piece_lens[q]].copy_(buf)
     elif piece_lens[rank]:
-        piece = torch.empty(piece_lens[rank], dtype=torch.uint8, device=out_device)
-        ctx.shard_piece(piece.data_ptr())
         if piece.device != dev:
             piece = piece.to(dev)
         for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, piece, 0, group=group)]):
@@ -89,9 +130,9 @@ def gather_pieces(ctx, piece_lens, out, out_device="cuda", group=None):
 def _scan_and_sweep(ctx, d_file, data, group):
     """Exchange 1 and the sweep of this rank's share: (piece_lens, all recomp flags, recompressed total, stats)."""
     dptr = d_file.data_ptr()
-    blob = ctx.shard_scan(dptr, data, dist.get_rank(group), dist.get_world_size(group))
+    blob = agree("shard_scan", lambda: ctx.shard_scan(dptr, data, dist.get_rank(group), dist.get_world_size(group)), group)
     blobs = allgather_bytes(blob, group)
-    piece_len, flags, n_recomp, st = ctx.shard_sweep(dptr, data, blobs)
+    piece_len, flags, n_recomp, st = agree("shard_sweep", lambda: ctx.shard_sweep(dptr, data, blobs), group)
     meta = allgather_ints([piece_len, n_recomp, len(flags)], group)
     return [m[0] for m in meta], b"".join(allgather_bytes(flags, group)), sum(m[1] for m in meta), st
 
@@ -105,12 +146,17 @@ def precompress_sharded_to_file(ctx, d_file, data, path, group=None, device="cud
     rank = dist.get_rank(group)
     piece_lens, flags, n_recomp, st = _scan_and_sweep(ctx, d_file, data, group)
     pieces = sum(piece_lens)
-    if rank == 0:
-        with open(path, "wb"):
-            pass
-    dist.barrier(group)
-    off = HEADER + sum(piece_lens[:rank])
-    if piece_lens[rank]:
+
+    def create():
+        if rank == 0:
+            with open(path, "wb"):
+                pass
+    agree("creating " + path, create, group)   # (also the barrier: the file exists before any rank opens it)
+
+    def write_piece():
+        if not piece_lens[rank]:
+            return
+        off = HEADER + sum(piece_lens[:rank])
         piece = torch.empty(piece_lens[rank], dtype=torch.uint8, device=device)
         ctx.shard_piece(piece.data_ptr())
         host = torch.empty(piece_lens[rank], dtype=torch.uint8, pin_memory=device != "cpu")
@@ -123,10 +169,16 @@ def precompress_sharded_to_file(ctx, d_file, data, path, group=None, device="cud
                 done += os.pwrite(fd, mv[done:], off + done)
         finally:
             os.close(fd)
-    n = 0
-    if rank == 0:
+    agree("writing the pieces", write_piece, group)
+
+    def assemble():
+        if rank != 0:
+            return 0
+        # atz_shard_assemble writes the header at 0 and the residue at 28 + pieces of one buffer, so the
+        # buffer spans the pieces too (never written here): rank 0's device peak holds 28 + pieces +
+        # the residue (at most the file) + 4 KiB, e.g. ~2.8 GB for C4 + C3, freed before returning
         cap = HEADER + pieces + len(data) + 4096
-        out = torch.empty(cap, dtype=torch.uint8, device=device)   # only the header and the residue are written
+        out = torch.empty(cap, dtype=torch.uint8, device=device)
         n = ctx.shard_assemble(d_file.data_ptr(), len(data), flags, n_recomp, pieces, out.data_ptr(), cap)
         head = out[:HEADER].cpu().numpy().tobytes()
         tail = out[HEADER + pieces:n].cpu().numpy().tobytes()
@@ -140,6 +192,8 @@ def precompress_sharded_to_file(ctx, d_file, data, path, group=None, device="cud
             os.ftruncate(fd, n)
         finally:
             os.close(fd)
+        return n
+    n = agree("shard_assemble", assemble, group)
     n = allgather_ints([n], group)[0][0]
     return n, st
 
@@ -151,12 +205,11 @@ def precompress_sharded(ctx, d_file, data, group=None, out_device="cuda"):
     rank = dist.get_rank(group)
     dptr = d_file.data_ptr()
     piece_lens, flags, n_recomp, st = _scan_and_sweep(ctx, d_file, data, group)
-    out = None
-    if rank == 0:
-        cap = HEADER + sum(piece_lens) + len(data) + 4096   # the residue is at most the whole file
-        out = torch.empty(cap, dtype=torch.uint8, device=out_device)
+    cap = HEADER + sum(piece_lens) + len(data) + 4096   # the residue is at most the whole file
+    out = agree("output buffer", lambda: torch.empty(cap, dtype=torch.uint8, device=out_device) if rank == 0 else None,
+                group)
     gather_pieces(ctx, piece_lens, out, out_device, group)
     if rank != 0:
         return None, 0, st
-    n = ctx.shard_assemble(dptr, len(data), flags, n_recomp, sum(piece_lens), out.data_ptr(), out.numel())
+    n = ctx.shard_assemble(dptr, len(data), flags, n_recomp, sum(piece_lens), out.data_ptr(), out.numel())   # no collective follows
     return out, n, st

@@ -63,7 +63,13 @@ def cpu_baseline(n_streams, seed, ctx, workload="c4"):
     ref = os.path.join(ROOT, "oracle", "_ref", "uncomp")
     if not os.path.exists(ref):
         return None
-    data = datagen.CONFIGS[workload](seed=seed, n_streams=n_streams)
+    if workload == "c2":     # the whole config: the reference takes ~3 s on it
+        data, what = datagen.gen_c2(), "the whole C2 config"
+    elif workload == "c3":   # a 10 MB prefix config of the same mix (the reference: ~1 MB/s here)
+        data, what = datagen.gen_c3(seed=seed, total=10 * 1000 * 1000), "a 10 MB config of the same C3 mix"
+    else:
+        data = datagen.CONFIGS[workload](seed=seed, n_streams=n_streams)
+        what = "%d-stream prefix config of the same generator" % n_streams
     d = tempfile.mkdtemp(prefix="atzcpu")
     p = os.path.join(d, "sample.bin")
     with open(p, "wb") as f:
@@ -94,8 +100,8 @@ def cpu_baseline(n_streams, seed, ctx, workload="c4"):
     return {"value": round(len(data) / 1e6 / dt, 4), "unit": "MB/s", "cores": 1, "kind": "reference",
             "cpu_model": model, "host_cpus_visible": visible,
             "atz_identical_to_reference": same, "atz_sha256": ref_sha[:16],
-            "sample": "%d-stream prefix config of the same generator (%.1f MB, seed %d), oracle/_ref/uncomp --notest, "
-                      "%.1f s wall" % (n_streams, len(data) / 1e6, seed, dt)
+            "sample": "%s (%.1f MB, seed %d), oracle/_ref/uncomp --notest, "
+                      "%.1f s wall" % (what, len(data) / 1e6, seed, dt)
                       + (" --brute-window" if workload == "c5" else "")}
 
 
@@ -203,9 +209,11 @@ def main():
     ap.add_argument("--no-recon", action="store_true", help="skip the reconstruct (-r / verify) measurement")
     ap.add_argument("--no-h2h", action="store_true", help="skip the host-to-host (atz_precompress) measurement")
     ap.add_argument("--cache", default=os.environ.get("ATZ_BENCH_CACHE", "/tmp/atz_bench_cache"))
-    ap.add_argument("--workload", choices=("c4", "c5", "c4c3"), default="c4",
+    ap.add_argument("--workload", choices=("c4", "c5", "c4c3", "c2", "c3"), default="c4",
                     help="c4: the metric's workload (BASELINE configs[3]); c5: configs[4], the same generator with "
                          "windowBits U10-15 and --brute-window (a measurement beside the metric, not its value); "
+                         "c2 / c3: configs[1] / configs[2] at their full size (10 000 x 4 KB level-6 streams; the 100 MB "
+                         "PDF/PNG/JAR mix), measurements beside the metric (--streams is ignored); "
                          "c4c3: C4 followed by a 100 MB C3 cluster, for the split's rank balance at N > 1")
     ap.add_argument("--files-per-gpu", type=int, default=1,
                     help="independent files in flight per GPU (one context and host thread each; shards mode). "
@@ -244,13 +252,15 @@ def main():
     import antiz_amd
     from antiz_amd import datagen
 
-    base = 5 if args.workload == "c5" else 4
+    base = {"c5": 5, "c2": 2, "c3": 3}.get(args.workload, 4)
     seed = base + rank if args.mode == "shards" else base
+    fixed = args.workload in ("c2", "c3")   # BASELINE's fixed-size configs: the generator's own defaults
+    gen = {"seed": seed} if fixed else {"seed": seed, "n_streams": args.streams}
     nf = max(1, args.files_per_gpu) if args.mode == "shards" else 1
     t0 = time.time()
     if args.mode == "file" and world > 1 and rank != 0:
         dist.barrier()   # rank 0 generates the one shared file first (same seed, same cache path)
-    path = datagen.cached(args.workload, args.cache, seed=seed, n_streams=args.streams)
+    path = datagen.cached(args.workload, args.cache, **({} if fixed and seed == base else gen))
     if args.mode == "file" and world > 1 and rank == 0:
         dist.barrier()
     with open(path, "rb") as f:
@@ -267,7 +277,7 @@ def main():
     # context, precompressed by their own host threads beside the first (ctypes drops the GIL)
     extra = []
     for k in range(1, nf):
-        p2 = datagen.cached(args.workload, args.cache, seed=base + world * k + rank, n_streams=args.streams)
+        p2 = datagen.cached(args.workload, args.cache, **dict(gen, seed=base + world * k + rank))
         with open(p2, "rb") as f:
             d2 = f.read()
         h2 = torch.frombuffer(bytearray(d2) + bytearray(4096), dtype=torch.uint8)
@@ -354,7 +364,7 @@ def main():
         gold = os.path.join(ROOT, "tests", "golden")
         sp = os.path.join(gold, "share_configs.json")
         ref = (json.load(open(sp)) if os.path.exists(sp) else {}).get("%s:%d" % (args.workload, args.streams))
-        if ref is None and args.streams == 100000:
+        if ref is None and (args.streams == 100000 or fixed):
             ref = json.load(open(os.path.join(gold, "full_configs.json"))).get(args.workload)
         if ref and len(data) == ref["input_bytes"]:
             h = torch.empty(n, dtype=torch.uint8)
@@ -446,9 +456,12 @@ def main():
 
     if rank == 0:
         wl = {"c4": "C4: %d zlib streams (clevel U1-9, memLevel U1-9, w15)",
+              "c2": "C2: 10 000 zlib streams (level 6, 4 KB of text each)",
+              "c3": "C3: 100 MB PDF-like / PNG-like Z_FILTERED / JAR-like mix",
               "c5": "C5: %d zlib streams (clevel U1-9, memLevel U1-9, windowBits U10-15), --brute-window",
               "c4c3": "C4 (%d zlib streams) followed by a 100 MB C3 cluster (PDF-like, PNG-like Z_FILTERED, "
-                      "JAR-like)"}[args.workload] % args.streams
+                      "JAR-like)"}[args.workload]
+        wl = wl if fixed else wl % args.streams
         out = {
             "metric": "input MB/s precompressed (1 GB synthetic, 100k streams) at 1/2/4/8 MI355X",
             "value": round(value, 3),

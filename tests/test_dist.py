@@ -161,3 +161,83 @@ def test_precompress_sharded_to_file(world, tmp_path):
     assert res[0][0] == want
     for r in range(world):
         assert res[r][1] == len(want) and res[r][2] == {"rank": r} and res[r][3] == ["scan", "sweep"]
+
+
+# ---- a rank that fails stops every rank (main.cpp:450-452, 663-665 abort the process) ----
+class FailingShardCtx(FakeShardCtx):
+    """FakeShardCtx whose `fail_at` call raises AtzError on `fail_rank` (as a library error would; rank 1
+    has an empty piece, so its shard_piece is never called)."""
+
+    def __init__(self, rank, world, fail_at, fail_rank=1):
+        super().__init__(rank, world)
+        self.fail_at, self.fail_rank = fail_at, fail_rank
+
+    def _maybe_fail(self, what):
+        if what == self.fail_at and self.rank == self.fail_rank:
+            from antiz_amd import AtzError
+            raise AtzError("atz error -7: injected %s failure" % what, -7)
+
+    def shard_scan(self, *a):
+        self._maybe_fail("scan")
+        return super().shard_scan(*a)
+
+    def shard_sweep(self, *a):
+        self._maybe_fail("sweep")
+        return super().shard_sweep(*a)
+
+    def shard_piece(self, dst):
+        self._maybe_fail("piece")
+        return super().shard_piece(dst)
+
+    def shard_assemble(self, *a):
+        self._maybe_fail("assemble")
+        return super().shard_assemble(*a)
+
+
+def _failing_worker(rank, world, port, q, fail_at, fail_rank, path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from antiz_amd import AtzError, shard
+    fake = FailingShardCtx(rank, world, fail_at, fail_rank)
+    try:
+        if path is None:
+            shard.precompress_sharded(fake, torch.zeros(16, dtype=torch.uint8), b"x" * 11, out_device="cpu")
+        else:
+            shard.precompress_sharded_to_file(fake, torch.zeros(16, dtype=torch.uint8), b"x" * 11, path, device="cpu")
+    except AtzError as e:
+        q.put((rank, str(e), e.code))
+        q.close()
+        q.join_thread()
+        os._exit(3)   # non-zero, like the reference's abort; no collective is left pending
+    q.put((rank, None, 0))
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+@pytest.mark.parametrize("fail_at,fail_rank,host", [("scan", 1, False), ("sweep", 1, False), ("piece", 2, False),
+                                                    ("piece", 0, False), ("sweep", 2, True), ("piece", 2, True),
+                                                    ("assemble", 0, True)])
+def test_rank_failure_stops_every_rank(fail_at, fail_rank, host, tmp_path):
+    """A library error on one rank makes every rank raise the same AtzError within seconds (the status
+    all-gather before each data collective), instead of the others blocking in the next collective."""
+    import time
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    path = str(tmp_path / "out.atz") if host else None
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, q, fail_at, fail_rank, path)) for r in range(world)]
+    t0 = time.time()
+    for p in procs:
+        p.start()
+    res = {r: (msg, code) for r, msg, code in (q.get(timeout=60) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 3, "every rank exits non-zero"
+    assert time.time() - t0 < 60
+    for r in range(world):
+        msg, code = res[r]
+        assert msg is not None and "failed on rank(s) %d" % fail_rank in msg, msg
+        assert code == -7

@@ -124,3 +124,21 @@ def test_inflate_edge_fixtures_pinned():
     for c in cases:
         got = _libs.ora_inflate(bytes.fromhex(c["hex"]))
         assert got == (c["status"], c["consumed"], c["produced"]), c["family"]
+
+
+def test_threshold_grid_near_pins_the_oracle():
+    """The oracle's rule (main.cpp:454, 590, 671, 685-700) under non-default thresholds equals the real
+    reference's ATZ1 on the `near` input (tests/golden/threshold_grid.json, tools/make_threshold_grid.py)."""
+    from antiz_amd import datagen
+    grid = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "threshold_grid.json")))
+    data = datagen.gen_near(seed=71, n_streams=600)
+    for e in (e for e in grid.values() if e["workload"] == "near"):
+        assert sha(data) == e["input_sha256"]
+        f = e["flags"]
+        kw = {"brute": int("--brute-window" in f)}
+        for name, key in (("--mismatch-tol", "tol"), ("--recomp-tresh", "recomp"), ("--sizediff-tresh", "sizediff"),
+                          ("--shortcut-len", "shortcut")):
+            if name in f:
+                kw[key] = int(f[f.index(name) + 1])
+        rc, atz, _ = _libs.ora_precompress(data, **kw)
+        assert rc == 0 and sha(atz) == e["atz_sha256"], f

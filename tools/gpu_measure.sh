@@ -3,7 +3,7 @@
 # step, and separate PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic.  Every GPU step has its
 # own time limit; the chain stops at the first failure.
 # usage: tools/gpu_measure.sh <tag> [stages...]
-#   stages: test bench prof pmc timing small shardtest file2 file4 (default: test bench prof pmc)
+#   stages: test bench prof pmc timing small shardtest file2 file4 grid knobs c2 c3 c5 (default: test bench prof pmc)
 #   timing: ATZ_TIMING=2 timeline of one C4 step; small: the same on a 12 500-stream file (one rank's
 #   share of C4 at 8 GPUs); shardtest: the one-file multi-rank tests only; fileN: bench.py --gpus N on one
 #   1 GB file with N ranks sharing the box's GPU over gloo (rehearsal of the driver's RCCL run)
@@ -20,6 +20,17 @@ from antiz_amd import datagen; print(datagen.cached('c4','/tmp/atz_bench_cache',
 if has test; then
   timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/test.log 2>&1 || exit 2
 fi
+if has grid; then
+  timeout -k 10 900 python3 -u -m pytest tests/test_gpu_grid.py -m gpu -x -v --timeout 400 --timeout-method thread > $O/grid.log 2>&1 || exit 11
+fi
+if has knobs; then
+  timeout -k 10 900 python3 -u -m pytest tests/test_gpu_knobs.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/knobs.log 2>&1 || exit 12
+fi
+for W in c2 c3 c5; do
+  if has $W; then
+    timeout -k 10 600 python3 bench.py --workload $W > $O/$W.json 2> $O/$W.err || exit 13
+  fi
+done
 if has bench; then
   timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || exit 3
 fi
