@@ -1702,16 +1702,41 @@ static uint64_t c_cfg_host(uint32_t level) {   // max_chain of a level (Z/deflat
   static const uint16_t chain[10] = {0, 4, 8, 32, 16, 32, 128, 256, 1024, 4096};
   return chain[level < 10 ? level : 9];
 }
-// Jobs whose walks touch at most 32 KiB of their stream run on k_match_lds (stream bytes and the
-// 16-bit prev[] chain staged in LDS: 3 bytes per staged position), one launch per size class so the
-// dynamic LDS -- and with it the blocks per CU -- fits the class; longer ones walk in HBM (k_match).
-static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj0) {
-  if (mj0.empty()) return 0;
-  static const uint64_t cls[] = {4096, 8192, 12288, 16384, 24576, 32768};
-  constexpr int NC = 6;
+// Every job runs on k_match_lds: the block stages the window its walks can touch (the stream bytes
+// [p0 - MAX_DIST, p1 + 282) and their 16-bit prev[] chain: 3 bytes per staged position), one launch per
+// size class so the dynamic LDS -- and with it the blocks per CU -- fits the class.  A job whose window
+// exceeds the largest class (streams past 48 KiB: C3's PNG-like streams) is cut into position ranges of
+// at most match_win() positions, each with its own window (<= 16320 + 282 + 32506 + 3 <= 49152 bytes).
+// ATZ_MATCH_WIN=0 sends such jobs to k_match instead, which walks the buckets in HBM (the round-5 path).
+static uint64_t match_win() {
+  static const uint64_t v = [] { const char* e = std::getenv("ATZ_MATCH_WIN"); return e ? (uint64_t)std::atoll(e) : 16320ull; }();
+  return v;
+}
+static uint64_t match_span(const MatchJob& m) {   // bytes k_match_lds stages for the job
+  const uint64_t md = (1ull << m.window) - 262;
+  const uint64_t lo = m.p0 > md ? (m.p0 - md) & ~3ull : 0ull;
+  return std::min<uint64_t>(m.p1 + 258 + 24, m.n) - lo;
+}
+static int launch_match(atz_ctx* x, Pipe* c, const std::vector<MatchJob>& mj_in) {
+  if (mj_in.empty()) return 0;
+  static const uint64_t cls[] = {4096, 8192, 12288, 16384, 24576, 32768, 40960, 49152};
+  constexpr int NC = 8;
+  std::vector<MatchJob> cut;
+  const bool win = match_win() > 0;
+  if (win)
+    for (const MatchJob& m : mj_in) {
+      if (match_span(m) <= cls[NC - 1]) { cut.push_back(m); continue; }
+      for (uint64_t a = m.p0; a < m.p1; a += std::min<uint64_t>(match_win(), 16320)) {
+        MatchJob h = m;
+        h.p0 = a;
+        h.p1 = std::min<uint64_t>(m.p1, a + std::min<uint64_t>(match_win(), 16320));
+        cut.push_back(h);
+      }
+    }
+  const std::vector<MatchJob>& mj0 = win ? cut : mj_in;
   auto class_of = [&](const MatchJob& m) -> int {
-    const uint64_t b = std::min<uint64_t>(m.p1 + 258 + 24, m.n);
-    for (int k = 0; k < NC; k++) if (b <= cls[k]) return k;
+    const uint64_t b = match_span(m);
+    for (int k = 0; k < NC; k++) if (b <= cls[k] && (win || k < 6)) return k;
     return NC;
   };
   // one launch per class; within a launch the longest walks go first (LPT)

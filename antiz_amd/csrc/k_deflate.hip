@@ -731,15 +731,25 @@ __global__ __launch_bounds__(256) void k_match(const uint8_t* __restrict__ infl,
 }
 
 // k_match_lds: the same walks with everything they touch in LDS.  The block stages the stream bytes
-// the walks can read ([0, p1 + 258 + 24)) and, for every position q < p1, its predecessor in its
-// hash bucket (prev[q] = bpos[sidx[q] - 1], NIL if q opens its bucket: zlib's prev[] chain), gathered
-// from the bucket arrays with all loads in flight at once.  A walk is then a chain of LDS reads
-// instead of dependent HBM round trips.  Host-side size classes keep positions < 32 Ki (16-bit).
+// the walks can read and, for every position q the walks can visit, its predecessor in its hash bucket
+// (prev[q] = bpos[sidx[q] - 1], NIL if q opens its bucket: zlib's prev[] chain), gathered from the
+// bucket arrays with all loads in flight at once.  A walk is then a chain of LDS reads instead of
+// dependent HBM round trips.
+// Walks from the job's positions [p0, p1) visit only nodes > p - MAX_DIST >= p0 - MAX_DIST, so the
+// block stages the window [lo, p1 + 258 + 24) with lo = p0 - MAX_DIST (rounded down to a word, 0 for
+// p0 <= MAX_DIST); offsets within it are 16-bit.  A node below lo ends a walk exactly as zlib's
+// `cur_match > limit` test does, so it is staged as NIL.  The host cuts longer streams (C3's 64 KiB
+// PNG-like streams) into position ranges whose window fits one block's LDS (launch_match).
 static constexpr uint32_t PREV_NIL = 0xffffu;
 #ifndef ATZ_MATCH_THREADS
 #define ATZ_MATCH_THREADS 1024  // threads per k_match_lds block, all sharing the staged stream (C4: 256 ~913, 512 ~974, 1024 ~986 MB/s)
 #endif
 static constexpr uint32_t MATCH_THREADS = ATZ_MATCH_THREADS;
+struct LdsWin {   // the staged words of [lo, ...) addressed by absolute word index
+  const LDS uint32_t* p;
+  uint32_t off;   // lo / 4
+  __device__ __forceinline__ uint32_t operator[](uint32_t w) const { return p[w - off]; }
+};
 __global__ __launch_bounds__(MATCH_THREADS) void k_match_lds(const uint8_t* __restrict__ infl, const uint32_t* __restrict__ chains,
                                                   uint2* __restrict__ R, const MatchJob* __restrict__ jobs) {
   extern __shared__ uint32_t dyn_lds[];
@@ -749,14 +759,22 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match_lds(const uint8_t* __re
   const uint32_t n = (uint32_t)jb.n, npad = (n + 63) & ~63u;
   const uint32_t* sidx = chains + jb.chain_off;
   const uint32_t* bpos = sidx + npad;
+  const uint32_t maxdist = (1u << jb.window) - 262;
+  const uint32_t lo = (uint32_t)jb.p0 > maxdist ? ((uint32_t)jb.p0 - maxdist) & ~3u : 0u;
+  const uint32_t w0 = lo >> 2;
   const uint64_t want = jb.p1 + 258 + 24;
-  const uint32_t nw = (uint32_t)(((want < n ? want : n) + 3) >> 2);
+  const uint32_t nw = (uint32_t)(((want < n ? want : n) + 3) >> 2) - w0;   // staged words
   LDS uint32_t* l32 = (LDS uint32_t*)dyn_lds;
-  LDS uint16_t* prv = (LDS uint16_t*)(l32 + nw + 8);
-  for (uint32_t w = threadIdx.x; w < nw + 8; w += MATCH_THREADS) l32[w] = w < nw ? g32[w] : 0u;
+  LDS uint16_t* prv = (LDS uint16_t*)(l32 + nw + 8);   // prv[q - lo]
+  for (uint32_t w = threadIdx.x; w < nw + 8; w += MATCH_THREADS) l32[w] = w < nw ? g32[w0 + w] : 0u;
   const uint32_t nh = n >= 3 ? n - 2 : 0;
   const uint32_t P = (uint32_t)jb.p1 < nh ? (uint32_t)jb.p1 : nh;   // candidates and walk starts are < P
-  if (4 * P >= nh) {
+  // a bucket entry's predecessor as staged: NIL when q opens its bucket or it lies below the window
+  auto pred = [&](uint32_t a, uint32_t b) -> uint16_t {
+    const uint32_t pq = b & ~BUCKET_FIRST;
+    return ((a & BUCKET_FIRST) || pq < lo) ? (uint16_t)PREV_NIL : (uint16_t)(pq - lo);
+  };
+  if (P > lo && 4 * (P - lo) >= nh) {
     // most positions wanted: one coalesced pass over the bucket array (entry i's predecessor is
     // entry i - 1 unless i opens its bucket), scattered into LDS -- no dependent gathers
     for (uint32_t i0 = 0; i0 < nh; i0 += 8 * MATCH_THREADS) {
@@ -770,11 +788,11 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match_lds(const uint8_t* __re
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const uint32_t q = a[u] & ~BUCKET_FIRST;
-        if (q < P) prv[q] = (a[u] & BUCKET_FIRST) ? (uint16_t)PREV_NIL : (uint16_t)(b[u] & ~BUCKET_FIRST);
+        if (q >= lo && q < P) prv[q - lo] = pred(a[u], b[u]);
       }
     }
   } else {
-    for (uint32_t q0 = 0; q0 < P; q0 += 8 * MATCH_THREADS) {
+    for (uint32_t q0 = lo; q0 < P; q0 += 8 * MATCH_THREADS) {
       uint32_t ix[8], a[8], b[8];
 #pragma unroll
       for (int u = 0; u < 8; u++) { const uint32_t q = q0 + MATCH_THREADS * u + threadIdx.x; ix[u] = q < P ? sidx[q] : 1u; }
@@ -783,16 +801,15 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match_lds(const uint8_t* __re
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const uint32_t q = q0 + MATCH_THREADS * u + threadIdx.x;
-        if (q < P) prv[q] = (a[u] & BUCKET_FIRST) ? (uint16_t)PREV_NIL : (uint16_t)(b[u] & ~BUCKET_FIRST);
+        if (q < P) prv[q - lo] = pred(a[u], b[u]);
       }
     }
   }
   __syncthreads();
-  const LDS uint32_t* in32 = l32;
+  const LdsWin in32{l32, w0};
   auto byte = [&](uint32_t x) -> uint32_t { return (in32[x >> 2] >> (8 * (x & 3))) & 0xffu; };
   uint2* r = R + jb.r_off;
   const uint32_t B = c_cfg[jb.level][3], nice = c_cfg[jb.level][2], Bq = B >> 2;
-  const uint32_t maxdist = (1u << jb.window) - 262;
   const uint32_t hbits = jb.memlevel + 7u, hmask = (1u << hbits) - 1u, hshift = (hbits + 2u) / 3u;
   for (uint32_t p = (uint32_t)jb.p0 + threadIdx.x; p < (uint32_t)jb.p1; p += MATCH_THREADS) {
     uint32_t bf = 2, df = 0, bq = 2, dq = 0, valid = 0, slot = 0, budget_out = 0;
@@ -801,8 +818,9 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match_lds(const uint8_t* __re
     if (p + 3 <= n) {
       slot = (((s0 << (2 * hshift)) ^ (byte(p + 1) << hshift) ^ byte(p + 2)) & hmask) & (HOLE_SLOTS_M - 1);
       const uint32_t lim = p > maxdist ? p - maxdist : 0u;   // walk continues to q only if q > lim
-      uint32_t cur = prv[p];
-      if (cur != PREV_NIL && cur >= 1 && cur + maxdist >= p) {   // hash_head valid
+      const uint32_t h0 = prv[p - lo];
+      uint32_t cur = h0 + lo;
+      if (h0 != PREV_NIL && cur >= 1 && cur + maxdist >= p) {   // hash_head valid
         valid = 1;
         const uint32_t left = n - p;
         const uint32_t cap = left < 258 ? left : 258u;
@@ -811,8 +829,9 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match_lds(const uint8_t* __re
         load16(in32, p, pv);
         for (uint32_t i = 0;;) {
           reach = cur;
-          const uint32_t nx = prv[cur];                        // next node, read ahead of the compare
-          const bool more = nx != PREV_NIL;
+          const uint32_t nr = prv[cur - lo];                   // next node, read ahead of the compare
+          const bool more = nr != PREV_NIL;
+          const uint32_t nx = nr + lo;
           uint32_t len = match16(in32, cur, p, pv, 0);
           if (len == 16)
             while (len < cap) {

@@ -160,6 +160,36 @@ def test_deflate_random_vs_oracle(ctx):
     assert not bad, bad[:10]
 
 
+def test_long_streams_windowed_match_tables_vs_oracle(ctx):
+    """Streams past one k_match_lds block's window (> 48 KiB: C3's PNG-like streams): the host cuts their
+    match jobs into position ranges, each staging [p0 - MAX_DIST, p1 + 282) in LDS, with bucket
+    predecessors below the window staged as chain ends.  Every level, windows 9-15, text and filtered-
+    image-like data of 49-200 KB, bit-exact against the oracle."""
+    r = random.Random(4242)
+    rng = np.random.default_rng(4242)
+    from antiz_amd import datagen
+    buf = bytearray()
+    items = []
+    for k in range(120):
+        n = r.randrange(49000, 200000 if k % 6 == 0 else 90000)
+        if k % 3 == 2:   # PNG-like rows: small deltas, many zeros, long runs of short matches
+            w = r.randrange(64, 512)
+            img = np.cumsum(rng.integers(-3, 4, size=(n // (3 * w) + 1, 3 * w)), axis=1) % 256
+            d = np.diff(img, axis=1, prepend=0).astype(np.uint8).tobytes()[:n]
+        else:
+            d = datagen.text(rng, n)
+        items.append((len(buf), len(d), k % 10, 9 + (k // 10) % 7, 1 + (k * 7) % 9))
+        buf += d
+    outs = ctx.deflate_batch(bytes(buf), items)
+    bad = []
+    for it, o in zip(items, outs):
+        want, _ = _libs.ora_deflate(bytes(buf[it[0]:it[0] + it[1]]), it[2], it[3], it[4])
+        if o != want:
+            first = next((i for i in range(min(len(o), len(want))) if o[i] != want[i]), min(len(o), len(want)))
+            bad.append((it[1:], len(o), len(want), first))
+    assert not bad, bad[:10]
+
+
 def test_fast_levels_holes_vs_oracle(ctx):
     """deflate_fast (levels 1-3) on repetitive text: long matches leave many positions uninserted
     ("holes") and chains exhaust their budget, which exercises the hole-slot check, the visited-node
