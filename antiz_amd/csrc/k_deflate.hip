@@ -1891,14 +1891,14 @@ __device__ __forceinline__ bool spec_stopped(const LDS TrialShared& s) {
   const uint64_t a = uni(s.stop_at);
   const uint32_t j = uni(s.stop_j);
   if (!a || !j) return false;
-  return uni(__hip_atomic_load((const uint32_t*)(uintptr_t)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < j;
+  return uni(__hip_atomic_load((const GLOBAL uint32_t*)(uintptr_t)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < j;
 }
 __device__ __forceinline__ void spec_stop(const LDS TrialShared& s, const SweepArgs& A, uint64_t best_ident, uint32_t state,
                                           uint64_t ident, uint64_t clen, int lane) {
   const uint64_t a = uni(s.stop_at);
   if (!a || state != TR_FULL || ident <= best_ident) return;
   if (ident != clen && ident + A.o.mismatch_tol < clen) return;
-  if (lane == 0) __hip_atomic_fetch_min((uint32_t*)(uintptr_t)a, uni(s.stop_j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) __hip_atomic_fetch_min((GLOBAL uint32_t*)(uintptr_t)a, uni(s.stop_j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ void trial_flusher(const SweepArgs& A, LDS TrialShared& s, LDS MWPart& mw, const Trial& tr,
@@ -1996,7 +1996,9 @@ struct TrialRun {
   const uint64_t lt;   // lanes below this one
   Lz z;
   bool saving = false, replay = false, rec = false;
-  uint32_t* syms = nullptr;
+  // global (not generic) pointers: a flat store counts in lgkmcnt too, so every later LDS wait of the
+  // parse would also wait for the store to reach L2
+  GLOBAL uint32_t* syms = nullptr;
   GLOBAL uint64_t* rtab = nullptr;
   uint32_t sbase = 0;            // symbols in the flushed blocks
   uint32_t saved_flags = 0;
@@ -2066,7 +2068,7 @@ struct TrialRun {
       }
       replay = same;
     }
-    syms = saving || replay ? (uint32_t*)(uintptr_t)tr.rp_syms : A.syms + tr.sym_off;
+    syms = saving || replay ? (GLOBAL uint32_t*)(uintptr_t)tr.rp_syms : (GLOBAL uint32_t*)(A.syms + tr.sym_off);
     // a saving slow trial records the match-table entries its parse reads (rp_tab, cleared first)
     rec = KIND == 2 && saving && (tr.mode & 32);
     rtab = (GLOBAL uint64_t*)(uintptr_t)tr.rp_tab;
@@ -2900,7 +2902,7 @@ __device__ void trial_body(const SweepArgs& A, SH& shm, int lane) {
     const Trial& tr = A.trials[blockIdx.x];
     const uint32_t j = uni(tr.spec_j);
     if (A.stopj && j &&
-        uni(__hip_atomic_load(A.stopj + uni(tr.stream), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < j) {
+        uni(__hip_atomic_load((const GLOBAL uint32_t*)A.stopj + uni(tr.stream), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < j) {
       if (lane == 0) {
         TrialRes r = {};
         r.state = TR_SKIPPED;

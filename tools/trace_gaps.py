@@ -58,6 +58,7 @@ def main():
     trial = union(by.get("k_trial", []))
     print("any kernel running %.1f%%, a trial kernel running %.1f%%, idle %.2f ms" % (100.0 * allb / span, 100.0 * trial / span,
                                                                                     (span - allb) / 1e6))
+    timeline(step, t0, t1)
     qs = {}
     for s, e, n, q in step:
         qs.setdefault(q, []).append((s, e))
@@ -83,6 +84,24 @@ def main():
                 cnt[0 if c == "k_trial" else 1 if c == "k_match" else 2 if c.startswith("k_bucket") else 3] += 1
         out.append("%d/%d/%d/%d" % tuple(cnt))
     print(" ".join(out))
+
+
+def timeline(step, t0, t1, bin_ms=10.0):
+    """Per bin: the busy fraction of each kernel class (union of its launches within the bin)."""
+    b = int(bin_ms * 1e6)
+    classes = ("k_inflate", "k_buckets_sort", "k_match", "k_trial", "idle")
+    print("%-10s" % "ms" + "".join("%15s" % c for c in classes))
+    for a in range(t0, t1, b):
+        e = min(a + b, t1)
+        row = []
+        allv = []
+        for c in classes[:-1]:
+            iv = [(max(s, a), min(en, e)) for s, en, n, _ in step if cls(n) == c and en > a and s < e]
+            allv += iv
+            row.append(union(iv) / (e - a))
+        anyb = union([(max(s, a), min(en, e)) for s, en, n, _ in step if en > a and s < e])
+        row.append(1.0 - anyb / (e - a))
+        print("%-10.0f" % ((a - t0) / 1e6) + "".join("%14.0f%%" % (100 * v) for v in row))
 
 
 if __name__ == "__main__":
