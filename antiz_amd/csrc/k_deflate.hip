@@ -2303,92 +2303,132 @@ struct TrialRun {
     return bad;
   }
 
-  // deflate_fast's longest_match at f over the INSERTED same-hash positions (Z/deflate.c:1148-1289):
-  // 64 bucket entries per step, lanes test insertion and compare bytes in parallel; the walk order is
-  // the lane order.  ml / ms: the match (0: none).
-  __device__ __forceinline__ void fast_exact_walk(uint32_t f, uint32_t Sf, uint32_t la, uint32_t sxl, int fln,
-                                                  uint32_t& ml, uint32_t& ms) {
-    const uint32_t si = uni((uint32_t)__builtin_amdgcn_readlane((int)sxl, fln));
-    bool done = false;
-    bool head_done = false, hv = false, won = false;
-    uint32_t examined = 0, best = 2, win = 0;
-    const uint32_t limit = f > maxd ? f - maxd : 0u;   // later nodes only while > limit
+  // deflate_fast's longest_match (Z/deflate.c:1148-1289) over the INSERTED same-hash positions, for up to
+  // eight bad nodes of a window at once: node g of the batch (the g-th set bit of bm, nb nodes) walks on
+  // lanes [g*S, g*S + S), S = 64 / G, S bucket entries per step in walk order (descending bucket index);
+  // lanes test insertion and compare bytes in parallel.  Each node is walked as if the window's path
+  // stands up to it, which is how the caller uses its result (it stops at the first node whose exact
+  // step differs from the table's).  The walk order, the budget count, the first maximum and the nice
+  // stop do not depend on the chunk size, so every node's result is the single 64-lane walk's.  Lane
+  // g*S of rml / rms gets node g's match (length 0: none).  One batch replaces a chain of dependent walks
+  // (bucket chunk, then candidate bytes, one HBM round trip each) per bad node: the slowest trials of a
+  // round (fast levels at memLevel 1-3, 1 000-4 000 walks each) have several bad nodes per window.
+  __device__ __forceinline__ void fast_exact_walks(uint64_t bm, uint32_t nb, uint32_t G, uint32_t wb, uint32_t Sb,
+                                                   uint32_t sxl, uint32_t& rml, uint32_t& rms) {
+    const uint32_t lg = G == 1 ? 6u : G == 2 ? 5u : G == 4 ? 4u : 3u;   // log2 S
+    const uint32_t S = 1u << lg;
+    const uint32_t ll = (uint32_t)lane & (S - 1u), g = (uint32_t)lane >> lg, base = g << lg;
+    const uint64_t smask = S == 64 ? ~0ull : ((1ull << S) - 1ull);
+    const uint64_t ltl = ll ? (~0ull >> (64 - ll)) : 0ull;   // lanes of the segment below this one
+    auto seg = [&](bool pred) -> uint64_t { return (__ballot(pred) >> base) & smask; };
+    uint32_t fl = 0;   // this segment's node: its lane in the window
+    {
+      uint64_t m = bm;
+      for (uint32_t gi = 0; gi < nb; gi++) {
+        const uint32_t bit = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1ull;
+        fl = g == gi ? bit : fl;
+      }
+    }
+    const uint32_t f = wb + fl;
+    const uint32_t si = (uint32_t)__shfl((int)sxl, (int)fl, 64);
+    const uint32_t Sf = S_iter(Sb, f);
+    const uint32_t la = n - f < LOOKMIN ? n - f : LOOKMIN;   // lookahead (>= 258 stands for more)
+    const uint32_t limit = f > maxd ? f - maxd : 0u;          // later nodes only while > limit
     const uint32_t cap = n - f < 258u ? n - f : 258u;
-    const uint32_t nicec = z.nice < la ? z.nice : la;   // <= cap
-    // lane l reads bucket entry top - l; the first chunk starts at f's own entry (lane 0), whose
-    // first-of-bucket flag says whether f has a chain at all
+    const uint32_t nicec = z.nice < la ? z.nice : la;         // <= cap
+    // the first chunk starts at f's own entry (local lane 0), whose first-of-bucket flag says whether f
+    // has a chain at all
     int32_t top = (int32_t)si;
-    int skip = 1;
-    while (!done) {
-      const int32_t k = top - lane;
-      const uint32_t e = k >= 0 ? bpos[k] : BUCKET_FIRST;
-      if (skip && (uni((uint32_t)__builtin_amdgcn_readlane((int)e, 0)) & BUCKET_FIRST)) break;   // first of its bucket: no chain
-      const uint64_t fm = __ballot((e & BUCKET_FIRST) != 0 && lane >= skip);
-      const int flane = fm ? __ffsll((unsigned long long)fm) - 1 : 64;   // bucket's first entry: last node
+    uint32_t skip = 1;
+    bool done = g >= nb, head_done = false, hv = false, won = false, nicew = false;
+    uint32_t examined = 0, best = 2, win = 0;
+    while (__ballot(!done)) {
+      const int32_t k = top - (int32_t)ll;
+      const uint32_t e = (!done && k >= 0) ? bpos[k] : BUCKET_FIRST;
+      const uint32_t e0 = (uint32_t)__shfl((int)e, (int)base, 64);
+      if (!done && skip && (e0 & BUCKET_FIRST)) done = true;   // first of its bucket: no chain
+      const uint64_t fm = seg(!done && (e & BUCKET_FIRST) != 0 && ll >= skip);
+      const uint32_t flane = fm ? (uint32_t)__builtin_ctzll(fm) : S;   // the bucket's first entry: last node
       const uint32_t qc = e & ~BUCKET_FIRST;
-      const bool insd = lane >= skip && lane <= flane && k >= 0 && ins_get(qc);
-      const uint64_t im = __ballot(insd);
-      int head_lane = -1, from = 0;
-      if (!head_done) {
+      const bool insd = !done && ll >= skip && ll <= flane && k >= 0 && ins_get(qc);
+      const uint64_t im = seg(insd);
+      bool go = !done;
+      uint32_t from = 0, head_ll = S;   // head_ll < S: the head was found in this chunk
+      if (go && !head_done) {
         if (!im) {   // no inserted node in this chunk yet
-          if (flane < 64) break;
-          top -= 64;
-          skip = 0;
-          continue;
+          if (flane < S) done = true;
+          go = false;
+        } else {
+          head_ll = (uint32_t)__builtin_ctzll(im);
+          head_done = true;
+          from = head_ll;
         }
-        head_lane = __ffsll((unsigned long long)im) - 1;
-        const uint32_t hh = (uint32_t)__builtin_amdgcn_readlane((int)qc, head_lane);
-        head_done = true;
+      }
+      const uint32_t hh = (uint32_t)__shfl((int)qc, (int)(base + (head_ll < S ? head_ll : 0u)), 64);
+      if (go && head_ll < S) {
         hv = hh > Sf && f - hh <= maxd;   // zlib calls longest_match only then
-        if (!hv) break;
-        from = head_lane;
+        if (!hv) { done = true; go = false; }
       }
       // the walk stops at the first inserted node <= limit (the head is always examined)
-      const uint64_t sm = __ballot(insd && lane >= from && lane != head_lane && qc <= limit);
-      const int slane = sm ? __ffsll((unsigned long long)sm) - 1 : 64;
-      bool cand = insd && lane >= from && lane < slane;
-      const uint32_t room = z.chain - examined;
-      cand = cand && (uint32_t)__popcll(__ballot(cand) & lt) < room;
-      const uint64_t cm = __ballot(cand);
-      examined += (uint32_t)__popcll(cm);
-      // match lengths capped at nice (16 bytes per round trip); the first candidate reaching
-      // nice ends the walk, so capped lengths decide the winner
+      const uint64_t sm = seg(go && insd && ll >= from && ll != head_ll && qc <= limit);
+      const uint32_t slane = sm ? (uint32_t)__builtin_ctzll(sm) : S;
+      bool cand = go && insd && ll >= from && ll < slane;
+      cand = cand && (uint32_t)__popcll(seg(cand) & ltl) < z.chain - examined;
+      if (go) examined += (uint32_t)__popcll(seg(cand));
+      // match lengths capped at nice (16 bytes per round trip); the first candidate reaching nice ends
+      // the walk, so capped lengths decide the winner
       uint32_t len = 0;
-      bool go = cand;
-      while (__ballot(go)) {
-        if (go) {
-          // 16 bytes per round trip: 5 aligned dword loads per side (stream bases are 256-byte aligned)
+      bool more = cand;
+      while (__ballot(more)) {
+        if (more) {
           const uint32_t run = match16((const GLOBAL uint32_t*)in, qc + len, f + len, nullptr, 0);
           const uint32_t left = nicec - len;
           len += run < left ? run : left;
-          go = run == 16 && len < nicec;
+          more = run == 16 && len < nicec;
         }
       }
-      const uint64_t nm = __ballot(cand && len >= nicec);
-      if (nm) {
-        const int wl = __ffsll((unsigned long long)nm) - 1;
-        win = (uint32_t)__builtin_amdgcn_readlane((int)qc, wl);
-        best = uni(common_len(in, win, f, nicec, cap, lane));   // full length of the winner
-        won = true;
-        break;
-      }
+      const uint64_t nm = seg(cand && len >= nicec);
       uint32_t mx = cand ? len : 0u;
-      for (int d = 32; d >= 1; d >>= 1) { const uint32_t o2 = __shfl_xor(mx, d, 64); mx = mx > o2 ? mx : o2; }
-      mx = uni(mx);
-      if (mx > best) {
-        const uint64_t xm = __ballot(cand && len == mx);
-        win = (uint32_t)__builtin_amdgcn_readlane((int)qc, __ffsll((unsigned long long)xm) - 1);
-        best = mx;
-        won = true;
+      for (uint32_t d = S >> 1; d >= 1; d >>= 1) {
+        const uint32_t o2 = (uint32_t)__shfl_xor((int)mx, (int)d, 64);
+        mx = mx > o2 ? mx : o2;
       }
-      done = examined >= z.chain || slane < 64 || flane < 64;
-      top -= 64;
+      const uint64_t xm = seg(cand && len == mx);
+      const uint32_t pick = nm ? (uint32_t)__builtin_ctzll(nm) : xm ? (uint32_t)__builtin_ctzll(xm) : 0u;
+      const uint32_t wq = (uint32_t)__shfl((int)qc, (int)(base + pick), 64);
+      if (go) {
+        if (nm) { win = wq; won = true; nicew = true; done = true; }
+        else {
+          if (mx > best) { win = wq; best = mx; won = true; }
+          if (examined >= z.chain || slane < S || flane < S) done = true;
+        }
+      }
+      top -= (int32_t)S;
       skip = 0;
     }
-    if (hv && won) {
-      ml = best <= la ? best : la;
-      ms = win;
+    // the full length of a nice winner (its first nicec bytes match), 16 bytes per lane per step: the
+    // first lane of the segment whose run ends gives it (its end lies before every later lane's offset)
+    bool need = nicew;
+    uint32_t o = nicec + 16u * ll;
+    while (__ballot(need)) {
+      uint32_t endp = ~0u;
+      if (need) {
+        if (o >= cap) endp = cap;
+        else {
+          const uint32_t r = match16((const GLOBAL uint32_t*)in, win + o, f + o, nullptr, 0);
+          if (r < 16 || o + r >= cap) endp = o + r < cap ? o + r : cap;
+        }
+      }
+      for (uint32_t d = S >> 1; d >= 1; d >>= 1) {
+        const uint32_t o2 = (uint32_t)__shfl_xor((int)endp, (int)d, 64);
+        endp = endp < o2 ? endp : o2;
+      }
+      if (need && endp != ~0u) { best = endp; need = false; }
+      o += 16u * S;
     }
+    rml = (hv && won) ? (best <= la ? best : la) : 0u;
+    rms = win;
   }
 
   __device__ __forceinline__ void parse_fast() {
@@ -2524,6 +2564,8 @@ struct TrialRun {
     uint32_t Dx = D;      // this lane's match distance (an exact walk may replace the table's)
     bool restart = false;
     uint32_t qnext = qn;
+    uint64_t batchm = 0;           // bad nodes of the current batch of exact walks
+    uint32_t rml = 0, rms = 0, bS = 64;
     for (;;) {
       // ---- tally the committed nodes' symbols lane-parallel, in position order
       const uint64_t Pc = (badm ? P & ((1ull << __builtin_ctzll(badm)) - 1ull) : P) & ~donem;
@@ -2568,14 +2610,24 @@ struct TrialRun {
       // same-hash positions (Z/deflate.c:1148-1289): 64 bucket entries per step, lanes test
       // insertion and compare bytes in parallel; the walk order is the lane order.
       fallbacks++;
-      const uint64_t cf0 = STEP_CLOCK();
       const int fln = __builtin_ctzll(badm);
       const uint32_t f = wb + (uint32_t)fln;
       const uint32_t Sf = S_iter(Sb, f);
-      const uint32_t la = n - f < LOOKMIN ? n - f : LOOKMIN;   // lookahead (>= 258 stands for more)
-      uint32_t ml = 0, ms = 0;
-      fast_exact_walk(f, Sf, la, sxl, fln, ml, ms);
-      cyc_fb += STEP_CLOCK() - cf0;
+      if (!((batchm >> fln) & 1ull)) {   // the next batch: up to eight of the bad nodes left, from fln on
+        const uint64_t cf0 = STEP_CLOCK();
+        const uint32_t nbad = (uint32_t)__popcll(badm);
+        const uint32_t G = nbad >= 5 ? 8u : nbad >= 3 ? 4u : nbad;
+        const uint32_t nb = nbad < G ? nbad : G;
+        uint64_t m = badm;
+        batchm = 0;
+        for (uint32_t i = 0; i < nb; i++) { batchm |= m & (0ull - m); m &= m - 1ull; }
+        fast_exact_walks(batchm, nb, G, wb, Sb, sxl, rml, rms);
+        bS = 64u / G;
+        cyc_fb += STEP_CLOCK() - cf0;
+      }
+      const uint32_t gidx = (uint32_t)__popcll(batchm & ((1ull << fln) - 1ull));
+      const uint32_t ml = uni((uint32_t)__builtin_amdgcn_readlane((int)rml, (int)(gidx * bS)));
+      const uint32_t ms = uni((uint32_t)__builtin_amdgcn_readlane((int)rms, (int)(gidx * bS)));
       const uint32_t twt = uni((uint32_t)__builtin_amdgcn_readlane((int)wt, fln));
       const uint32_t tL = uni((uint32_t)__builtin_amdgcn_readlane((int)L, fln));
       if (ml >= 3 ? (twt == 2 && tL == ml) : twt == 1) {   // same step: the path stands
