@@ -2343,13 +2343,9 @@ struct TrialRun {
     uint32_t skip = 1;
     bool done = g >= nb, head_done = false, hv = false, won = false, nicew = false;
     uint32_t examined = 0, best = 2, win = 0;
-    // the bucket chunk of the next step is loaded beside this step's candidate bytes, so a step costs
-    // one HBM round trip, not two (a segment that ends this step has loaded one chunk for nothing)
-    uint32_t en = (!done && top - (int32_t)ll >= 0) ? bpos[top - (int32_t)ll] : BUCKET_FIRST;
     while (__ballot(!done)) {
       const int32_t k = top - (int32_t)ll;
-      const uint32_t e = en;
-      en = (!done && k - (int32_t)S >= 0) ? bpos[k - (int32_t)S] : BUCKET_FIRST;
+      const uint32_t e = (!done && k >= 0) ? bpos[k] : BUCKET_FIRST;
       const uint32_t e0 = (uint32_t)__shfl((int)e, (int)base, 64);
       if (!done && skip && (e0 & BUCKET_FIRST)) done = true;   // first of its bucket: no chain
       const uint64_t fm = seg(!done && (e & BUCKET_FIRST) != 0 && ll >= skip);
