@@ -966,8 +966,20 @@ struct ScanState {
   uint64_t max_records() const { return cands.size() + chunks.size() + 1; }
 };
 
+// ATZ_CAP_DIV=d (read once; tests): every device-memory cap of the library divided by d -- the scan's
+// output arena, the bucket cache, the replay arena and the round / batch scratch budgets -- so that
+// small inputs take the paths past the caps (re-inflates, per-round tables, unsaved replays, deferred
+// streams, several reconstruct batches) that only inputs of tens of GB reach otherwise.
+static uint64_t cap_bytes(uint64_t cap) {
+  static const uint64_t d = [] {
+    const char* e = std::getenv("ATZ_CAP_DIV");
+    const long long v = e ? std::atoll(e) : 1;
+    return (uint64_t)(v > 1 ? v : 1);
+  }();
+  return std::max<uint64_t>(cap / d, 4096);
+}
 static uint64_t arena_cap_for(uint64_t scanned) {
-  return std::min<uint64_t>(64ull << 30, std::max<uint64_t>(1ull << 30, 8 * scanned));
+  return cap_bytes(std::min<uint64_t>(64ull << 30, std::max<uint64_t>(1ull << 30, 8 * scanned)));
 }
 static int scan_plan(atz_ctx* c, const uint8_t* h, const uint8_t* d_file, uint64_t F, ScanState& S) {
   auto tm_ = std::chrono::steady_clock::now();
@@ -2322,7 +2334,7 @@ struct Round {
     mbeg.assign(active.size() + 1, 0);
     mine.reserve(active.size() * K);
     uint64_t round_bytes = 0;
-    const uint64_t round_budget = ROUND_BUDGET_BYTES / x->pipes_running;
+    const uint64_t round_budget = cap_bytes(ROUND_BUDGET_BYTES) / x->pipes_running;
     for (size_t a = 0; a < active.size(); a++) {
       mbeg[a] = (uint32_t)mine.size();
       const uint32_t s = active[a];
@@ -2881,8 +2893,8 @@ static int sweep_begin(atz_ctx* c, const uint8_t* d_file, std::vector<StreamStat
   ss.assign(n_max, StreamState());
   c->chain_off.assign(n_max, {});
   for (auto& a : c->chain_off) a.fill(~0ull);
-  c->chain_arena.reset(CHAIN_CACHE_CAP);
-  c->rp_arena.reset(RP_ARENA_CAP);
+  c->chain_arena.reset(cap_bytes(CHAIN_CACHE_CAP));
+  c->rp_arena.reset(cap_bytes(RP_ARENA_CAP));
   c->rp_pool.clear();
   c->rp_pool.reserve(n_max);
   if (int r = c->depth_pin.reserve(n_max * 40 + 64)) return r;
@@ -3375,7 +3387,7 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
   Pipe* p = c->pipes[0].get();
   p->mw_cap = mw_cap_for(~(size_t)0);   // the large-sweep cap (or ATZ_MW)
   if (int r = c->d_tmp.reserve(4096)) return r;   // zero-length "file" for the compare side
-  const uint64_t budget = ROUND_BUDGET_BYTES;
+  const uint64_t budget = cap_bytes(ROUND_BUDGET_BYTES);
   for (size_t s0 = 0; s0 < n;) {
     // a batch: streams until the scratch estimate passes the budget (at least one)
     size_t s1 = s0;
@@ -3387,7 +3399,7 @@ static int deflate_dev(atz_ctx* c, const std::vector<uint64_t>& addr, const std:
     }
     c->chain_off.assign(n, {});
     for (auto& a2 : c->chain_off) a2.fill(~0ull);
-    c->chain_arena.reset(CHAIN_CACHE_CAP);   // the last batch's kernels are done (run_trials synchronised)
+    c->chain_arena.reset(cap_bytes(CHAIN_CACHE_CAP));   // the last batch's kernels are done (run_trials synchronised)
     p->tmp_chains.clear();
     p->chains_next = 0;
     std::vector<std::pair<uint32_t, int>> need;
@@ -4159,7 +4171,7 @@ int atz_inflate_batch(atz_ctx_t* c, const uint8_t* buf, uint64_t len, const uint
       jobs[k].in_off = offs[k]; jobs[k].in_len = lens[k]; jobs[k].out_off = ARENA_OUT; jobs[k].out_cap = ARENA_SLOT;
     }
     std::vector<InfRes> res;
-    const uint64_t arena_cap = std::min<uint64_t>(64ull << 30, std::max<uint64_t>(256ull << 20, n * ARENA_SLOT));
+    const uint64_t arena_cap = cap_bytes(std::min<uint64_t>(64ull << 30, std::max<uint64_t>(256ull << 20, n * ARENA_SLOT)));
     if (int r = run_inflate_jobs(c, c->d_tmp.as<uint8_t>(), nullptr, jobs, res, arena_cap)) return r;
     for (uint64_t k = 0; k < n; k++) { status[k] = res[k].status; consumed[k] = res[k].consumed; produced[k] = res[k].produced; }
     return ATZ_OK;

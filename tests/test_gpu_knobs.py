@@ -22,6 +22,7 @@ the ATZ1 bytes must equal the oracle's (the reference's algorithm, oracle/) for 
                cannot replay are launched before it)
   ATZ_STAGE    0: uploads straight from pageable memory (default: through a pinned staging buffer)
   ATZ_STOPFLAG 0: speculative trials run to their own end (default: a stream's stop ends its later trials)
+  ATZ_CAP_DIV  every device-memory cap divided by this (test_memory_caps_bind_...): the paths past the caps
 """
 import hashlib
 import os
@@ -75,3 +76,33 @@ def test_switch_keeps_the_atz_bytes(sample, env):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().splitlines()[-1] == want
+
+
+CAPS = r"""
+import hashlib, sys
+sys.path.insert(0, %r)
+import antiz_amd
+data = open(sys.argv[1], "rb").read()
+with antiz_amd.Context(chunksize=int(sys.argv[2]), device=0) as c:
+    out, st = c.precompress(data)
+    back = c.reconstruct(out)
+print(st["n_inflate_retries"], int(back == data))
+print(hashlib.sha256(out).hexdigest())
+""" % ROOT
+
+
+@pytest.mark.parametrize("div", ["4096", "1000000000"])
+def test_memory_caps_bind_and_keep_the_atz_bytes(sample, div):
+    """The caps on device memory (scan output arena, bucket cache, replay arena, round and reconstruct
+    batch budgets: atz_accel.cpp cap_bytes) bind only on inputs of tens of GB. Divided down, they bind on
+    this sample: candidates are re-inflated, rounds build their own tables and defer streams, replays go
+    unsaved, reconstruct runs in batches. 1e9 puts every cap at its 4 KiB floor (one stream per round)."""
+    path, want = sample
+    r = subprocess.run([sys.executable, "-c", CAPS, path, "65536"], env=dict(os.environ, ATZ_CAP_DIV=div),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.strip().splitlines()
+    retries, same = (int(v) for v in lines[-2].split())
+    assert lines[-1] == want
+    assert same == 1
+    assert retries > 0   # the scan arena did overflow
