@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, path, chunksize, q, out_path=None):
+def _worker(rank, world, port, path, chunksize, q, out_path=None, backend="gloo"):
     try:
         sys.path.insert(0, ROOT)
         os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -34,7 +34,7 @@ def _worker(rank, world, port, path, chunksize, q, out_path=None):
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(0)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group(backend, rank=rank, world_size=world)
         import antiz_amd
         from antiz_amd import shard
         data = open(path, "rb").read()
@@ -53,12 +53,12 @@ def _worker(rank, world, port, path, chunksize, q, out_path=None):
         q.put((rank, None, 0, 0, 0, repr(e)))
 
 
-def _run(world, path, chunksize, out_path=None):
+def _run(world, path, chunksize, out_path=None, backend="gloo"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, path, chunksize, q, out_path)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, path, chunksize, q, out_path, backend)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -94,6 +94,19 @@ def test_sharded_equals_single_gpu_and_oracle(sample, world, chunksize):
     assert hashlib.sha256(res[0][0]).hexdigest() == hashlib.sha256(one).hexdigest()
     assert sum(v[1] for v in res.values()) == st["n_streams"]     # the ranks' records partition the file's
     assert sum(v[2] for v in res.values()) == st["n_recomp"]
+
+
+def test_sharded_one_rank_over_rccl(sample, tmp_path):
+    """The "nccl" (RCCL) branches of shard.py -- status and blob all-gathers on device tensors -- at one
+    rank: RCCL refuses two ranks on one GPU, so this is as far as the one-GPU box goes (bench.py runs
+    them at N > 1 on a node)."""
+    path, data = sample
+    rc, ref, _ = _libs.ora_precompress(data, chunksize=524288)
+    assert rc == 0
+    res = _run(1, path, 524288, backend="nccl")
+    assert res[0][0] == ref
+    res = _run(1, path, 524288, out_path=str(tmp_path / "out.atz"), backend="nccl")
+    assert res[0][0] == ref
 
 
 @pytest.fixture(scope="module")
