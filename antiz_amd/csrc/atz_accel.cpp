@@ -197,6 +197,8 @@ struct DevAcct {
     while (v > p && !peak.compare_exchange_weak(p, v)) {}
   }
   void sub(uint64_t n) { cur.fetch_sub(n); }
+  // diagnostics (ATZ_TIMING): allocations / frees and the host time they took (a hipFree waits for the device)
+  std::atomic<uint64_t> n_alloc{0}, n_free{0}, alloc_us{0};
 };
 DevAcct g_dev;
 void dev_mark_call() { g_dev.peak.store(g_dev.cur.load()); }
@@ -307,15 +309,19 @@ struct DBuf {              // device buffer, freed with its owner (atz_close del
   ~DBuf() { release(); }
   int reserve(size_t need) {
     if (need <= n) return 0;
+    const auto t0 = std::chrono::steady_clock::now();
     release();
     size_t cap = need + need / 4 + 65536;
-    if (hipMalloc(&p, cap) != hipSuccess) { p = nullptr; return ATZ_E_NOMEM; }
+    const hipError_t e = hipMalloc(&p, cap);
+    g_dev.n_alloc++;
+    g_dev.alloc_us += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (e != hipSuccess) { p = nullptr; return ATZ_E_NOMEM; }
     n = cap;
     g_dev.add(n);
     return 0;
   }
   void release() {
-    if (p) { hipFree(p); g_dev.sub(n); }
+    if (p) { hipFree(p); g_dev.sub(n); g_dev.n_free++; }
     p = nullptr;
     n = 0;
   }
@@ -331,10 +337,14 @@ struct PinBuf {            // pinned host buffer that kernels write directly
   ~PinBuf() { if (p) (void)hipHostFree(p); }
   int reserve(size_t need) {
     if (need <= n) return 0;
-    if (p) (void)hipHostFree(p);
+    const auto t0 = std::chrono::steady_clock::now();
+    if (p) { (void)hipHostFree(p); g_dev.n_free++; }
     p = nullptr;
     n = 0;
-    if (hipHostMalloc(&p, need, hipHostMallocDefault) != hipSuccess) return ATZ_E_NOMEM;
+    const hipError_t e = hipHostMalloc(&p, need, hipHostMallocDefault);
+    g_dev.n_alloc++;
+    g_dev.alloc_us += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (e != hipSuccess) return ATZ_E_NOMEM;
     n = need;
     return 0;
   }
@@ -3002,6 +3012,8 @@ static int sweep_finish(atz_ctx* c, SweepRun& R) {
   if (timing_on()) {
     std::fprintf(stderr, "atz: sweep host: chains %.1f ms (incl. kernels), trials %.1f ms (incl. kernels), apply %.1f ms, total %.1f ms\n",
                  tch, ttr, tap, ms_since(R.t0));
+    std::fprintf(stderr, "atz: device/pinned allocations so far: %llu allocs, %llu frees, %.1f ms in them\n",
+                 (unsigned long long)g_dev.n_alloc.load(), (unsigned long long)g_dev.n_free.load(), g_dev.alloc_us.load() / 1e3);
     for (size_t g = 0; g < np; g++) {
       Pipe* p = c->pipes[g].get();
       std::fprintf(stderr, "atz: pipe %zu: %llu copy calls %.1f ms, %llu syncs %.1f ms\n", g, (unsigned long long)p->n_copy,
