@@ -83,7 +83,7 @@ import hashlib, sys
 sys.path.insert(0, %r)
 import antiz_amd
 data = open(sys.argv[1], "rb").read()
-with antiz_amd.Context(chunksize=int(sys.argv[2]), device=0) as c:
+with antiz_amd.Context(chunksize=int(sys.argv[2]), device=0, brute_window=sys.argv[3] == "1") as c:
     out, st = c.precompress(data)
     back = c.reconstruct(out)
 print(st["n_inflate_retries"], int(back == data))
@@ -98,7 +98,7 @@ def test_memory_caps_bind_and_keep_the_atz_bytes(sample, div):
     this sample: candidates are re-inflated, rounds build their own tables and defer streams, replays go
     unsaved, reconstruct runs in batches. 1e9 puts every cap at its 4 KiB floor (one stream per round)."""
     path, want = sample
-    r = subprocess.run([sys.executable, "-c", CAPS, path, "65536"], env=dict(os.environ, ATZ_CAP_DIV=div),
+    r = subprocess.run([sys.executable, "-c", CAPS, path, "65536", "0"], env=dict(os.environ, ATZ_CAP_DIV=div),
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = r.stdout.strip().splitlines()
@@ -106,3 +106,27 @@ def test_memory_caps_bind_and_keep_the_atz_bytes(sample, div):
     assert lines[-1] == want
     assert same == 1
     assert retries > 0   # the scan arena did overflow
+
+
+@pytest.fixture(scope="module")
+def sample_c5(tmp_path_factory):
+    from antiz_amd import datagen
+    data = datagen.gen_c5(seed=52, n_streams=400)   # windows 10-15: brute-window phases, sliding windows
+    path = str(tmp_path_factory.mktemp("knobs5") / "c5k.bin")
+    with open(path, "wb") as f:
+        f.write(data)
+    rc, ref, _ = _libs.ora_precompress(data, chunksize=65536, brute=1)
+    assert rc == 0
+    return path, hashlib.sha256(ref).hexdigest()
+
+
+def test_memory_caps_bind_under_brute_window(sample_c5):
+    """The same caps divided down on a --brute-window (C5-like) sample: the brute-window lists (main.cpp:590)
+    run through deferred rounds, per-round tables and unsaved replays."""
+    path, want = sample_c5
+    r = subprocess.run([sys.executable, "-c", CAPS, path, "65536", "1"], env=dict(os.environ, ATZ_CAP_DIV="4096"),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.strip().splitlines()
+    assert lines[-1] == want
+    assert lines[-2].split()[1] == "1"

@@ -109,6 +109,18 @@ def test_sharded_one_rank_over_rccl(sample, tmp_path):
     assert res[0][0] == ref
 
 
+def test_sharded_with_memory_caps_bound(sample, monkeypatch):
+    """Two ranks with every device-memory cap divided down (ATZ_CAP_DIV, inherited by the spawned ranks):
+    the shard scan's arena overflows into re-inflates and the shard sweeps defer streams; rank 0's ATZ1
+    bytes still equal the oracle's."""
+    path, data = sample
+    rc, ref, _ = _libs.ora_precompress(data, chunksize=65536)
+    assert rc == 0
+    monkeypatch.setenv("ATZ_CAP_DIV", "4096")
+    res = _run(2, path, 65536)
+    assert res[0][0] == ref
+
+
 @pytest.fixture(scope="module")
 def clustered(tmp_path_factory):
     """C4 streams followed by a cluster of C3's PNG-like Z_FILTERED streams (they match no trial, so
