@@ -119,7 +119,7 @@ static int search_chunk(searcher *z, const uint8_t *buf, uint64_t len, svec *out
 int ora_scan(const uint8_t *file, uint64_t n, uint64_t cs, ora_result_t *res) {
     memset(res, 0, sizeof(*res));
     if (cs < 2) return -2;              /* reference loops forever at cs==1 (main.cpp:410-415) */
-    if (n == 0) return 0;               /* reference reads rBuffer[-1] (main.cpp:406): UB, report none */
+    if (n == 0) return -21;             /* reference reads rBuffer[-1] (main.cpp:406) and crashes (tests/golden/fuzz_small.json: rc -11): UB, reported as the library does (ATZ_E_REF_UB) */
     svec out = {0};
     searcher z;
     memset(&z, 0, sizeof(z));

@@ -629,3 +629,21 @@ def test_speculative_scan_withdrawal(atz, monkeypatch):
     with atz.Context(chunksize=65536) as c:
         out, st = c.precompress(data)
         assert sha(out) == sha(ref) and st["n_continuations"] > 0
+
+
+def test_fuzz_small_files_vs_oracle(atz):
+    """Seeded random small files (tests/golden_cases.py fuzz_cases) under chunk sizes from 2 bytes up
+    (streams cross chunk boundaries, pending streams refill many times, main.cpp:205-246 and 405-415),
+    default and non-default thresholds: the ATZ1 bytes (or the error code) equal the oracle's, which
+    tests/golden/fuzz_small.json pins to the real reference's; every ATZ1 reconstructs its input."""
+    for i, data, cs, opts in G.fuzz_cases():
+        rc, want, _ = _libs.ora_precompress(data, chunksize=cs, **G.opts_kwargs(opts))
+        with atz.Context(chunksize=cs, **opts) as c:
+            if rc != 0:   # the oracle's reference-UB codes (its own numbering): the library must fail too
+                with pytest.raises(atz.AtzError) as ei:
+                    c.precompress(data)
+                assert ei.value.code == -6, (i, len(data), cs, opts)   # ATZ_E_REF_UB
+                continue
+            got, _ = c.precompress(data)
+            assert got == want, (i, len(data), cs, opts)
+            assert c.reconstruct(got) == data, (i, len(data), cs, opts)

@@ -142,3 +142,23 @@ def test_threshold_grid_near_pins_the_oracle():
                 kw[key] = int(f[f.index(name) + 1])
         rc, atz, _ = _libs.ora_precompress(data, **kw)
         assert rc == 0 and sha(atz) == e["atz_sha256"], f
+
+
+def test_fuzz_small_files_pin_the_oracle():
+    """The seeded fuzz cases (small files, chunk sizes from 2 bytes, threshold variants): the oracle's
+    ATZ1 equals the real reference's (tests/golden/fuzz_small.json, tools/make_fuzz_golden.py) on every
+    case the reference completes; where it crashes (empty input, main.cpp:406 reads rBuffer[-1]) the
+    oracle reports undefined behaviour instead of bytes."""
+    fx = json.load(open(os.path.join(GOLD, "fuzz_small.json")))
+    checked = 0
+    for i, data, cs, opts in G.fuzz_cases():
+        f = fx[str(i)]
+        if sha(data) != f["input_sha256"]:   # another zlib build made different input streams
+            continue
+        rc, atz, _ = _libs.ora_precompress(data, chunksize=cs, **G.opts_kwargs(opts))
+        if "atz_sha256" in f:
+            assert rc == 0 and sha(atz) == f["atz_sha256"], (i, cs, opts)
+        else:
+            assert f["rc"] != 0 and rc != 0, (i, cs, opts, f["rc"], rc)
+        checked += 1
+    assert checked >= 150
