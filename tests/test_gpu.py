@@ -631,12 +631,14 @@ def test_speculative_scan_withdrawal(atz, monkeypatch):
         assert sha(out) == sha(ref) and st["n_continuations"] > 0
 
 
-def test_fuzz_small_files_vs_oracle(atz):
+@pytest.mark.parametrize("n,seed", [(160, 20261018), (800, 7)], ids=["pinned", "wide"])
+def test_fuzz_small_files_vs_oracle(atz, n, seed):
     """Seeded random small files (tests/golden_cases.py fuzz_cases) under chunk sizes from 2 bytes up
     (streams cross chunk boundaries, pending streams refill many times, main.cpp:205-246 and 405-415),
     default and non-default thresholds: the ATZ1 bytes (or the error code) equal the oracle's, which
-    tests/golden/fuzz_small.json pins to the real reference's; every ATZ1 reconstructs its input."""
-    for i, data, cs, opts in G.fuzz_cases():
+    tests/golden/fuzz_small.json pins to the real reference's on the first seed's 160 cases (the wide
+    seed's 800 against the oracle alone; 1 500 passed once, gpurun_out/fuzz); every ATZ1 reconstructs its input."""
+    for i, data, cs, opts in G.fuzz_cases(n, seed):
         rc, want, _ = _libs.ora_precompress(data, chunksize=cs, **G.opts_kwargs(opts))
         with atz.Context(chunksize=cs, **opts) as c:
             if rc != 0:   # the oracle's reference-UB codes (its own numbering): the library must fail too
