@@ -121,6 +121,25 @@ def test_sharded_with_memory_caps_bound(sample, monkeypatch):
     assert res[0][0] == ref
 
 
+@pytest.mark.parametrize("k", range(4))
+def test_sharded_fuzz_files_equal_oracle(k, tmp_path):
+    """Fuzz files (tests/golden_cases.py fuzz_file, 40 of them joined: ~60 KB of streams, noise,
+    truncated streams and bare headers) over three ranks with chunks of 64 B - 4 KiB, so the ranks'
+    chunk ranges split pending streams and refills: rank 0's ATZ1 equals the oracle's."""
+    import random
+    import golden_cases as G
+    r = random.Random(900 + k)
+    data = b"".join(G.fuzz_file(r) for _ in range(40))
+    cs = [64, 257, 1000, 4096][k]
+    rc, ref, _ = _libs.ora_precompress(data, chunksize=cs)
+    assert rc == 0
+    path = str(tmp_path / "fz.bin")
+    with open(path, "wb") as f:
+        f.write(data)
+    res = _run(3, path, cs)
+    assert res[0][0] == ref
+
+
 @pytest.fixture(scope="module")
 def clustered(tmp_path_factory):
     """C4 streams followed by a cluster of C3's PNG-like Z_FILTERED streams (they match no trial, so
