@@ -649,3 +649,44 @@ def test_fuzz_small_files_vs_oracle(atz, n, seed):
             got, _ = c.precompress(data)
             assert got == want, (i, len(data), cs, opts)
             assert c.reconstruct(got) == data, (i, len(data), cs, opts)
+
+
+def test_reconstruct_fuzzed_atz_rejected_or_equal_to_oracle(atz):
+    """ATZ1 files are untrusted input: seeded single-byte mutations and truncations of valid files
+    (fuzz cases with streams and diffs) must either be refused with AtzError or reconstruct exactly what
+    the oracle's ATZ1 reader (the reference's reconstructATZ restated) makes of them -- never a crash.
+    Mutations land mostly in the header and the stream descriptors (offsets, lengths, parameters, diff
+    lists), the rest in the payloads."""
+    import struct
+    r = random.Random(4242)
+    files = []
+    for i, data, cs, opts in G.fuzz_cases(400, 99):
+        if len(files) == 30:
+            break
+        rc, want, st = _libs.ora_precompress(data, chunksize=cs, **G.opts_kwargs(opts))
+        if rc == 0 and len(want) > 40 and st["streams"]:
+            files.append((data, want, opts))
+    assert len(files) >= 20
+    accepted = refused = 0
+    with atz.Context() as c:
+        for data, good, opts in files:
+            assert c.reconstruct(good) == data
+            for _ in range(25):
+                b = bytearray(good)
+                if r.random() < 0.15:
+                    b = b[:r.randrange(28, len(b))]
+                    b[4:12] = struct.pack("<Q", len(b))   # keep the length field consistent
+                else:
+                    hi = min(len(b), 28 + 43 * 3) if r.random() < 0.8 else len(b)
+                    at = r.randrange(12, hi)             # past the magic and the length field
+                    b[at] = r.randrange(256) if r.random() < 0.5 else b[at] ^ (1 << r.randrange(8))
+                b = bytes(b)
+                try:
+                    got = c.reconstruct(b)
+                except atz.AtzError:
+                    refused += 1
+                    continue
+                rc, want = _libs.ora_reconstruct(b)   # only files the library accepted reach the oracle
+                assert rc == 0 and got == want
+                accepted += 1
+    assert accepted > 0 and refused > 0
